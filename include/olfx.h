@@ -1,0 +1,182 @@
+/*
+ * include/olfx.h -- C-ABI of the MI355X bulk audio-effect engine (libolfx.so).
+ *
+ * One engine = one effect kind x N independent instances on one GPU.  Every call processes a
+ * block of frames for ALL instances at once on a HIP stream; per-instance parameters and note
+ * events are applied at the next block boundary (the JUCE-host pattern, reference
+ * modules/juce/host/host.cpp:646-653).  No torch types, plain pointers and sizes only.
+ *
+ * What each entry point replaces in the reference (/root/reference):
+ *   olfx_create / olfx_destroy  <- DattorroVerb_create / _delete (libs/dattorro-verb/verb.h:5-8,
+ *                                  verb.cpp:225-251); fxlib XxxFx::Init(sr) (modules/fxlib/Fx.h:183,
+ *                                  :290); SynthVoice::Init(sr) (modules/synthlib/SynthVoice.h:31-39);
+ *                                  README ChorusEffect::init(sr) (README.md:117-127)
+ *   olfx_set_params             <- DattorroVerb_set* (verb.h:10-16, verb.cpp:137-170);
+ *                                  ChorusEffect::setDepth/setRate (README.md:120-121) and the RNBO
+ *                                  chorus params (modules/rnbo/patcher/mono-chorus.rnbopat:431-4353);
+ *                                  SynthVoice::UpdateConfig/Update (SynthVoice.h:55-98)
+ *   olfx_note_events            <- SynthVoice::NoteOn/NoteOff (SynthVoice.h:245-256)
+ *   olfx_process                <- the per-frame loops DattorroVerb_process + getLeft/getRight
+ *                                  (verb.cpp:258-325), ReverbFx glue (modules/fxlib/ReverbFx.cpp:11-27),
+ *                                  ChorusEffect::process(sample) (README.md:124), SynthVoice::Process
+ *                                  (SynthVoice.h:41-53) -- batched: n_frames x n_inst per call
+ *   olfx_last_error             <- (reference has none: void returns / NULL, verb.cpp:89-90,227)
+ *
+ * Audio layout (both host and device pointers accepted, see OLFX_IO_*):
+ *   in  : [in_channels ][n_frames][n_inst]  float32, instance index fastest
+ *   out : [out_channels][n_frames][n_inst]  float32
+ * Channel counts per kind are given by olfx_kind_info().
+ *
+ * Errors: every function returns 0 on success or a negative OLFX_E_* code; no C++ exception
+ * crosses this boundary.  An engine is not re-entrant: one host thread drives one engine.
+ */
+#ifndef OLFX_H
+#define OLFX_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OLFX_ABI_VERSION 1
+
+/* ---- status codes ---- */
+enum {
+    OLFX_OK          = 0,
+    OLFX_E_ARG       = -1,   /* bad argument (null, out of range, wrong size) */
+    OLFX_E_NOMEM     = -2,   /* host or device allocation failed */
+    OLFX_E_HIP       = -3,   /* a HIP runtime call failed; see olfx_last_error */
+    OLFX_E_NODEVICE  = -4,   /* no GPU / device index invalid */
+    OLFX_E_KIND      = -5,   /* unknown effect kind */
+    OLFX_E_STATE     = -6    /* call not valid in the engine's current state */
+};
+
+/* ---- effect kinds ---- */
+enum {
+    OLFX_KIND_DATTORRO   = 1,  /* libs/dattorro-verb: stereo in -> (l+r)/2 -> stereo out (ReverbFx.cpp:11-27),
+                                  or mono in (verb.h:19) */
+    OLFX_KIND_CHORUS     = 2,  /* RNBO stereo-chorus (mono-chorus x2, shared params) */
+    OLFX_KIND_PITCHSHIFT = 3,  /* gen~ pitchshift, stereo */
+    OLFX_KIND_VOICE      = 4,  /* synthlib SynthVoice: polyBLEP saw -> SVF LP (env cutoff) -> amp env; mono out */
+    OLFX_KIND_CHAIN      = 5   /* fused chorus -> pitch-shift -> dattorro, stereo */
+};
+
+/* ---- parameters (field index, value is what the reference setter takes) ---- */
+/* Dattorro: verb.h:10-16 */
+enum {
+    OLFX_DT_PREDELAY = 0,        /* [0,1] x 4800 samples; ENGINE-WIDE (uniform taps keep rings coalesced) */
+    OLFX_DT_PREFILTER,           /* setPreFilter */
+    OLFX_DT_INPUT_DIFFUSION1,    /* setInputDiffusion1 */
+    OLFX_DT_INPUT_DIFFUSION2,    /* setInputDiffusion2 */
+    OLFX_DT_DECAY_DIFFUSION,     /* setDecayDiffusion */
+    OLFX_DT_DECAY,               /* setDecay (also derives decay diffusion 2, verb.cpp:164) */
+    OLFX_DT_DAMPING,             /* setDamping */
+    OLFX_DT_NPARAMS
+};
+/* Chorus (RNBO params, clamped to @min/@max like RNBO; mono-chorus.rnbopat line of each param) */
+enum {
+    OLFX_CH_PITCH = 0,   /* [0,3]      default 0    :431   pitch-shifter phasor rate, Hz */
+    OLFX_CH_MIX,         /* [0,1]      default 0.5  :1772 */
+    OLFX_CH_Q,           /* [0,1]      default 0.5  :2226  lores~ resonance */
+    OLFX_CH_CUTOFF,      /* [0,1]      default 0.3  :2660  -> 300..15000 Hz (:2242) */
+    OLFX_CH_PHASE,       /* [0,1]      default 1    :3420  cycle~ phase offset */
+    OLFX_CH_DEPTH,       /* [0.08,1]   default 0.5  :3854  -> 1..12 ms (:3436) */
+    OLFX_CH_RATE,        /* [0.01,1]   default 0.2  :4353  -> 0.01..0.5 Hz (:3935) */
+    OLFX_CH_WINDOW,      /* [4,10] ms  default 10   pitchshift.gendsp "Param window" */
+    OLFX_CH_NPARAMS
+};
+/* Pitch-shift stage (gen~ pitchshift.gendsp) */
+enum {
+    OLFX_PS_SHIFT = 0,   /* [0,3] Hz phasor rate (inlet 2 of pitchshift.gendsp) */
+    OLFX_PS_WINDOW,      /* [4,10] ms */
+    OLFX_PS_NPARAMS
+};
+/* Voice: Voice::Config field order (modules/synthlib/Voice.h:14-31) */
+enum {
+    OLFX_VC_FILTER_CUTOFF = 0, OLFX_VC_FILTER_RESONANCE, OLFX_VC_FILTER_DRIVE, OLFX_VC_FILTER_ENV_AMOUNT,
+    OLFX_VC_FILTER_ATTACK, OLFX_VC_FILTER_ATTACK_SHAPE, OLFX_VC_FILTER_DECAY, OLFX_VC_FILTER_SUSTAIN,
+    OLFX_VC_FILTER_RELEASE, OLFX_VC_AMP_ENV_AMOUNT, OLFX_VC_AMP_ATTACK, OLFX_VC_AMP_ATTACK_SHAPE,
+    OLFX_VC_AMP_DECAY, OLFX_VC_AMP_SUSTAIN, OLFX_VC_AMP_RELEASE, OLFX_VC_PORTAMENTO,
+    OLFX_VC_NPARAMS
+};
+/* Chain: chorus params, then pitch-shift params, then dattorro params */
+#define OLFX_CN_CHORUS0   0
+#define OLFX_CN_PITCH0    (OLFX_CH_NPARAMS)
+#define OLFX_CN_VERB0     (OLFX_CH_NPARAMS + OLFX_PS_NPARAMS)
+#define OLFX_CN_NPARAMS   (OLFX_CH_NPARAMS + OLFX_PS_NPARAMS + OLFX_DT_NPARAMS)
+
+/* ---- note events (voices) ---- */
+enum { OLFX_EV_NOTE_OFF = 0, OLFX_EV_NOTE_ON = 1 };
+typedef struct olfx_event {
+    uint32_t inst;      /* instance index */
+    uint8_t  type;      /* OLFX_EV_* */
+    uint8_t  note;      /* MIDI note (NoteOn: freq = mtof(note)) */
+    uint8_t  velocity;  /* unused by SynthVoice (SynthVoice.h:245) */
+    uint8_t  pad;
+} olfx_event;
+
+/* ---- I/O flags ---- */
+enum {
+    OLFX_IO_DEVICE = 0,  /* in/out are device pointers (no copies; the fast path) */
+    OLFX_IO_HOST   = 1   /* in/out are host pointers: staged through pinned buffers, PCIe-inclusive */
+};
+
+typedef struct olfx_engine olfx_engine;
+
+typedef struct olfx_kind_info {
+    int      kind;
+    uint32_t n_params;
+    uint32_t in_channels;       /* channels olfx_process reads */
+    uint32_t out_channels;      /* channels olfx_process writes */
+    uint64_t state_bytes_per_instance;   /* device state (rings + scalars + params) */
+} olfx_kind_info;
+
+int olfx_abi_version(void);
+int olfx_kind_info_get(int kind, float sample_rate, olfx_kind_info *info);
+
+/* Create an engine of `kind` with n_inst instances on HIP device `device`.  All instances start
+   in the reference's freshly-created state (zeroed rings, default parameters).
+   block = the frames per olfx_process call the caller intends (any multiple of 4 is accepted). */
+int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32_t block,
+                olfx_engine **out);
+int olfx_destroy(olfx_engine *e);
+
+/* Zero all state and restore defaults (== destroy + create, without reallocating). */
+int olfx_reset(olfx_engine *e);
+
+/* Set parameters of instances [first, first+count): `values` is field-major
+   [n_fields][count] for fields [field0, field0+n_fields).  Host pointer.  Applied at the start
+   of the next olfx_process. */
+int olfx_set_params(olfx_engine *e, uint32_t first, uint32_t count, uint32_t field0,
+                    uint32_t n_fields, const float *values);
+/* Convenience: one field of one instance. */
+int olfx_set_param(olfx_engine *e, uint32_t inst, uint32_t field, float value);
+/* Read back the current (host shadow) value of one parameter. */
+int olfx_get_param(olfx_engine *e, uint32_t inst, uint32_t field, float *value);
+
+/* Queue note events (voices); applied in order at the start of the next olfx_process. */
+int olfx_note_events(olfx_engine *e, const olfx_event *ev, uint32_t n);
+
+/* Process n_frames (multiple of 4) for all instances.  `stream` is a hipStream_t (NULL = the
+   engine's own stream).  With OLFX_IO_DEVICE the call is asynchronous on that stream. */
+int olfx_process(olfx_engine *e, const float *in, float *out, uint32_t n_frames, int io_flags,
+                 void *stream);
+
+/* Block until all work queued by this engine is done. */
+int olfx_sync(olfx_engine *e);
+
+/* Engine facts. */
+uint32_t olfx_num_instances(const olfx_engine *e);
+int      olfx_kind(const olfx_engine *e);
+uint64_t olfx_frames_processed(const olfx_engine *e);   /* per instance, since create/reset */
+/* Algorithmic ("compulsory") HBM bytes per instance-frame of the dominant kernel, the figure
+   bench.py's roofline uses. */
+double   olfx_algorithmic_bytes_per_frame(const olfx_engine *e);
+const char *olfx_kernel_name(const olfx_engine *e);
+const char *olfx_last_error(const olfx_engine *e);   /* e may be NULL: last global error */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OLFX_H */

@@ -1,0 +1,113 @@
+"""ctypes binding of libolfx.so (include/olfx.h).
+
+This is the Python mirror of the C-ABI a maintainer would bind from the reference side
+(INTEGRATION.md).  It loads the in-tree ``ol_dsp_amd/libolfx.so`` and fails loudly if it is
+missing: there is no CPU fallback anywhere in the product.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libolfx.so")
+
+# status codes (olfx.h)
+OLFX_OK = 0
+OLFX_E_ARG = -1
+OLFX_E_NOMEM = -2
+OLFX_E_HIP = -3
+OLFX_E_NODEVICE = -4
+OLFX_E_KIND = -5
+OLFX_E_STATE = -6
+
+# kinds
+KIND_DATTORRO = 1
+KIND_CHORUS = 2
+KIND_PITCHSHIFT = 3
+KIND_VOICE = 4
+KIND_CHAIN = 5
+
+IO_DEVICE = 0
+IO_HOST = 1
+
+EV_NOTE_OFF = 0
+EV_NOTE_ON = 1
+
+
+class OlfxError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"olfx error {code}: {msg}")
+        self.code = code
+
+
+class KindInfo(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int),
+        ("n_params", ctypes.c_uint32),
+        ("in_channels", ctypes.c_uint32),
+        ("out_channels", ctypes.c_uint32),
+        ("state_bytes_per_instance", ctypes.c_uint64),
+    ]
+
+
+class Event(ctypes.Structure):
+    _fields_ = [
+        ("inst", ctypes.c_uint32),
+        ("type", ctypes.c_uint8),
+        ("note", ctypes.c_uint8),
+        ("velocity", ctypes.c_uint8),
+        ("pad", ctypes.c_uint8),
+    ]
+
+
+# every symbol include/olfx.h declares, with (restype, argtypes)
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_F = ctypes.c_float
+SIGNATURES = {
+    "olfx_abi_version": (ctypes.c_int, []),
+    "olfx_kind_info_get": (ctypes.c_int, [ctypes.c_int, _F, ctypes.POINTER(KindInfo)]),
+    "olfx_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _U32, _F, _U32, ctypes.POINTER(_P)]),
+    "olfx_destroy": (ctypes.c_int, [_P]),
+    "olfx_reset": (ctypes.c_int, [_P]),
+    "olfx_set_params": (ctypes.c_int, [_P, _U32, _U32, _U32, _U32, ctypes.POINTER(_F)]),
+    "olfx_set_param": (ctypes.c_int, [_P, _U32, _U32, _F]),
+    "olfx_get_param": (ctypes.c_int, [_P, _U32, _U32, ctypes.POINTER(_F)]),
+    "olfx_note_events": (ctypes.c_int, [_P, ctypes.POINTER(Event), _U32]),
+    "olfx_process": (ctypes.c_int, [_P, _P, _P, _U32, ctypes.c_int, _P]),
+    "olfx_sync": (ctypes.c_int, [_P]),
+    "olfx_num_instances": (_U32, [_P]),
+    "olfx_kind": (ctypes.c_int, [_P]),
+    "olfx_frames_processed": (ctypes.c_uint64, [_P]),
+    "olfx_algorithmic_bytes_per_frame": (ctypes.c_double, [_P]),
+    "olfx_kernel_name": (ctypes.c_char_p, [_P]),
+    "olfx_last_error": (ctypes.c_char_p, [_P]),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libolfx.so (once).  Raises if the HIP library has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(make -C ol_dsp_amd/csrc).  There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, handle=None) -> None:
+    if rc != OLFX_OK:
+        lib = load()
+        msg = lib.olfx_last_error(handle)
+        raise OlfxError(rc, msg.decode() if msg else "")

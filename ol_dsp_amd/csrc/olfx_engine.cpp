@@ -1,0 +1,861 @@
+// ol_dsp_amd/csrc/olfx_engine.cpp -- host side of libolfx.so: the C-ABI of include/olfx.h.
+//
+// Owns all device state of an engine (SoA rings, recursive scalars, derived coefficients),
+// derives per-instance coefficients from the reference's setter semantics on the host (control
+// rate), applies parameter changes / note events at block boundaries, and launches the gfx950
+// kernels on a HIP stream.  There is no CPU compute path: if no GPU is present olfx_create
+// fails with OLFX_E_NODEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/olfx.h"
+#include "olfx_internal.h"
+
+using namespace olfx;
+
+namespace {
+
+std::mutex g_err_mu;
+std::string g_err;
+
+void set_global_error(const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    g_err = buf;
+}
+
+uint32_t pow2_at_least(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+uint32_t phase_inc_u32(double hz, double sr) {
+    double v = std::floor(hz / sr * 4294967296.0 + 0.5);
+    if (v < 0) v = 0;
+    return (uint32_t)(uint64_t)v;
+}
+
+uint32_t as_u32(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Per-kind constants
+// ---------------------------------------------------------------------------------------------
+uint32_t n_params_of(int kind) {
+    switch (kind) {
+    case OLFX_KIND_DATTORRO: return OLFX_DT_NPARAMS;
+    case OLFX_KIND_CHORUS: return OLFX_CH_NPARAMS;
+    case OLFX_KIND_PITCHSHIFT: return OLFX_PS_NPARAMS;
+    case OLFX_KIND_VOICE: return OLFX_VC_NPARAMS;
+    case OLFX_KIND_CHAIN: return OLFX_CN_NPARAMS;
+    default: return 0;
+    }
+}
+
+// Reference defaults of the user-facing parameters.
+void default_params(int kind, float *p) {
+    switch (kind) {
+    case OLFX_KIND_DATTORRO:
+        // verb.cpp:215-221
+        p[OLFX_DT_PREDELAY] = (float)0.1;
+        p[OLFX_DT_PREFILTER] = (float)0.85;
+        p[OLFX_DT_INPUT_DIFFUSION1] = (float)0.75;
+        p[OLFX_DT_INPUT_DIFFUSION2] = (float)0.625;
+        p[OLFX_DT_DECAY_DIFFUSION] = (float)0.70;
+        p[OLFX_DT_DECAY] = (float)0.75;
+        p[OLFX_DT_DAMPING] = (float)0.95;
+        break;
+    case OLFX_KIND_CHORUS:
+        // mono-chorus.rnbopat param boxes (:431,1772,2226,2660,3420,3854,4353)
+        p[OLFX_CH_PITCH] = 0.0f;
+        p[OLFX_CH_MIX] = 0.5f;
+        p[OLFX_CH_Q] = 0.5f;
+        p[OLFX_CH_CUTOFF] = 0.3f;
+        p[OLFX_CH_PHASE] = 1.0f;
+        p[OLFX_CH_DEPTH] = 0.5f;
+        p[OLFX_CH_RATE] = 0.2f;
+        p[OLFX_CH_WINDOW] = 10.0f;
+        break;
+    case OLFX_KIND_PITCHSHIFT:
+        p[OLFX_PS_SHIFT] = 0.0f;
+        p[OLFX_PS_WINDOW] = 10.0f;
+        break;
+    case OLFX_KIND_VOICE:
+        // SynthVoice member defaults (SynthVoice.h:285-311); Config order (Voice.h:14-31)
+        p[OLFX_VC_FILTER_CUTOFF] = 0.0f;
+        p[OLFX_VC_FILTER_RESONANCE] = 0.0f;
+        p[OLFX_VC_FILTER_DRIVE] = 0.0f;
+        p[OLFX_VC_FILTER_ENV_AMOUNT] = 1.0f;
+        p[OLFX_VC_FILTER_ATTACK] = 0.0f;
+        p[OLFX_VC_FILTER_ATTACK_SHAPE] = 1.0f;
+        p[OLFX_VC_FILTER_DECAY] = 0.2f;
+        p[OLFX_VC_FILTER_SUSTAIN] = 0.0f;
+        p[OLFX_VC_FILTER_RELEASE] = 0.0f;
+        p[OLFX_VC_AMP_ENV_AMOUNT] = 0.8f;
+        p[OLFX_VC_AMP_ATTACK] = 0.01f;
+        p[OLFX_VC_AMP_ATTACK_SHAPE] = 1.0f;
+        p[OLFX_VC_AMP_DECAY] = 0.0f;
+        p[OLFX_VC_AMP_SUSTAIN] = 1.0f;
+        p[OLFX_VC_AMP_RELEASE] = 0.01f;
+        p[OLFX_VC_PORTAMENTO] = 0.0f;
+        break;
+    case OLFX_KIND_CHAIN:
+        default_params(OLFX_KIND_CHORUS, p + OLFX_CN_CHORUS0);
+        default_params(OLFX_KIND_PITCHSHIFT, p + OLFX_CN_PITCH0);
+        default_params(OLFX_KIND_DATTORRO, p + OLFX_CN_VERB0);
+        break;
+    default: break;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Coefficient derivation (control rate, host).  These restate the reference setters.
+// ---------------------------------------------------------------------------------------------
+void derive_dattorro(const float *p, float *c) {
+    c[DTC_PREFILTER] = p[OLFX_DT_PREFILTER];
+    c[DTC_IN1] = p[OLFX_DT_INPUT_DIFFUSION1];
+    c[DTC_IN2] = p[OLFX_DT_INPUT_DIFFUSION2];
+    c[DTC_DD1] = p[OLFX_DT_DECAY_DIFFUSION];
+    c[DTC_DAMPING] = p[OLFX_DT_DAMPING];
+    c[DTC_DECAY] = p[OLFX_DT_DECAY];
+    // verb.cpp:49,162-165: clamp(t_sample x, ...) narrows value+0.15 to float
+    float x = (float)((double)p[OLFX_DT_DECAY] + 0.15);
+    c[DTC_DD2] = x < 0.25f ? 0.25f : (x > 0.5f ? 0.5f : x);
+}
+
+uint32_t dattorro_predelay_samples(float v) {
+    // verb.cpp:137-139: uint16(value * 4800.f); the engine accepts [0, 1]
+    float d = v * 4800.0f;
+    return d <= 0.0f ? 0u : (uint32_t)(uint16_t)d;
+}
+
+// chorus: p = [OLFX_CH_*], c = [CHC_*] (u32 words)
+void derive_chorus(const float *p, double sr, uint32_t *c) {
+    const double pitch = clampf(p[OLFX_CH_PITCH], 0.0f, 3.0f);
+    const double mix = clampf(p[OLFX_CH_MIX], 0.0f, 1.0f);
+    const double q = clampf(p[OLFX_CH_Q], 0.0f, 1.0f);
+    const double cutoff = clampf(p[OLFX_CH_CUTOFF], 0.0f, 1.0f);
+    const double phase = clampf(p[OLFX_CH_PHASE], 0.0f, 1.0f);
+    const double depth = clampf(p[OLFX_CH_DEPTH], 0.08f, 1.0f);
+    const double rate = clampf(p[OLFX_CH_RATE], 0.01f, 1.0f);
+    const double window = clampf(p[OLFX_CH_WINDOW], 4.0f, 10.0f);
+
+    const double rate_hz = 0.01 + rate * (0.5 - 0.01);           // scale 0 1 0.01 0.5 (:3935)
+    const double depth_ms = 1.0 + depth * (12.0 - 1.0);          // scale 0 1 1 12 1   (:3436)
+    const double fc = 300.0 + cutoff * (15000.0 - 300.0);         // scale 0 1 300 15000 1 (:2242)
+    c[CHC_LFO_INC] = phase_inc_u32(rate_hz, sr);
+    c[CHC_LFO_OFF] = (uint32_t)(uint64_t)std::floor(phase * 4294967296.0 + 0.5);  // 1.0 wraps to 0
+    c[CHC_PS_INC] = phase_inc_u32(pitch, sr);
+    c[CHC_DEPTH] = as_u32((float)(depth_ms * sr / 1000.0));       // mstosamps (:3897)
+    c[CHC_WINDOW] = as_u32((float)(window * sr / 1000.0));        // mstosamps(window)
+    // lores~ -> RBJ biquad low-pass, Q = 1/sqrt(2) + 20 q^3 (declared)
+    const double Q = 0.70710678118654752 + 20.0 * q * q * q;
+    const double w0 = 2.0 * 3.14159265358979323846 * fc / sr;
+    const double cw = std::cos(w0), sw = std::sin(w0);
+    const double alpha = sw / (2.0 * Q);
+    const double a0 = 1.0 + alpha;
+    c[CHC_B0] = as_u32((float)((1.0 - cw) * 0.5 / a0));
+    c[CHC_B1] = as_u32((float)((1.0 - cw) / a0));
+    c[CHC_B2] = as_u32((float)((1.0 - cw) * 0.5 / a0));
+    c[CHC_A1] = as_u32((float)(-2.0 * cw / a0));
+    c[CHC_A2] = as_u32((float)((1.0 - alpha) / a0));
+    const float mixf = (float)mix;
+    c[CHC_MIX] = as_u32(mixf);
+    c[CHC_DRY] = as_u32(1.0f - mixf);                             // !- 1 (:1176)
+}
+
+// pitch-shift stage only: reuse the chorus coefficient block (mode 1 ignores the rest)
+void derive_pitchshift(const float *p, double sr, uint32_t *c) {
+    float cp[OLFX_CH_NPARAMS];
+    default_params(OLFX_KIND_CHORUS, cp);
+    cp[OLFX_CH_PITCH] = p[OLFX_PS_SHIFT];
+    cp[OLFX_CH_WINDOW] = p[OLFX_PS_WINDOW];
+    derive_chorus(cp, sr, c);
+}
+
+// DaisySP Adsr coefficient setters (restated; DaisySP is absent from the reference tree, see
+// DESIGN.md "parity unpinned"): SetAttackTime / SetTimeConstant.
+float adsr_attack_d0(float T, float shape, float sr, float *target_out) {
+    float target = 9.f * powf(shape, 10.f) + 0.3f * shape + 1.01f;
+    *target_out = target;
+    if (T > 0.f) {
+        float logTarget = logf(1.f - (1.f / target));
+        return 1.f - expf(logTarget / (T * sr));
+    }
+    return 1.f;
+}
+float adsr_time_d0(float T, float sr) {
+    if (T > 0.f) {
+        const float target = logf((float)(1. / M_E));
+        return 1.f - expf(target / (T * sr));
+    }
+    return 1.f;
+}
+float adsr_sustain(float s) { return (s <= 0.f) ? -0.01f : (s > 1.f ? 1.f : s); }
+
+// Voice: `configured` = false reproduces SynthVoice::Init without any Update()
+// (SynthVoice.h:31-39): DaisySP Init defaults in the envelopes and the Svf.
+void derive_voice(const float *p, bool configured, float sr, float *c) {
+    float tgt;
+    if (!configured) {
+        // daisysp::Adsr::Init: attack 0.1 s shape 0, decay 0.1 s, release 0.1 s, sustain 0.7
+        c[VCC_ATK_D0A] = adsr_attack_d0(0.1f, 0.0f, sr, &tgt); c[VCC_ATK_TGT_A] = tgt;
+        c[VCC_DEC_D0A] = adsr_time_d0(0.1f, sr);
+        c[VCC_REL_D0A] = adsr_time_d0(0.1f, sr);
+        c[VCC_SUS_A] = 0.7f;
+        c[VCC_ATK_D0F] = c[VCC_ATK_D0A]; c[VCC_ATK_TGT_F] = tgt;
+        c[VCC_DEC_D0F] = c[VCC_DEC_D0A];
+        c[VCC_REL_D0F] = c[VCC_REL_D0A];
+        c[VCC_SUS_F] = 0.7f;
+        // daisysp::Svf::Init: res 0.5, drive 0.5
+        c[VCC_DAMP_RES] = 2.0f * (1.0f - powf(0.5f, 0.25f));
+        c[VCC_DRIVE] = 0.5f;
+    } else {
+        c[VCC_ATK_D0A] = adsr_attack_d0(p[OLFX_VC_AMP_ATTACK], p[OLFX_VC_AMP_ATTACK_SHAPE], sr, &tgt);
+        c[VCC_ATK_TGT_A] = tgt;
+        c[VCC_DEC_D0A] = adsr_time_d0(p[OLFX_VC_AMP_DECAY], sr);
+        c[VCC_REL_D0A] = adsr_time_d0(p[OLFX_VC_AMP_RELEASE], sr);
+        c[VCC_SUS_A] = adsr_sustain(p[OLFX_VC_AMP_SUSTAIN]);
+        c[VCC_ATK_D0F] = adsr_attack_d0(p[OLFX_VC_FILTER_ATTACK], p[OLFX_VC_FILTER_ATTACK_SHAPE], sr, &tgt);
+        c[VCC_ATK_TGT_F] = tgt;
+        c[VCC_DEC_D0F] = adsr_time_d0(p[OLFX_VC_FILTER_DECAY], sr);
+        c[VCC_REL_D0F] = adsr_time_d0(p[OLFX_VC_FILTER_RELEASE], sr);
+        c[VCC_SUS_F] = adsr_sustain(p[OLFX_VC_FILTER_SUSTAIN]);
+        // Svf::SetRes then Svf::SetDrive (SynthVoice::Update, SynthVoice.h:82-83)
+        float res = fminf(fmaxf(p[OLFX_VC_FILTER_RESONANCE], 0.f), 1.f);
+        float pre_drive = fminf(fmaxf(p[OLFX_VC_FILTER_DRIVE] * 0.1f, 0.f), 1.f);
+        c[VCC_DAMP_RES] = 2.0f * (1.0f - powf(res, 0.25f));
+        c[VCC_DRIVE] = pre_drive * res;
+    }
+    c[VCC_AMP_AMT] = p[OLFX_VC_AMP_ENV_AMOUNT];
+    c[VCC_CUTOFF] = p[OLFX_VC_FILTER_CUTOFF];
+    c[VCC_FENV_AMT] = p[OLFX_VC_FILTER_ENV_AMOUNT];
+    // daisysp::Port (in-tree stub, Portamento.h:223-226); Init happens with htime 0 and
+    // SetHtime(portamento) on Update
+    float htime = configured ? p[OLFX_VC_PORTAMENTO] : 0.0f;
+    c[VCC_PORT_COEF] = expf(-1.0f / (htime * sr));
+    c[VCC_FC_MAX] = sr / 3.f;
+    c[VCC_SR] = sr;
+    c[VCC_INV_SR] = 1.0f / sr;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// Engine
+// ---------------------------------------------------------------------------------------------
+struct olfx_engine {
+    int kind = 0;
+    int device = 0;
+    uint32_t n = 0;
+    uint32_t block = 0;
+    float sr = 48000.f;
+    hipStream_t stream = nullptr;
+    uint64_t frames = 0;
+    std::string err;
+
+    // user parameters [n_params][n] (host shadow) and device coefficient blocks
+    uint32_t n_params = 0;
+    std::vector<float> params;
+    std::vector<uint8_t> configured;     // voice: UpdateConfig seen
+    bool dirty = true;
+
+    // device memory: one allocation per engine, carved
+    void *d_mem = nullptr;
+    size_t d_bytes = 0;
+
+    // dattorro (also the chain's reverb stage)
+    float *dt_rings = nullptr;
+    float *dt_state = nullptr;
+    float *dt_coef = nullptr;
+    uint32_t dt_predelay = 480;
+
+    // chorus / pitch-shift (also the chain's first two stages)
+    uint32_t psize = 0, csize = 0;
+    float *ch_pring = nullptr, *ch_cring = nullptr;
+    uint32_t *ch_state = nullptr, *ch_coef = nullptr;
+    float *ps_pring = nullptr, *ps_cring = nullptr;      // chain stage 2
+    uint32_t *ps_state = nullptr, *ps_coef = nullptr;
+    float *chain_tmp = nullptr;                          // chain intermediates [2][2][block][n]
+    uint32_t chain_tmp_frames = 0;
+
+    // voice
+    float *vc_state = nullptr, *vc_coef = nullptr;
+    std::vector<olfx_event> events;
+    std::vector<float> h_vstate;                         // host copy for event application
+
+    // host-pointer I/O staging
+    float *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+    size_t stage_floats_in = 0, stage_floats_out = 0;
+
+    int fail(int code, const char *fmt, ...) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        set_global_error("%s", buf);
+        return code;
+    }
+    int hip_fail(hipError_t e, const char *what) {
+        return fail(OLFX_E_HIP, "%s: %s", what, hipGetErrorString(e));
+    }
+};
+
+#define HIPCHK(e, call)                                          \
+    do {                                                         \
+        hipError_t _r = (call);                                  \
+        if (_r != hipSuccess) return (e)->hip_fail(_r, #call);   \
+    } while (0)
+
+namespace {
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct Carve {
+    size_t off = 0;
+    size_t take(size_t bytes) {
+        size_t o = off;
+        off = align_up(off + bytes, 256);
+        return o;
+    }
+};
+
+void chorus_sizes(float sr, uint32_t *psize, uint32_t *csize) {
+    // pitch ring: delays up to W = 10 ms plus the interpolation neighbour
+    *psize = pow2_at_least((uint32_t)std::ceil(10.0 * sr / 1000.0) + 2);
+    // chorus ring: delays up to 2 D, D <= 12 ms (delay~ @maxsize samplerate*2 is never reached)
+    *csize = pow2_at_least(2u * (uint32_t)std::ceil(12.0 * sr / 1000.0) + 2);
+}
+
+uint64_t state_bytes(int kind, uint32_t n, float sr) {
+    uint32_t ps, cs;
+    chorus_sizes(sr, &ps, &cs);
+    const uint64_t dt = (uint64_t)dt_total_floats() * 4 + DTS_N * 4 + DTC_N * 4;
+    const uint64_t ch = (uint64_t)2 * (ps + cs) * 4 + CHS_N * 4 + CHC_N * 4;
+    const uint64_t vc = (uint64_t)VCS_N * 4 + VCC_N * 4;
+    switch (kind) {
+    case OLFX_KIND_DATTORRO: return dt * n;
+    case OLFX_KIND_CHORUS:
+    case OLFX_KIND_PITCHSHIFT: return ch * n;
+    case OLFX_KIND_VOICE: return vc * n;
+    case OLFX_KIND_CHAIN: return (dt + 2 * ch) * n;
+    default: return 0;
+    }
+}
+
+int upload_params(olfx_engine *e, hipStream_t s) {
+    if (!e->dirty) return OLFX_OK;
+    const uint32_t n = e->n, np = e->n_params;
+    std::vector<float> p(np);
+    auto gather = [&](uint32_t i) {
+        for (uint32_t f = 0; f < np; ++f) p[f] = e->params[(size_t)f * n + i];
+    };
+    if (e->kind == OLFX_KIND_DATTORRO || e->kind == OLFX_KIND_CHAIN) {
+        const uint32_t base = e->kind == OLFX_KIND_CHAIN ? OLFX_CN_VERB0 : 0;
+        std::vector<float> c((size_t)DTC_N * n);
+        float cc[DTC_N];
+        for (uint32_t i = 0; i < n; ++i) {
+            gather(i);
+            derive_dattorro(p.data() + base, cc);
+            for (int k = 0; k < DTC_N; ++k) c[(size_t)k * n + i] = cc[k];
+        }
+        e->dt_predelay = dattorro_predelay_samples(e->params[(size_t)(base + OLFX_DT_PREDELAY) * n + 0]);
+        HIPCHK(e, hipMemcpyAsync(e->dt_coef, c.data(), c.size() * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(e, hipStreamSynchronize(s));
+    }
+    if (e->kind == OLFX_KIND_CHORUS || e->kind == OLFX_KIND_PITCHSHIFT || e->kind == OLFX_KIND_CHAIN) {
+        std::vector<uint32_t> c((size_t)CHC_N * n), c2;
+        if (e->kind == OLFX_KIND_CHAIN) c2.resize((size_t)CHC_N * n);
+        uint32_t cc[CHC_N];
+        for (uint32_t i = 0; i < n; ++i) {
+            gather(i);
+            if (e->kind == OLFX_KIND_PITCHSHIFT) derive_pitchshift(p.data(), e->sr, cc);
+            else derive_chorus(p.data() + (e->kind == OLFX_KIND_CHAIN ? OLFX_CN_CHORUS0 : 0), e->sr, cc);
+            for (int k = 0; k < CHC_N; ++k) c[(size_t)k * n + i] = cc[k];
+            if (e->kind == OLFX_KIND_CHAIN) {
+                derive_pitchshift(p.data() + OLFX_CN_PITCH0, e->sr, cc);
+                for (int k = 0; k < CHC_N; ++k) c2[(size_t)k * n + i] = cc[k];
+            }
+        }
+        HIPCHK(e, hipMemcpyAsync(e->ch_coef, c.data(), c.size() * 4, hipMemcpyHostToDevice, s));
+        if (e->kind == OLFX_KIND_CHAIN)
+            HIPCHK(e, hipMemcpyAsync(e->ps_coef, c2.data(), c2.size() * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(e, hipStreamSynchronize(s));
+    }
+    if (e->kind == OLFX_KIND_VOICE) {
+        std::vector<float> c((size_t)VCC_N * n);
+        float cc[VCC_N];
+        for (uint32_t i = 0; i < n; ++i) {
+            gather(i);
+            derive_voice(p.data(), e->configured[i] != 0, e->sr, cc);
+            for (int k = 0; k < VCC_N; ++k) c[(size_t)k * n + i] = cc[k];
+        }
+        HIPCHK(e, hipMemcpyAsync(e->vc_coef, c.data(), c.size() * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(e, hipStreamSynchronize(s));
+    }
+    e->dirty = false;
+    return OLFX_OK;
+}
+
+// Voice note events: NoteOn = GateOn + freq = mtof(note) + Retrigger(true) on both envelopes
+// (SynthVoice.h:245-251); NoteOff = GateOff (:253-256).  Applied to the device state with a
+// read-modify-write of the affected instances (control rate, between blocks).
+int apply_events(olfx_engine *e, hipStream_t s) {
+    if (e->events.empty()) return OLFX_OK;
+    const uint32_t n = e->n;
+    std::vector<float> st((size_t)VCS_N * n);
+    HIPCHK(e, hipMemcpyAsync(st.data(), e->vc_state, st.size() * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(e, hipStreamSynchronize(s));
+    for (const olfx_event &ev : e->events) {
+        const uint32_t i = ev.inst;
+        uint32_t flags;
+        std::memcpy(&flags, &st[(size_t)VCS_FLAGS * n + i], 4);
+        if (ev.type == OLFX_EV_NOTE_ON) {
+            flags |= 1u << 8;                                   // gate = true
+            // Retrigger(true): mode = ATTACK (1), x = 0, for amp (bits 0-2) and filter (3-5)
+            flags = (flags & ~0x3Fu) | 1u | (1u << 3);
+            st[(size_t)VCS_ENVA_X * n + i] = 0.f;
+            st[(size_t)VCS_ENVF_X * n + i] = 0.f;
+            st[(size_t)VCS_FREQ * n + i] = powf(2.f, (ev.note - 69.0f) / 12.0f) * 440.0f;  // daisysp::mtof
+        } else {
+            flags &= ~(1u << 8);
+        }
+        std::memcpy(&st[(size_t)VCS_FLAGS * n + i], &flags, 4);
+    }
+    e->events.clear();
+    HIPCHK(e, hipMemcpyAsync(e->vc_state, st.data(), st.size() * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(e, hipStreamSynchronize(s));
+    return OLFX_OK;
+}
+
+int init_state(olfx_engine *e) {
+    HIPCHK(e, hipMemsetAsync(e->d_mem, 0, e->d_bytes, e->stream));
+    if (e->kind == OLFX_KIND_VOICE) {
+        // daisysp Oscillator::Init phase 0; Svf::Init states 0 and freq 0.25; Adsr idle;
+        // freq_ = 0 (SynthVoice.h:276); Port z1 = 0.
+        std::vector<float> st((size_t)VCS_N * e->n, 0.f);
+        for (uint32_t i = 0; i < e->n; ++i) st[(size_t)VCS_FREQ * e->n + i] = 0.f;
+        HIPCHK(e, hipMemcpyAsync(e->vc_state, st.data(), st.size() * 4, hipMemcpyHostToDevice, e->stream));
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->params.assign((size_t)e->n_params * e->n, 0.f);
+    std::vector<float> d(e->n_params);
+    default_params(e->kind, d.data());
+    for (uint32_t f = 0; f < e->n_params; ++f)
+        std::fill(e->params.begin() + (size_t)f * e->n, e->params.begin() + (size_t)(f + 1) * e->n, d[f]);
+    e->configured.assign(e->n, 0);
+    e->events.clear();
+    e->frames = 0;
+    e->dirty = true;
+    return OLFX_OK;
+}
+
+int ensure_staging(olfx_engine *e, size_t fin, size_t fout) {
+    if (fin > e->stage_floats_in) {
+        if (e->h_in) (void)hipHostFree(e->h_in);
+        if (e->d_in) (void)hipFree(e->d_in);
+        e->h_in = nullptr; e->d_in = nullptr;
+        HIPCHK(e, hipHostMalloc((void **)&e->h_in, fin * 4, hipHostMallocDefault));
+        HIPCHK(e, hipMalloc((void **)&e->d_in, fin * 4));
+        e->stage_floats_in = fin;
+    }
+    if (fout > e->stage_floats_out) {
+        if (e->h_out) (void)hipHostFree(e->h_out);
+        if (e->d_out) (void)hipFree(e->d_out);
+        e->h_out = nullptr; e->d_out = nullptr;
+        HIPCHK(e, hipHostMalloc((void **)&e->h_out, fout * 4, hipHostMallocDefault));
+        HIPCHK(e, hipMalloc((void **)&e->d_out, fout * 4));
+        e->stage_floats_out = fout;
+    }
+    return OLFX_OK;
+}
+
+int ensure_chain_tmp(olfx_engine *e, uint32_t n_frames) {
+    if (n_frames <= e->chain_tmp_frames) return OLFX_OK;
+    if (e->chain_tmp) (void)hipFree(e->chain_tmp);
+    e->chain_tmp = nullptr;
+    HIPCHK(e, hipMalloc((void **)&e->chain_tmp, (size_t)4 * n_frames * e->n * 4));
+    e->chain_tmp_frames = n_frames;
+    return OLFX_OK;
+}
+
+int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hipStream_t s) {
+    hipError_t r = hipSuccess;
+    const uint32_t t0 = (uint32_t)(e->frames & 0xFFFFFFFFu);
+    auto dt_args = [&](const float *in, float *out) {
+        DattorroArgs a{};
+        size_t off = 0;
+        for (int l = 0; l < DT_NLINES; ++l) {
+            a.ring[l] = e->dt_rings + off;
+            off += (size_t)kDtSize[l] * e->n;
+        }
+        a.state = e->dt_state;
+        a.coef = e->dt_coef;
+        a.in = in;
+        a.out = out;
+        a.n = e->n;
+        a.n_frames = n_frames;
+        a.t0 = t0 & 0xFFFFu;
+        a.pre_delay = e->dt_predelay;
+        a.in_ch = 2;
+        return a;
+    };
+    auto ch_args = [&](float *pr, float *cr, uint32_t *st, const uint32_t *cf, const float *in,
+                       float *out, uint32_t mode) {
+        ChorusArgs a{};
+        a.pitch_ring = pr;
+        a.chorus_ring = cr;
+        a.state = st;
+        a.coef = cf;
+        a.in = in;
+        a.out = out;
+        a.n = e->n;
+        a.n_frames = n_frames;
+        a.t0 = t0;
+        a.psize = e->psize;
+        a.csize = e->csize;
+        a.mode = mode;
+        return a;
+    };
+    switch (e->kind) {
+    case OLFX_KIND_DATTORRO: r = launch_dattorro(dt_args(din, dout), s); break;
+    case OLFX_KIND_CHORUS:
+        r = launch_chorus(ch_args(e->ch_pring, e->ch_cring, e->ch_state, e->ch_coef, din, dout, 0), s);
+        break;
+    case OLFX_KIND_PITCHSHIFT:
+        r = launch_chorus(ch_args(e->ch_pring, e->ch_cring, e->ch_state, e->ch_coef, din, dout, 1), s);
+        break;
+    case OLFX_KIND_VOICE: {
+        VoiceArgs a{};
+        a.state = e->vc_state;
+        a.coef = e->vc_coef;
+        a.out = dout;
+        a.n = e->n;
+        a.n_frames = n_frames;
+        r = launch_voice(a, s);
+        break;
+    }
+    case OLFX_KIND_CHAIN: {
+        int rc = ensure_chain_tmp(e, n_frames);
+        if (rc) return rc;
+        float *t1 = e->chain_tmp;
+        float *t2 = e->chain_tmp + (size_t)2 * n_frames * e->n;
+        r = launch_chorus(ch_args(e->ch_pring, e->ch_cring, e->ch_state, e->ch_coef, din, t1, 0), s);
+        if (r == hipSuccess)
+            r = launch_chorus(ch_args(e->ps_pring, e->ps_cring, e->ps_state, e->ps_coef, t1, t2, 1), s);
+        if (r == hipSuccess) r = launch_dattorro(dt_args(t2, dout), s);
+        break;
+    }
+    default: return e->fail(OLFX_E_KIND, "unknown kind");
+    }
+    if (r != hipSuccess) return e->hip_fail(r, "kernel launch");
+    return OLFX_OK;
+}
+
+uint32_t in_channels(int kind) { return kind == OLFX_KIND_VOICE ? 0u : 2u; }
+uint32_t out_channels(int kind) { return kind == OLFX_KIND_VOICE ? 1u : 2u; }
+
+}  // namespace
+
+// =============================================================================================
+// C-ABI
+// =============================================================================================
+extern "C" {
+
+int olfx_abi_version(void) { return OLFX_ABI_VERSION; }
+
+int olfx_kind_info_get(int kind, float sample_rate, olfx_kind_info *info) {
+    if (!info) return OLFX_E_ARG;
+    const uint32_t np = n_params_of(kind);
+    if (!np) return OLFX_E_KIND;
+    info->kind = kind;
+    info->n_params = np;
+    info->in_channels = in_channels(kind);
+    info->out_channels = out_channels(kind);
+    info->state_bytes_per_instance = state_bytes(kind, 1, sample_rate);
+    return OLFX_OK;
+}
+
+int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32_t block,
+                olfx_engine **out) {
+    if (!out) return OLFX_E_ARG;
+    *out = nullptr;
+    if (!n_params_of(kind)) {
+        set_global_error("olfx_create: unknown kind %d", kind);
+        return OLFX_E_KIND;
+    }
+    if (n_inst == 0 || !(sample_rate > 1000.f && sample_rate <= 384000.f) || block == 0 || (block & 3u)) {
+        set_global_error("olfx_create: bad argument (n_inst=%u sr=%g block=%u)", n_inst, sample_rate, block);
+        return OLFX_E_ARG;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        set_global_error("olfx_create: no HIP device visible (this library has no CPU path)");
+        return OLFX_E_NODEVICE;
+    }
+    if (device < 0 || device >= ndev) {
+        set_global_error("olfx_create: device %d out of range (%d devices)", device, ndev);
+        return OLFX_E_NODEVICE;
+    }
+    olfx_engine *e = new (std::nothrow) olfx_engine();
+    if (!e) return OLFX_E_NOMEM;
+    e->kind = kind;
+    e->device = device;
+    e->n = n_inst;
+    e->block = block;
+    e->sr = sample_rate;
+    e->n_params = n_params_of(kind);
+    chorus_sizes(sample_rate, &e->psize, &e->csize);
+
+    hipError_t r = hipSetDevice(device);
+    if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (r != hipSuccess) {
+        int rc = e->hip_fail(r, "olfx_create: stream");
+        delete e;
+        return rc;
+    }
+
+    // carve one allocation
+    const size_t n = n_inst;
+    Carve cv;
+    size_t o_dt_r = 0, o_dt_s = 0, o_dt_c = 0, o_ch_p = 0, o_ch_c = 0, o_ch_s = 0, o_ch_k = 0;
+    size_t o_ps_p = 0, o_ps_c = 0, o_ps_s = 0, o_ps_k = 0, o_vc_s = 0, o_vc_c = 0;
+    const bool has_dt = kind == OLFX_KIND_DATTORRO || kind == OLFX_KIND_CHAIN;
+    const bool has_ch = kind == OLFX_KIND_CHORUS || kind == OLFX_KIND_PITCHSHIFT || kind == OLFX_KIND_CHAIN;
+    const bool has_ps = kind == OLFX_KIND_CHAIN;
+    const bool has_vc = kind == OLFX_KIND_VOICE;
+    if (has_dt) {
+        o_dt_r = cv.take((size_t)dt_total_floats() * n * 4);
+        o_dt_s = cv.take((size_t)DTS_N * n * 4);
+        o_dt_c = cv.take((size_t)DTC_N * n * 4);
+    }
+    if (has_ch) {
+        o_ch_p = cv.take((size_t)2 * e->psize * n * 4);
+        o_ch_c = cv.take((size_t)2 * e->csize * n * 4);
+        o_ch_s = cv.take((size_t)CHS_N * n * 4);
+        o_ch_k = cv.take((size_t)CHC_N * n * 4);
+    }
+    if (has_ps) {
+        o_ps_p = cv.take((size_t)2 * e->psize * n * 4);
+        o_ps_c = cv.take(256);
+        o_ps_s = cv.take((size_t)CHS_N * n * 4);
+        o_ps_k = cv.take((size_t)CHC_N * n * 4);
+    }
+    if (has_vc) {
+        o_vc_s = cv.take((size_t)VCS_N * n * 4);
+        o_vc_c = cv.take((size_t)VCC_N * n * 4);
+    }
+    e->d_bytes = cv.off;
+    r = hipMalloc(&e->d_mem, e->d_bytes);
+    if (r != hipSuccess) {
+        int rc = e->fail(OLFX_E_NOMEM, "olfx_create: hipMalloc(%zu bytes): %s", e->d_bytes, hipGetErrorString(r));
+        (void)hipStreamDestroy(e->stream);
+        delete e;
+        return rc;
+    }
+    char *base = (char *)e->d_mem;
+    if (has_dt) {
+        e->dt_rings = (float *)(base + o_dt_r);
+        e->dt_state = (float *)(base + o_dt_s);
+        e->dt_coef = (float *)(base + o_dt_c);
+    }
+    if (has_ch) {
+        e->ch_pring = (float *)(base + o_ch_p);
+        e->ch_cring = (float *)(base + o_ch_c);
+        e->ch_state = (uint32_t *)(base + o_ch_s);
+        e->ch_coef = (uint32_t *)(base + o_ch_k);
+    }
+    if (has_ps) {
+        e->ps_pring = (float *)(base + o_ps_p);
+        e->ps_cring = (float *)(base + o_ps_c);
+        e->ps_state = (uint32_t *)(base + o_ps_s);
+        e->ps_coef = (uint32_t *)(base + o_ps_k);
+    }
+    if (has_vc) {
+        e->vc_state = (float *)(base + o_vc_s);
+        e->vc_coef = (float *)(base + o_vc_c);
+    }
+    int rc = init_state(e);
+    if (rc) {
+        olfx_destroy(e);
+        return rc;
+    }
+    *out = e;
+    return OLFX_OK;
+}
+
+int olfx_destroy(olfx_engine *e) {
+    if (!e) return OLFX_E_ARG;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->d_mem) (void)hipFree(e->d_mem);
+    if (e->chain_tmp) (void)hipFree(e->chain_tmp);
+    if (e->h_in) (void)hipHostFree(e->h_in);
+    if (e->h_out) (void)hipHostFree(e->h_out);
+    if (e->d_in) (void)hipFree(e->d_in);
+    if (e->d_out) (void)hipFree(e->d_out);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return OLFX_OK;
+}
+
+int olfx_reset(olfx_engine *e) {
+    if (!e) return OLFX_E_ARG;
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return init_state(e);
+}
+
+int olfx_set_params(olfx_engine *e, uint32_t first, uint32_t count, uint32_t field0, uint32_t n_fields,
+                    const float *values) {
+    if (!e) return OLFX_E_ARG;
+    if (!values || (uint64_t)first + count > e->n || (uint64_t)field0 + n_fields > e->n_params)
+        return e->fail(OLFX_E_ARG, "olfx_set_params: range out of bounds");
+    for (uint32_t f = 0; f < n_fields; ++f) {
+        const uint32_t field = field0 + f;
+        for (uint32_t k = 0; k < count; ++k) {
+            float v = values[(size_t)f * count + k];
+            if (!std::isfinite(v)) return e->fail(OLFX_E_ARG, "olfx_set_params: non-finite value");
+            e->params[(size_t)field * e->n + first + k] = v;
+        }
+        // the dattorro pre-delay is engine-wide: uniform taps keep every ring access coalesced
+        const bool predelay = (e->kind == OLFX_KIND_DATTORRO && field == OLFX_DT_PREDELAY) ||
+                              (e->kind == OLFX_KIND_CHAIN && field == OLFX_CN_VERB0 + OLFX_DT_PREDELAY);
+        if (predelay && count) {
+            float v = values[(size_t)f * count];
+            if (v < 0.f || v > 1.f) return e->fail(OLFX_E_ARG, "olfx_set_params: pre-delay outside [0,1]");
+            std::fill(e->params.begin() + (size_t)field * e->n, e->params.begin() + (size_t)(field + 1) * e->n, v);
+        }
+    }
+    if (e->kind == OLFX_KIND_VOICE)
+        for (uint32_t k = 0; k < count; ++k) e->configured[first + k] = 1;
+    e->dirty = true;
+    return OLFX_OK;
+}
+
+int olfx_set_param(olfx_engine *e, uint32_t inst, uint32_t field, float value) {
+    return olfx_set_params(e, inst, 1, field, 1, &value);
+}
+
+int olfx_get_param(olfx_engine *e, uint32_t inst, uint32_t field, float *value) {
+    if (!e || !value || inst >= e->n || field >= e->n_params) return OLFX_E_ARG;
+    *value = e->params[(size_t)field * e->n + inst];
+    return OLFX_OK;
+}
+
+int olfx_note_events(olfx_engine *e, const olfx_event *ev, uint32_t n) {
+    if (!e) return OLFX_E_ARG;
+    if (e->kind != OLFX_KIND_VOICE) return e->fail(OLFX_E_STATE, "olfx_note_events: not a voice engine");
+    if (n && !ev) return e->fail(OLFX_E_ARG, "olfx_note_events: null events");
+    for (uint32_t k = 0; k < n; ++k) {
+        if (ev[k].inst >= e->n || ev[k].note > 127 || ev[k].type > 1)
+            return e->fail(OLFX_E_ARG, "olfx_note_events: bad event %u", k);
+    }
+    e->events.insert(e->events.end(), ev, ev + n);
+    return OLFX_OK;
+}
+
+int olfx_process(olfx_engine *e, const float *in, float *out, uint32_t n_frames, int io_flags, void *stream) {
+    if (!e) return OLFX_E_ARG;
+    if (n_frames == 0) return OLFX_OK;
+    if ((n_frames & 3u) || !out || (in_channels(e->kind) && !in))
+        return e->fail(OLFX_E_ARG, "olfx_process: bad argument (n_frames=%u must be a multiple of 4)", n_frames);
+    if (io_flags != OLFX_IO_DEVICE && io_flags != OLFX_IO_HOST)
+        return e->fail(OLFX_E_ARG, "olfx_process: bad io_flags");
+    HIPCHK(e, hipSetDevice(e->device));
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    int rc = upload_params(e, s);
+    if (rc) return rc;
+    if (e->kind == OLFX_KIND_VOICE) {
+        rc = apply_events(e, s);
+        if (rc) return rc;
+    }
+    const size_t fin = (size_t)in_channels(e->kind) * n_frames * e->n;
+    const size_t fout = (size_t)out_channels(e->kind) * n_frames * e->n;
+    if (io_flags == OLFX_IO_HOST) {
+        rc = ensure_staging(e, fin ? fin : 1, fout);
+        if (rc) return rc;
+        if (fin) {
+            std::memcpy(e->h_in, in, fin * 4);
+            HIPCHK(e, hipMemcpyAsync(e->d_in, e->h_in, fin * 4, hipMemcpyHostToDevice, s));
+        }
+        rc = launch(e, e->d_in, e->d_out, n_frames, s);
+        if (rc) return rc;
+        HIPCHK(e, hipMemcpyAsync(e->h_out, e->d_out, fout * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(e, hipStreamSynchronize(s));
+        std::memcpy(out, e->h_out, fout * 4);
+    } else {
+        rc = launch(e, in, out, n_frames, s);
+        if (rc) return rc;
+    }
+    e->frames += n_frames;
+    return OLFX_OK;
+}
+
+int olfx_sync(olfx_engine *e) {
+    if (!e) return OLFX_E_ARG;
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipDeviceSynchronize());
+    return OLFX_OK;
+}
+
+uint32_t olfx_num_instances(const olfx_engine *e) { return e ? e->n : 0; }
+int olfx_kind(const olfx_engine *e) { return e ? e->kind : 0; }
+uint64_t olfx_frames_processed(const olfx_engine *e) { return e ? e->frames : 0; }
+
+double olfx_algorithmic_bytes_per_frame(const olfx_engine *e) {
+    if (!e) return 0.0;
+    // DESIGN.md section 4 / SURVEY.md section 8d, B = 256: compulsory ring traffic + I/O
+    switch (e->kind) {
+    case OLFX_KIND_DATTORRO: return 164.6;     // 148.6 state + 8 in + 8 out (stereo in)
+    case OLFX_KIND_CHORUS: return 56.0;        // 2 x (pitch w + 2 taps + chorus w + tap) x 4 + 16 I/O
+    case OLFX_KIND_PITCHSHIFT: return 40.0;    // 2 x (w + 2 taps) x 4 + 16 I/O
+    case OLFX_KIND_VOICE: return 5.4;          // 4 B out + per-block state
+    case OLFX_KIND_CHAIN: return 228.6;
+    default: return 0.0;
+    }
+}
+
+const char *olfx_kernel_name(const olfx_engine *e) {
+    if (!e) return "";
+    switch (e->kind) {
+    case OLFX_KIND_DATTORRO: return "dattorro_block_v1";
+    case OLFX_KIND_CHORUS:
+    case OLFX_KIND_PITCHSHIFT: return "chorus_block_v1";
+    case OLFX_KIND_VOICE: return "voice_block_v1";
+    case OLFX_KIND_CHAIN: return "dattorro_block_v1";
+    default: return "";
+    }
+}
+
+const char *olfx_last_error(const olfx_engine *e) {
+    if (e) return e->err.c_str();
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    static thread_local std::string copy;
+    copy = g_err;
+    return copy.c_str();
+}
+
+}  // extern "C"

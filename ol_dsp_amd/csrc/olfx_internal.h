@@ -1,0 +1,179 @@
+// ol_dsp_amd/csrc/olfx_internal.h -- kernel argument blocks, ring geometry and the
+// host/device-shared scalar DSP helpers of libolfx.so.
+//
+// Everything here is written for gfx950 (CDNA4, wave64) and compiled with -ffp-contract=off so
+// that the device arithmetic is the exact IEEE single-precision sequence the CPU oracle uses.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define OLFX_HD __host__ __device__ __forceinline__
+
+namespace olfx {
+
+// ----------------------------------------------------------------------------------------------
+// Dattorro plate: 13 power-of-two rings (reference libs/dattorro-verb/verb.cpp:65-98,173-212).
+// ----------------------------------------------------------------------------------------------
+enum DtLine {
+    DT_PRE = 0, DT_IN0, DT_IN1, DT_IN2, DT_IN3,
+    DT_AP1A, DT_DL1A, DT_AP2A, DT_DL2A,
+    DT_AP1B, DT_DL1B, DT_AP2B, DT_DL2B,
+    DT_NLINES
+};
+// nominal (TAP_MAIN) delay of each line
+constexpr uint32_t kDtDelay[DT_NLINES] = {4800, 142, 107, 379, 277, 672, 4453, 1800, 3720,
+                                          908, 4217, 2656, 3163};
+// ring size = 2^(bit length of delay)
+constexpr uint32_t dt_ring_size(uint32_t d) {
+    uint32_t b = 0;
+    while (d) { ++b; d >>= 1; }
+    return 1u << b;
+}
+constexpr uint32_t kDtSize[DT_NLINES] = {
+    dt_ring_size(4800), dt_ring_size(142), dt_ring_size(107), dt_ring_size(379),
+    dt_ring_size(277), dt_ring_size(672), dt_ring_size(4453), dt_ring_size(1800),
+    dt_ring_size(3720), dt_ring_size(908), dt_ring_size(4217), dt_ring_size(2656),
+    dt_ring_size(3163)};
+constexpr uint32_t dt_total_floats() {
+    uint32_t s = 0;
+    for (int l = 0; l < DT_NLINES; ++l) s += kDtSize[l];
+    return s;
+}
+static_assert(dt_total_floats() == 42368, "dattorro ring geometry");
+
+// Output tap delays (verb.cpp:187-212) and the stereo tap sums (verb.cpp:302-325).
+// Left  = +DL1B.o1 +DL1B.o2 -AP2B.o2 +DL2B.o2 -DL1A.o3 -AP2A.o1 +DL2A.o1
+// Right = +DL1A.o1 +DL1A.o2 -AP2A.o2 +DL2A.o2 -DL1B.o3 -AP2B.o1 +DL2B.o1
+constexpr uint32_t kDl1A_o1 = 353, kDl1A_o2 = 3627, kDl1A_o3 = 1990;
+constexpr uint32_t kAp2A_o1 = 187, kAp2A_o2 = 1228;
+constexpr uint32_t kDl2A_o1 = 1066, kDl2A_o2 = 2673;
+constexpr uint32_t kDl1B_o1 = 266, kDl1B_o2 = 2974, kDl1B_o3 = 2111;
+constexpr uint32_t kAp2B_o1 = 335, kAp2B_o2 = 1913;
+constexpr uint32_t kDl2B_o1 = 121, kDl2B_o2 = 1996;
+
+// Derived per-instance coefficients (field-major [DTC_N][n] on the device).
+enum { DTC_PREFILTER = 0, DTC_IN1, DTC_IN2, DTC_DD1, DTC_DAMPING, DTC_DECAY, DTC_DD2, DTC_N };
+// Per-instance recursive scalar state ([DTS_N][n]).
+enum { DTS_LP_PRE = 0, DTS_LP_DAMP_A, DTS_LP_DAMP_B, DTS_N };
+
+// Extra delay of both tank input all-passes at stream time t16 (verb.cpp:262-270): their read
+// offset is decremented at every t16 = k*2048 < 32768 and incremented at every k*2048 >= 32768,
+// *before* the sample at that t is processed.  For an instance created at t = 0 the count is
+// closed-form, so every chunk can compute it without carrying the offset.
+OLFX_HD uint32_t dt_ap1_extra(uint32_t t16) {
+    uint32_t dec = ((t16 >> 11) < 15u ? (t16 >> 11) : 15u) + 1u;
+    uint32_t inc = t16 >= 32768u ? ((t16 - 32768u) >> 11) + 1u : 0u;
+    return dec - inc;
+}
+
+struct DattorroArgs {
+    float *ring[DT_NLINES];     // ring l: [kDtSize[l]][n]   (position-major, instance fastest)
+    float *state;               // [DTS_N][n]
+    const float *coef;          // [DTC_N][n]
+    const float *in;            // [2][n_frames][n]
+    float *out;                 // [2][n_frames][n]
+    uint32_t n;                 // instances
+    uint32_t n_frames;
+    uint32_t t0;                // stream time (frames since create) of the first frame, mod 2^16
+    uint32_t pre_delay;         // engine-wide pre-delay in samples (0..4800)
+    uint32_t in_ch;             // 1 or 2
+};
+
+// ----------------------------------------------------------------------------------------------
+// Deterministic cos(2*pi*x): used by the chorus LFO (RNBO cycle~) and the pitch-shifter
+// crossfade windows (gen~ cos).  Only +,-,*, rint and compares, evaluated in a fixed order, so the
+// host (oracle) and gfx950 produce identical bits under -ffp-contract=off.  |err| < 2e-7.
+// ----------------------------------------------------------------------------------------------
+OLFX_HD float cos2pi(float x) {
+    float u = x - rintf(x);                 // exact, u in [-0.5, 0.5]
+    float a = u < 0.0f ? -u : u;            // cos is even
+    float sgn = 1.0f;
+    if (a > 0.25f) { a = 0.5f - a; sgn = -1.0f; }   // cos(2pi(1/2 - a)) = -cos(2pi a), exact
+    float r;
+    if (a <= 0.125f) {
+        float th = a * 6.28318530717958647692f;
+        float t2 = th * th;
+        // cos, Taylor to th^10 on [0, pi/4]
+        r = 1.0f + t2 * (-0.5f + t2 * (4.16666666666666666667e-2f + t2 * (-1.38888888888888888889e-3f +
+            t2 * (2.48015873015873015873e-5f + t2 * (-2.75573192239858906526e-7f)))));
+    } else {
+        float b = 0.25f - a;                // exact
+        float th = b * 6.28318530717958647692f;
+        float t2 = th * th;
+        // sin, Taylor to th^11 on [0, pi/4]
+        r = th * (1.0f + t2 * (-1.66666666666666666667e-1f + t2 * (8.33333333333333333333e-3f +
+            t2 * (-1.98412698412698412698e-4f + t2 * (2.75573192239858906526e-6f +
+            t2 * (-2.50521083854417187751e-8f))))));
+    }
+    return sgn * r;
+}
+
+// ----------------------------------------------------------------------------------------------
+// Chorus / pitch-shift (spec: DESIGN.md section 3, from modules/rnbo/patcher/mono-chorus.rnbopat
+// and pitchshift.gendsp).  Per-instance rings are instance-major ([n][size]) because the taps are
+// modulated per instance: each lane streams through its own ring.
+// ----------------------------------------------------------------------------------------------
+enum {
+    CHC_LFO_INC = 0,    // u32 phase increment of cycle~ (2^32 = one cycle)
+    CHC_LFO_OFF,        // u32 phase offset of cycle~
+    CHC_PS_INC,         // u32 phase increment of the pitch-shifter phasor
+    CHC_DEPTH,          // D = mstosamps(1 + 11 depth)       (float)
+    CHC_WINDOW,         // W = mstosamps(window)             (float)
+    CHC_B0, CHC_B1, CHC_B2, CHC_A1, CHC_A2,   // lores~ (RBJ biquad LP, normalised by a0)
+    CHC_MIX, CHC_DRY,   // mix, 1 - mix
+    CHC_N
+};
+enum {
+    CHS_LFO_ACC = 0,    // u32
+    CHS_PS_ACC,         // u32
+    CHS_Z1L, CHS_Z2L, CHS_Z1R, CHS_Z2R,   // biquad TDF-II state per channel
+    CHS_N
+};
+
+struct ChorusArgs {
+    float *pitch_ring;          // [n][2][psize]
+    float *chorus_ring;         // [n][2][csize]
+    uint32_t *state;            // [CHS_N][n] (floats stored bitwise)
+    const uint32_t *coef;       // [CHC_N][n]
+    const float *in;            // [2][n_frames][n]
+    float *out;                 // [2][n_frames][n]
+    uint32_t n, n_frames;
+    uint32_t t0;                // write position of the first frame (mod ring sizes)
+    uint32_t psize, csize;      // ring sizes (powers of two)
+    uint32_t mode;              // 0 = full chorus, 1 = pitch-shift stage only
+};
+
+// ----------------------------------------------------------------------------------------------
+// Voice (SynthVoice): registers only.
+// ----------------------------------------------------------------------------------------------
+enum {
+    VCC_ATK_D0A = 0, VCC_ATK_TGT_A, VCC_DEC_D0A, VCC_REL_D0A, VCC_SUS_A,   // amp env
+    VCC_ATK_D0F, VCC_ATK_TGT_F, VCC_DEC_D0F, VCC_REL_D0F, VCC_SUS_F,       // filter env
+    VCC_AMP_AMT, VCC_CUTOFF, VCC_FENV_AMT,
+    VCC_DAMP_RES,       // 2 * (1 - powf(res, 0.25))   (Svf::SetRes, computed on host)
+    VCC_DRIVE,          // pre_drive * res
+    VCC_PORT_COEF,      // expf(-1/(htime*sr))
+    VCC_FC_MAX,         // sr / 3
+    VCC_SR,             // sample rate
+    VCC_INV_SR,         // Oscillator sr_recip_ = 1/sr
+    VCC_N
+};
+enum {
+    VCS_PHASE = 0, VCS_PORT_Z, VCS_ENVA_X, VCS_ENVF_X, VCS_LOW, VCS_BAND, VCS_FREQ,
+    VCS_FLAGS,          // bits 0-2 amp mode, 3-5 filt mode, 6 gate(amp prev), 7 gate(filt prev), 8 gate
+    VCS_N
+};
+
+struct VoiceArgs {
+    float *state;               // [VCS_N][n]
+    const float *coef;          // [VCC_N][n]
+    float *out;                 // [1][n_frames][n]
+    uint32_t n, n_frames;
+};
+
+// Launchers (defined in the .hip files).
+hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s);
+hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s);
+hipError_t launch_voice(const VoiceArgs &a, hipStream_t s);
+
+}  // namespace olfx

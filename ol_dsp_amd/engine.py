@@ -1,0 +1,193 @@
+"""Host-side Python mirror of the batch engine C-ABI (include/olfx.h).
+
+``Engine`` owns one libolfx engine: one effect kind x N independent instances on one GPU.
+Audio crosses the boundary as ``[channels][frames][instances]`` float32 buffers, either torch
+CUDA tensors (device pointers, the fast path; torch is only plumbing for device memory and
+streams) or numpy arrays (host pointers, staged through pinned memory inside the library).
+
+Reference surfaces this mirrors (per instance, batched here):
+  DattorroVerb_create/set*/process/getLeft/getRight   libs/dattorro-verb/verb.h:5-26
+  ChorusEffect init/setDepth/setRate/process           README.md:114-128 (+ RNBO params)
+  SynthVoice Init/UpdateConfig/NoteOn/NoteOff/Process  modules/synthlib/SynthVoice.h:31-256
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, load
+
+KIND_NAMES = {
+    "dattorro": _lib.KIND_DATTORRO,
+    "chorus": _lib.KIND_CHORUS,
+    "pitchshift": _lib.KIND_PITCHSHIFT,
+    "voice": _lib.KIND_VOICE,
+    "chain": _lib.KIND_CHAIN,
+}
+
+# parameter field names, in C-ABI order
+PARAMS = {
+    _lib.KIND_DATTORRO: ["pre_delay", "pre_filter", "input_diffusion1", "input_diffusion2",
+                         "decay_diffusion", "decay", "damping"],
+    _lib.KIND_CHORUS: ["pitch", "mix", "q", "cutoff", "phase", "depth", "rate", "window"],
+    _lib.KIND_PITCHSHIFT: ["shift", "window"],
+    _lib.KIND_VOICE: ["filter_cutoff", "filter_resonance", "filter_drive", "filter_env_amount",
+                      "filter_attack", "filter_attack_shape", "filter_decay", "filter_sustain",
+                      "filter_release", "amp_env_amount", "amp_attack", "amp_attack_shape",
+                      "amp_decay", "amp_sustain", "amp_release", "portamento"],
+}
+PARAMS[_lib.KIND_CHAIN] = (["chorus_" + p for p in PARAMS[_lib.KIND_CHORUS]]
+                           + ["pitch_" + p for p in PARAMS[_lib.KIND_PITCHSHIFT]]
+                           + ["verb_" + p for p in PARAMS[_lib.KIND_DATTORRO]])
+
+
+def kind_info(kind: int, sample_rate: float = 48000.0) -> _lib.KindInfo:
+    info = _lib.KindInfo()
+    check(load().olfx_kind_info_get(int(kind), float(sample_rate), ctypes.byref(info)))
+    return info
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+class Engine:
+    """N instances of one effect kind on one GPU (see module docstring)."""
+
+    def __init__(self, kind, n_inst: int, sample_rate: float = 48000.0, block: int = 256,
+                 device: int = 0):
+        self.lib = load()
+        self.kind = KIND_NAMES[kind] if isinstance(kind, str) else int(kind)
+        self.n = int(n_inst)
+        self.sample_rate = float(sample_rate)
+        self.block = int(block)
+        self.device = int(device)
+        self.info = kind_info(self.kind, sample_rate)
+        h = ctypes.c_void_p()
+        check(self.lib.olfx_create(self.kind, self.device, self.n, self.sample_rate, self.block,
+                                   ctypes.byref(h)))
+        self._h = h
+
+    # ---- lifetime ----
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.lib.olfx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def reset(self) -> None:
+        check(self.lib.olfx_reset(self._h), self._h)
+
+    # ---- parameters ----
+    def field(self, name_or_index) -> int:
+        if isinstance(name_or_index, str):
+            return PARAMS[self.kind].index(name_or_index)
+        return int(name_or_index)
+
+    def set_param(self, inst: int, field, value: float) -> None:
+        check(self.lib.olfx_set_param(self._h, int(inst), self.field(field), float(value)), self._h)
+
+    def get_param(self, inst: int, field) -> float:
+        v = ctypes.c_float()
+        check(self.lib.olfx_get_param(self._h, int(inst), self.field(field), ctypes.byref(v)), self._h)
+        return v.value
+
+    def set_params(self, field0, values, first: int = 0) -> None:
+        """values: array [n_fields][count] (field-major) for fields field0.. and instances first.."""
+        arr = np.ascontiguousarray(np.asarray(values, dtype=np.float32))
+        if arr.ndim == 1:
+            arr = arr[None, :]
+        nf, cnt = arr.shape
+        check(self.lib.olfx_set_params(self._h, int(first), int(cnt), self.field(field0), int(nf),
+                                       arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float))), self._h)
+
+    def note_events(self, events: Iterable[Sequence[int]]) -> None:
+        """events: iterable of (inst, type, note[, velocity]); type 1 = NoteOn, 0 = NoteOff."""
+        evs = list(events)
+        if not evs:
+            return
+        arr = (_lib.Event * len(evs))()
+        for k, e in enumerate(evs):
+            arr[k].inst = int(e[0])
+            arr[k].type = int(e[1])
+            arr[k].note = int(e[2])
+            arr[k].velocity = int(e[3]) if len(e) > 3 else 100
+        check(self.lib.olfx_note_events(self._h, arr, len(evs)), self._h)
+
+    # ---- processing ----
+    def process(self, x, out=None, n_frames: Optional[int] = None, stream=None):
+        """Process one block for all instances.
+
+        x: [in_ch][frames][n] torch CUDA tensor or numpy array (None for voices).
+        out: optional preallocated output of the same kind; returned.
+        stream: hipStream_t as int (torch.cuda.Stream.cuda_stream) or None = torch's current
+        stream for tensors, the engine's stream for numpy.
+        """
+        ich, och = self.info.in_channels, self.info.out_channels
+        ref = x if x is not None else out
+        if n_frames is None:
+            if x is not None:
+                n_frames = int(x.shape[1])
+            elif out is not None:
+                n_frames = int(out.shape[1])
+            else:
+                raise ValueError("n_frames required")
+        if ref is not None and _is_torch(ref):
+            import torch
+            if x is not None:
+                assert x.is_cuda and x.dtype == torch.float32 and x.is_contiguous()
+                assert tuple(x.shape) == (ich, n_frames, self.n), (tuple(x.shape), (ich, n_frames, self.n))
+            if out is None:
+                out = torch.empty((och, n_frames, self.n), dtype=torch.float32, device=ref.device)
+            assert out.is_contiguous() and tuple(out.shape) == (och, n_frames, self.n)
+            if stream is None:
+                stream = torch.cuda.current_stream(ref.device).cuda_stream
+            check(self.lib.olfx_process(self._h, ctypes.c_void_p(x.data_ptr() if x is not None else 0),
+                                        ctypes.c_void_p(out.data_ptr()), int(n_frames), _lib.IO_DEVICE,
+                                        ctypes.c_void_p(stream)), self._h)
+            return out
+        # host path
+        xin = None
+        if x is not None:
+            xin = np.ascontiguousarray(np.asarray(x, dtype=np.float32))
+            assert xin.shape == (ich, n_frames, self.n), (xin.shape, (ich, n_frames, self.n))
+        if out is None:
+            out = np.empty((och, n_frames, self.n), dtype=np.float32)
+        check(self.lib.olfx_process(self._h, ctypes.c_void_p(xin.ctypes.data if xin is not None else 0),
+                                    ctypes.c_void_p(out.ctypes.data), int(n_frames), _lib.IO_HOST,
+                                    ctypes.c_void_p(stream or 0)), self._h)
+        return out
+
+    def sync(self) -> None:
+        check(self.lib.olfx_sync(self._h), self._h)
+
+    # ---- facts ----
+    @property
+    def frames_processed(self) -> int:
+        return int(self.lib.olfx_frames_processed(self._h))
+
+    @property
+    def algorithmic_bytes_per_frame(self) -> float:
+        return float(self.lib.olfx_algorithmic_bytes_per_frame(self._h))
+
+    @property
+    def kernel_name(self) -> str:
+        return self.lib.olfx_kernel_name(self._h).decode()

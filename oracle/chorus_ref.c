@@ -1,0 +1,235 @@
+/*
+ * oracle/chorus_ref.c -- CPU spec oracle for the RNBO stereo chorus and the gen~ pitch-shifter.
+ *
+ * TEST INFRASTRUCTURE ONLY (tests/, smoke(), bench.py cpu_baseline).  Never part of the product.
+ *
+ * Parity status: UNPINNED.  The reference defines the chorus and pitch-shift only as Max/RNBO and
+ * gen~ patches (modules/rnbo/patcher/mono-chorus.rnbopat, stereo-chorus.rnbopat,
+ * pitchshift.gendsp); Max/RNBO/genlib are proprietary and absent, and the RNBO C++ export is
+ * git-ignored (modules/rnbo/patcher/.gitignore:1).  No reference test, fixture or golden vector
+ * covers them.  This file restates the patch dataflow exactly as written (per-object citations
+ * below) with the build's declared spec choices:
+ *   - fp32 arithmetic (gen~/RNBO compute in double);
+ *   - phasors as 32-bit fixed-point accumulators, 24-bit fraction -> float;
+ *   - cos(2 pi x) by a fixed polynomial (cos2pi below), standing in for cycle~'s wavetable and
+ *     gen~'s cos;
+ *   - gen Delay.read: linear interpolation, delay clamped to [1, size-2] (read before write);
+ *     RNBO delay~: linear interpolation, delay clamped to [0, size-2] (write before read);
+ *   - lores~: RBJ biquad low-pass (transposed direct form II), Q = 1/sqrt(2) + 20 q^3.
+ *
+ * Dataflow (mono-chorus.rnbopat patchlines):
+ *   in~1 -> gen~ pitchshift (:1119) -> delay~ (:1793) -> lores~ (:1808) -> *~ mix (:1302) -> +~ -> out~1
+ *   in~1 -> *~ (1 - mix) (:1157, !- 1 :1176) -> +~ (:1191)
+ *   param rate (:4353) -> scale 0 1 0.01 0.5 (:3935) -> cycle~ freq (:3002); param phase (:3420) -> cycle~ phase
+ *   param depth (:3854) -> scale 0 1 1 12 1 (:3436) -> mstosamps (:3897) = D;
+ *   cycle~ * D (:2935) + D (:2920) -> delay~ time;  param cutoff (:2660) -> scale 0 1 300 15000 1
+ *   (:2242) -> lores~ cutoff; param q (:2226) -> lores~ resonance
+ * pitchshift gencode (mono-chorus.rnbopat:962, pitchshift.gendsp:19-305):
+ *   W = mstosamps(window); ph = phasor(in2); p0 = ph % 1; p1 = (ph + .5) % 1;
+ *   out1 = read(p1 W) cos((p1-.5) pi) + read(p0 W) cos((p0-.5) pi); write(in1)
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include "oracle.h"
+
+static float clampf_(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+static uint32_t pow2ge(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; return p; }
+
+static uint32_t fix_inc(double hz, double sr)
+{
+    double v = floor(hz / sr * 4294967296.0 + 0.5);
+    return v < 0 ? 0u : (uint32_t)(uint64_t)v;
+}
+
+static float unit24(uint32_t acc) { return (float)(acc >> 8) * 5.9604644775390625e-8f; }
+
+/* cos(2 pi x) by reduction to [0, 1/8] and Taylor polynomials (identical op order on the GPU) */
+float oracle_cos2pi(float x)
+{
+    float u = x - rintf(x);
+    float a = u < 0.0f ? -u : u;
+    float sgn = 1.0f;
+    if (a > 0.25f) { a = 0.5f - a; sgn = -1.0f; }
+    float r;
+    if (a <= 0.125f) {
+        float th = a * 6.28318530717958647692f;
+        float t2 = th * th;
+        r = 1.0f + t2 * (-0.5f + t2 * (4.16666666666666666667e-2f + t2 * (-1.38888888888888888889e-3f +
+            t2 * (2.48015873015873015873e-5f + t2 * (-2.75573192239858906526e-7f)))));
+    } else {
+        float b = 0.25f - a;
+        float th = b * 6.28318530717958647692f;
+        float t2 = th * th;
+        r = th * (1.0f + t2 * (-1.66666666666666666667e-1f + t2 * (8.33333333333333333333e-3f +
+            t2 * (-1.98412698412698412698e-4f + t2 * (2.75573192239858906526e-6f +
+            t2 * (-2.50521083854417187751e-8f))))));
+    }
+    return sgn * r;
+}
+
+typedef struct {
+    uint32_t lfo_inc, lfo_off, ps_inc;
+    float D, W, b0, b1, b2, a1, a2, mix, dry;
+} chcoef_t;
+
+typedef struct {
+    uint32_t lfo_acc, ps_acc;
+    float z1[2], z2[2];
+    float *pring[2], *cring[2];
+} chstate_t;
+
+struct oracle_chorus {
+    int n, mode;
+    double sr;
+    uint32_t psize, csize;
+    uint64_t w;                /* stream write position */
+    float *pool;
+    chcoef_t *k;
+    chstate_t *s;
+    float *params;             /* [n][OCH_NPARAMS] */
+};
+
+static void derive(const float *p, double sr, chcoef_t *c)
+{
+    const double pitch = clampf_(p[OCH_PITCH], 0.0f, 3.0f);
+    const double mix = clampf_(p[OCH_MIX], 0.0f, 1.0f);
+    const double q = clampf_(p[OCH_Q], 0.0f, 1.0f);
+    const double cutoff = clampf_(p[OCH_CUTOFF], 0.0f, 1.0f);
+    const double phase = clampf_(p[OCH_PHASE], 0.0f, 1.0f);
+    const double depth = clampf_(p[OCH_DEPTH], 0.08f, 1.0f);
+    const double rate = clampf_(p[OCH_RATE], 0.01f, 1.0f);
+    const double window = clampf_(p[OCH_WINDOW], 4.0f, 10.0f);
+    const double rate_hz = 0.01 + rate * (0.5 - 0.01);
+    const double depth_ms = 1.0 + depth * (12.0 - 1.0);
+    const double fc = 300.0 + cutoff * (15000.0 - 300.0);
+    c->lfo_inc = fix_inc(rate_hz, sr);
+    c->lfo_off = (uint32_t)(uint64_t)floor(phase * 4294967296.0 + 0.5);
+    c->ps_inc = fix_inc(pitch, sr);
+    c->D = (float)(depth_ms * sr / 1000.0);
+    c->W = (float)(window * sr / 1000.0);
+    const double Q = 0.70710678118654752 + 20.0 * q * q * q;
+    const double w0 = 2.0 * 3.14159265358979323846 * fc / sr;
+    const double cw = cos(w0), sw = sin(w0);
+    const double alpha = sw / (2.0 * Q);
+    const double a0 = 1.0 + alpha;
+    c->b0 = (float)((1.0 - cw) * 0.5 / a0);
+    c->b1 = (float)((1.0 - cw) / a0);
+    c->b2 = (float)((1.0 - cw) * 0.5 / a0);
+    c->a1 = (float)(-2.0 * cw / a0);
+    c->a2 = (float)((1.0 - alpha) / a0);
+    c->mix = (float)mix;
+    c->dry = 1.0f - c->mix;
+}
+
+static void default_params(float *p)
+{
+    p[OCH_PITCH] = 0.0f; p[OCH_MIX] = 0.5f; p[OCH_Q] = 0.5f; p[OCH_CUTOFF] = 0.3f;
+    p[OCH_PHASE] = 1.0f; p[OCH_DEPTH] = 0.5f; p[OCH_RATE] = 0.2f; p[OCH_WINDOW] = 10.0f;
+}
+
+oracle_chorus *oracle_chorus_create(int n_inst, float sample_rate, int mode)
+{
+    if (n_inst <= 0 || (mode != 0 && mode != 1)) return NULL;
+    oracle_chorus *o = (oracle_chorus *)calloc(1, sizeof(*o));
+    if (!o) return NULL;
+    o->n = n_inst;
+    o->mode = mode;
+    o->sr = sample_rate;
+    o->psize = pow2ge((uint32_t)ceil(10.0 * sample_rate / 1000.0) + 2);
+    o->csize = pow2ge(2u * (uint32_t)ceil(12.0 * sample_rate / 1000.0) + 2);
+    const size_t per = 2u * (o->psize + o->csize);
+    o->pool = (float *)calloc(per * (size_t)n_inst, sizeof(float));
+    o->k = (chcoef_t *)calloc((size_t)n_inst, sizeof(chcoef_t));
+    o->s = (chstate_t *)calloc((size_t)n_inst, sizeof(chstate_t));
+    o->params = (float *)calloc((size_t)n_inst * OCH_NPARAMS, sizeof(float));
+    if (!o->pool || !o->k || !o->s || !o->params) { oracle_chorus_destroy(o); return NULL; }
+    for (int i = 0; i < n_inst; i++) {
+        float *base = o->pool + per * (size_t)i;
+        o->s[i].pring[0] = base;
+        o->s[i].pring[1] = base + o->psize;
+        o->s[i].cring[0] = base + 2 * o->psize;
+        o->s[i].cring[1] = base + 2 * o->psize + o->csize;
+        default_params(o->params + (size_t)i * OCH_NPARAMS);
+        derive(o->params + (size_t)i * OCH_NPARAMS, o->sr, &o->k[i]);
+    }
+    return o;
+}
+
+void oracle_chorus_destroy(oracle_chorus *o)
+{
+    if (!o) return;
+    free(o->pool); free(o->k); free(o->s); free(o->params); free(o);
+}
+
+int oracle_chorus_set(oracle_chorus *o, int inst, int field, float value)
+{
+    if (!o || inst < 0 || inst >= o->n || field < 0 || field >= OCH_NPARAMS) return -1;
+    o->params[(size_t)inst * OCH_NPARAMS + field] = value;
+    derive(o->params + (size_t)inst * OCH_NPARAMS, o->sr, &o->k[inst]);
+    return 0;
+}
+
+static float read_frac(const float *ring, uint32_t mask, uint32_t w, float d, float dmin, float dmax)
+{
+    d = fminf(fmaxf(d, dmin), dmax);
+    uint32_t di = (uint32_t)d;
+    float fr = d - (float)di;
+    float x0 = ring[(w - di) & mask];
+    float x1 = ring[(w - di - 1u) & mask];
+    return x0 + fr * (x1 - x0);
+}
+
+/* in/out [2][n_frames][n] */
+int oracle_chorus_process(oracle_chorus *o, const float *in, float *out, int n_frames, int n_threads)
+{
+    if (!o || n_frames < 0) return -1;
+    const long n = o->n;
+    const long plane = n * (long)n_frames;
+    const uint32_t pmask = o->psize - 1, cmask = o->csize - 1;
+    const float pmax = (float)(o->psize - 2), cmax = (float)(o->csize - 2);
+    const uint32_t w0 = (uint32_t)o->w;
+    (void)n_threads;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) num_threads(n_threads > 0 ? n_threads : 1)
+#endif
+    for (long i = 0; i < n; i++) {
+        const chcoef_t *k = &o->k[i];
+        chstate_t *s = &o->s[i];
+        for (int f = 0; f < n_frames; f++) {
+            const uint32_t w = w0 + (uint32_t)f;
+            const float lfo = oracle_cos2pi(unit24(s->lfo_acc + k->lfo_off));
+            s->lfo_acc += k->lfo_inc;
+            const float dch = lfo * k->D + k->D;
+            const float p0 = unit24(s->ps_acc);
+            const float p1 = unit24(s->ps_acc + 0x80000000u);
+            s->ps_acc += k->ps_inc;
+            const float g0 = oracle_cos2pi((p0 - 0.5f) * 0.5f);
+            const float g1 = oracle_cos2pi((p1 - 0.5f) * 0.5f);
+            const float d0 = p0 * k->W, d1 = p1 * k->W;
+            for (int c = 0; c < 2; c++) {
+                const float x = in[c * plane + (long)f * n + i];
+                const float t0 = read_frac(s->pring[c], pmask, w, d0, 1.0f, pmax);
+                const float t1 = read_frac(s->pring[c], pmask, w, d1, 1.0f, pmax);
+                const float ps = t1 * g1 + t0 * g0;
+                s->pring[c][w & pmask] = x;
+                float y;
+                if (o->mode == 0) {
+                    s->cring[c][w & cmask] = ps;
+                    const float wet = read_frac(s->cring[c], cmask, w, dch, 0.0f, cmax);
+                    const float lp = k->b0 * wet + s->z1[c];
+                    s->z1[c] = (k->b1 * wet - k->a1 * lp) + s->z2[c];
+                    s->z2[c] = k->b2 * wet - k->a2 * lp;
+                    y = x * k->dry + lp * k->mix;
+                } else {
+                    y = ps;
+                }
+                out[c * plane + (long)f * n + i] = y;
+            }
+        }
+    }
+    o->w += (uint64_t)n_frames;
+    return 0;
+}

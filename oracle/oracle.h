@@ -1,0 +1,72 @@
+/*
+ * oracle/oracle.h -- C API of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+ *
+ * Used by tests/ (via ctypes), __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+ * Never linked into the product library (ol_dsp_amd/libolfx.so).
+ *
+ * Layouts match the product C-ABI (include/olfx.h):
+ *   audio in : [in_ch][n_frames][n_inst]   (instance index fastest)
+ *   audio out: [out_ch][n_frames][n_inst]
+ */
+#ifndef OLFX_ORACLE_H
+#define OLFX_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- Dattorro plate reverb (bit-exact restatement of libs/dattorro-verb/verb.cpp) ---- */
+enum {
+    ODT_PREDELAY = 0,          /* DattorroVerb_setPreDelay       verb.cpp:137 */
+    ODT_PREFILTER,             /* DattorroVerb_setPreFilter      verb.cpp:142 */
+    ODT_INPUT_DIFFUSION1,      /* DattorroVerb_setInputDiffusion1 verb.cpp:147 */
+    ODT_INPUT_DIFFUSION2,      /* DattorroVerb_setInputDiffusion2 verb.cpp:152 */
+    ODT_DECAY_DIFFUSION,       /* DattorroVerb_setDecayDiffusion verb.cpp:157 */
+    ODT_DECAY,                 /* DattorroVerb_setDecay          verb.cpp:162 */
+    ODT_DAMPING,               /* DattorroVerb_setDamping        verb.cpp:168 */
+    ODT_NPARAMS
+};
+typedef struct oracle_dattorro oracle_dattorro;
+size_t oracle_dattorro_state_floats(void);
+oracle_dattorro *oracle_dattorro_create(int n_inst);
+void oracle_dattorro_destroy(oracle_dattorro *o);
+int oracle_dattorro_set(oracle_dattorro *o, int inst, int field, float value);
+int oracle_dattorro_process(oracle_dattorro *o, const float *in, int in_ch, float *out,
+                            int n_frames, int n_threads);
+/* KAT helpers: xorshift32 noise and FNV-1a-64 over L,R frame bytes */
+uint32_t oracle_xorshift_noise(uint32_t seed, float *out, long n, long stride);
+uint64_t oracle_fnv1a64_lr(const float *l, const float *r, long n_frames, long stride);
+
+/* ---- RNBO stereo chorus / gen~ pitch-shift (spec oracle, parity unpinned) ---- */
+enum {
+    OCH_PITCH = 0, OCH_MIX, OCH_Q, OCH_CUTOFF, OCH_PHASE, OCH_DEPTH, OCH_RATE, OCH_WINDOW,
+    OCH_NPARAMS
+};
+typedef struct oracle_chorus oracle_chorus;
+float oracle_cos2pi(float x);
+/* mode 0 = full chorus, 1 = pitch-shift stage only (params OCH_PITCH = shift Hz, OCH_WINDOW) */
+oracle_chorus *oracle_chorus_create(int n_inst, float sample_rate, int mode);
+void oracle_chorus_destroy(oracle_chorus *o);
+int oracle_chorus_set(oracle_chorus *o, int inst, int field, float value);
+int oracle_chorus_process(oracle_chorus *o, const float *in, float *out, int n_frames, int n_threads);
+
+/* ---- synthlib SynthVoice (DaisySP restatement, parity unpinned) ---- */
+enum {  /* Voice::Config order, modules/synthlib/Voice.h:14-31 */
+    OVC_FILTER_CUTOFF = 0, OVC_FILTER_RESONANCE, OVC_FILTER_DRIVE, OVC_FILTER_ENV_AMOUNT,
+    OVC_FILTER_ATTACK, OVC_FILTER_ATTACK_SHAPE, OVC_FILTER_DECAY, OVC_FILTER_SUSTAIN,
+    OVC_FILTER_RELEASE, OVC_AMP_ENV_AMOUNT, OVC_AMP_ATTACK, OVC_AMP_ATTACK_SHAPE,
+    OVC_AMP_DECAY, OVC_AMP_SUSTAIN, OVC_AMP_RELEASE, OVC_PORTAMENTO,
+    OVC_NPARAMS
+};
+typedef struct oracle_voice oracle_voice;
+oracle_voice *oracle_voice_create(int n_inst, float sample_rate);
+void oracle_voice_destroy(oracle_voice *o);
+int oracle_voice_config(oracle_voice *o, int inst, const float *values);
+int oracle_voice_note(oracle_voice *o, int inst, int on, int note);
+int oracle_voice_process(oracle_voice *o, float *out, int n_frames, int n_threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,209 @@
+"""ctypes access to the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg -- never by the
+product package.  Two libraries:
+  oracle/liboracle.so        the C restatements (dattorro bit-exact; chorus/pitch/voice spec oracles)
+  oracle/_ref/libverb_ref.so the REAL reference reverb compiled from /root/reference (dev container;
+                             travels to the GPU box as a prebuilt .so, never rebuilt there)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+REF_LIB = os.path.join(HERE, "_ref", "libverb_ref.so")
+REF_LIB_O0 = os.path.join(HERE, "_ref", "libverb_ref_O0.so")
+
+DT_FIELDS = ["pre_delay", "pre_filter", "input_diffusion1", "input_diffusion2",
+             "decay_diffusion", "decay", "damping"]
+CH_FIELDS = ["pitch", "mix", "q", "cutoff", "phase", "depth", "rate", "window"]
+VC_FIELDS = ["filter_cutoff", "filter_resonance", "filter_drive", "filter_env_amount",
+             "filter_attack", "filter_attack_shape", "filter_decay", "filter_sustain",
+             "filter_release", "amp_env_amount", "amp_attack", "amp_attack_shape",
+             "amp_decay", "amp_sustain", "amp_release", "portamento"]
+VOICE_DEFAULTS = [0.0, 0.0, 0.0, 1.0, 0.0, 1.0, 0.2, 0.0, 0.0, 0.8, 0.01, 1.0, 0.0, 1.0, 0.01, 0.0]
+
+_F = ctypes.c_float
+_PF = ctypes.POINTER(ctypes.c_float)
+_lib = None
+_ref = {}
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        L.oracle_dattorro_create.restype = ctypes.c_void_p
+        L.oracle_dattorro_create.argtypes = [ctypes.c_int]
+        L.oracle_dattorro_destroy.argtypes = [ctypes.c_void_p]
+        L.oracle_dattorro_set.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _F]
+        L.oracle_dattorro_process.argtypes = [ctypes.c_void_p, _PF, ctypes.c_int, _PF, ctypes.c_int, ctypes.c_int]
+        L.oracle_dattorro_state_floats.restype = ctypes.c_size_t
+        L.oracle_xorshift_noise.restype = ctypes.c_uint32
+        L.oracle_xorshift_noise.argtypes = [ctypes.c_uint32, _PF, ctypes.c_long, ctypes.c_long]
+        L.oracle_fnv1a64_lr.restype = ctypes.c_uint64
+        L.oracle_fnv1a64_lr.argtypes = [_PF, _PF, ctypes.c_long, ctypes.c_long]
+        L.oracle_cos2pi.restype = _F
+        L.oracle_cos2pi.argtypes = [_F]
+        L.oracle_chorus_create.restype = ctypes.c_void_p
+        L.oracle_chorus_create.argtypes = [ctypes.c_int, _F, ctypes.c_int]
+        L.oracle_chorus_destroy.argtypes = [ctypes.c_void_p]
+        L.oracle_chorus_set.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _F]
+        L.oracle_chorus_process.argtypes = [ctypes.c_void_p, _PF, _PF, ctypes.c_int, ctypes.c_int]
+        L.oracle_voice_create.restype = ctypes.c_void_p
+        L.oracle_voice_create.argtypes = [ctypes.c_int, _F]
+        L.oracle_voice_destroy.argtypes = [ctypes.c_void_p]
+        L.oracle_voice_config.argtypes = [ctypes.c_void_p, ctypes.c_int, _PF]
+        L.oracle_voice_note.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oracle_voice_process.argtypes = [ctypes.c_void_p, _PF, ctypes.c_int, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def ref_available(o0: bool = False) -> bool:
+    return os.path.exists(REF_LIB_O0 if o0 else REF_LIB)
+
+
+def ref_lib(o0: bool = False) -> ctypes.CDLL:
+    path = REF_LIB_O0 if o0 else REF_LIB
+    if path not in _ref:
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} not built (needs /root/reference at build time)")
+        L = ctypes.CDLL(path)
+        L.ref_verb_create.restype = ctypes.c_void_p
+        L.ref_verb_create.argtypes = [ctypes.c_int]
+        L.ref_verb_destroy.argtypes = [ctypes.c_void_p]
+        L.ref_verb_set.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _F]
+        L.ref_verb_process.argtypes = [ctypes.c_void_p, _PF, ctypes.c_int, _PF, ctypes.c_int, ctypes.c_int]
+        _ref[path] = L
+    return _ref[path]
+
+
+def _pf(a: np.ndarray):
+    assert a.dtype == np.float32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_PF)
+
+
+def xorshift_noise(seed: int, n: int) -> np.ndarray:
+    out = np.empty(n, dtype=np.float32)
+    lib().oracle_xorshift_noise(seed & 0xFFFFFFFF, _pf(out), n, 1)
+    return out
+
+
+def fnv1a64_lr(l: np.ndarray, r: np.ndarray) -> int:
+    l = np.ascontiguousarray(l, dtype=np.float32)
+    r = np.ascontiguousarray(r, dtype=np.float32)
+    return int(lib().oracle_fnv1a64_lr(_pf(l), _pf(r), len(l), 1))
+
+
+def instance_seed(i: int, c: int) -> int:
+    """SURVEY.md section 8d per-(instance, channel) seed."""
+    return ((0x9E3779B9 ^ (((2 * i + c + 1) * 0x85EBCA6B) & 0xFFFFFFFF)) | 1) & 0xFFFFFFFF
+
+
+class _Bank:
+    """Common shape: process(in [ch][frames][n]) -> out [och][frames][n]."""
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Dattorro(_Bank):
+    """The C restatement (ref=False) or the real reference (ref=True) for n instances."""
+
+    def __init__(self, n: int, ref: bool = False, o0: bool = False):
+        self.n = n
+        self.ref = ref
+        if ref:
+            self.L = ref_lib(o0)
+            self.h = self.L.ref_verb_create(n)
+        else:
+            self.L = lib()
+            self.h = self.L.oracle_dattorro_create(n)
+        assert self.h
+
+    def close(self):
+        if getattr(self, "h", None):
+            (self.L.ref_verb_destroy if self.ref else self.L.oracle_dattorro_destroy)(self.h)
+            self.h = None
+
+    def set(self, inst: int, field, value: float) -> None:
+        f = DT_FIELDS.index(field) if isinstance(field, str) else int(field)
+        rc = (self.L.ref_verb_set if self.ref else self.L.oracle_dattorro_set)(self.h, inst, f, value)
+        assert rc == 0
+
+    def process(self, x: np.ndarray, threads: int = 1) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        ch, frames, n = x.shape
+        assert n == self.n and ch in (1, 2)
+        out = np.empty((2, frames, n), dtype=np.float32)
+        fn = self.L.ref_verb_process if self.ref else self.L.oracle_dattorro_process
+        assert fn(self.h, _pf(x), ch, _pf(out), frames, threads) == 0
+        return out
+
+
+class Chorus(_Bank):
+    """mode 0 = stereo chorus, 1 = pitch-shift stage (fields 'pitch' = shift Hz, 'window')."""
+
+    def __init__(self, n: int, sample_rate: float = 48000.0, mode: int = 0):
+        self.n = n
+        self.L = lib()
+        self.h = self.L.oracle_chorus_create(n, sample_rate, mode)
+        assert self.h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.oracle_chorus_destroy(self.h)
+            self.h = None
+
+    def set(self, inst: int, field, value: float) -> None:
+        f = CH_FIELDS.index(field) if isinstance(field, str) else int(field)
+        assert self.L.oracle_chorus_set(self.h, inst, f, value) == 0
+
+    def process(self, x: np.ndarray, threads: int = 1) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        ch, frames, n = x.shape
+        assert ch == 2 and n == self.n
+        out = np.empty_like(x)
+        assert self.L.oracle_chorus_process(self.h, _pf(x), _pf(out), frames, threads) == 0
+        return out
+
+
+class Voice(_Bank):
+    def __init__(self, n: int, sample_rate: float = 48000.0):
+        self.n = n
+        self.L = lib()
+        self.h = self.L.oracle_voice_create(n, sample_rate)
+        assert self.h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.oracle_voice_destroy(self.h)
+            self.h = None
+
+    def config(self, inst: int, values) -> None:
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.float32))
+        assert v.shape == (len(VC_FIELDS),)
+        assert self.L.oracle_voice_config(self.h, inst, _pf(v)) == 0
+
+    def note(self, inst: int, on: bool, note: int = 60) -> None:
+        assert self.L.oracle_voice_note(self.h, inst, int(bool(on)), int(note)) == 0
+
+    def process(self, frames: int, threads: int = 1) -> np.ndarray:
+        out = np.empty((1, frames, self.n), dtype=np.float32)
+        assert self.L.oracle_voice_process(self.h, _pf(out), frames, threads) == 0
+        return out

@@ -1,0 +1,247 @@
+/*
+ * oracle/voice_ref.c -- CPU oracle for the synthlib SynthVoice (osc + 2 ADSR + SVF + portamento).
+ *
+ * TEST INFRASTRUCTURE ONLY (tests/, smoke(), bench.py cpu_baseline).  Never part of the product.
+ *
+ * Parity status: UNPINNED for the DaisySP arithmetic.  The voice composition is in-tree and
+ * restated literally from modules/synthlib/SynthVoice.h:31-53 (Init/Process), :55-98
+ * (UpdateConfig/Update), :245-256 (NoteOn/NoteOff), Portamento.h:12-42 (in-tree daisysp::Port
+ * stub), but the primitives are the third-party module DaisySP (pinned only as "commit": "master"
+ * in submodules.json:74-80, fork URL .gitmodules:4-6), which is not vendored and not in this
+ * container.  Its published algorithm is restated here:
+ *   daisysp::Oscillator (WAVE_POLYBLEP_SAW, normalised phase, amp 0.5),
+ *   daisysp::Adsr (Init(sr, 1), SetAttackTime(t, shape), SetTimeConstant, Process(gate), Retrigger),
+ *   daisysp::Svf (double-sampled Chamberlin, SetFreq/SetRes/SetDrive, Low()),
+ *   daisysp::mtof.
+ * The only reference pins at this boundary are qualitative (synth_test.cpp:102-148: first sample
+ * after NoteOn/NoteOff/NoteOn is exactly 0, later != 0 and != 1; amp_env_amount 0 -> 0) and are
+ * reproduced by tests/test_oracle.py.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include "oracle.h"
+
+enum { SEG_IDLE = 0, SEG_ATTACK = 1, SEG_DECAY = 2, SEG_RELEASE = 3 };
+
+typedef struct {
+    float x, atk_d0, atk_tgt, dec_d0, rel_d0, sus;
+    int mode, gate_prev;
+} adsr_t;
+
+typedef struct {
+    /* oscillator */
+    float phase, sr_recip;
+    /* svf */
+    float sr, fc_max, res, pre_drive, drive, low, band;
+    /* port */
+    float port_coef, port_z;
+    adsr_t amp_env, filt_env;
+    /* voice members (SynthVoice.h:276-315) */
+    float freq, amp_env_amount, filter_cutoff, filter_env_amount;
+    int gate;
+} voice_t;
+
+struct oracle_voice {
+    int n;
+    float sr;
+    voice_t *v;
+    float *params;    /* [n][OVC_NPARAMS] SynthVoice members (Config order) */
+};
+
+/* daisysp::Adsr setters */
+static void adsr_attack(adsr_t *e, float T, float shape, float sr)
+{
+    float target = 9.f * powf(shape, 10.f) + 0.3f * shape + 1.01f;
+    e->atk_tgt = target;
+    if (T > 0.f) {
+        float logTarget = logf(1.f - (1.f / target));
+        e->atk_d0 = 1.f - expf(logTarget / (T * sr));
+    } else {
+        e->atk_d0 = 1.f;
+    }
+}
+static float adsr_tc(float T, float sr)
+{
+    if (T > 0.f) {
+        const float target = logf((float)(1. / M_E));
+        return 1.f - expf(target / (T * sr));
+    }
+    return 1.f;
+}
+static float adsr_sus(float s) { return (s <= 0.f) ? -0.01f : (s > 1.f ? 1.f : s); }
+
+static void adsr_init(adsr_t *e, float sr)
+{
+    memset(e, 0, sizeof(*e));
+    e->sus = 0.7f;
+    e->mode = SEG_IDLE;
+    adsr_attack(e, 0.1f, 0.0f, sr);
+    e->dec_d0 = adsr_tc(0.1f, sr);
+    e->rel_d0 = adsr_tc(0.1f, sr);
+}
+
+static float adsr_process(adsr_t *e, int gate)
+{
+    if (gate && !e->gate_prev) e->mode = SEG_ATTACK;
+    else if (!gate && e->gate_prev) e->mode = SEG_RELEASE;
+    e->gate_prev = gate;
+    float d0 = e->atk_d0;
+    if (e->mode == SEG_DECAY) d0 = e->dec_d0;
+    else if (e->mode == SEG_RELEASE) d0 = e->rel_d0;
+    float target = e->mode == SEG_DECAY ? e->sus : -0.01f;
+    float out = 0.0f;
+    switch (e->mode) {
+    case SEG_ATTACK:
+        e->x += d0 * (e->atk_tgt - e->x);
+        out = e->x;
+        if (out > 1.f) { e->x = out = 1.f; e->mode = SEG_DECAY; }
+        break;
+    case SEG_DECAY:
+    case SEG_RELEASE:
+        e->x += d0 * (target - e->x);
+        out = e->x;
+        if (out < 0.0f) { e->x = out = 0.f; e->mode = SEG_IDLE; }
+        break;
+    default: break;
+    }
+    return out;
+}
+
+static float polyblep(float dt, float t)
+{
+    if (t < dt) { t /= dt; return t + t - t * t - 1.0f; }
+    else if (t > 1.0f - dt) { t = (t - 1.0f) / dt; return t * t + t + t + 1.0f; }
+    return 0.0f;
+}
+
+static float fclampf(float in, float mn, float mx) { return fminf(fmaxf(in, mn), mx); }
+#define MINF(a, b) ((a) < (b) ? (a) : (b))
+
+static void voice_init(voice_t *v, float sr)
+{
+    memset(v, 0, sizeof(*v));
+    v->sr_recip = 1.0f / sr;                        /* Oscillator::Init */
+    v->sr = sr; v->fc_max = sr / 3.f;               /* Svf::Init */
+    v->res = 0.5f; v->pre_drive = 0.5f; v->drive = 0.5f;
+    adsr_init(&v->amp_env, sr);                     /* SynthVoice::Init: Init(sr, 1) x2 */
+    adsr_init(&v->filt_env, sr);
+    v->port_coef = expf(-1.0f / (0.0f * sr));       /* Port::Init(sr, htime = 0) */
+    v->amp_env_amount = 0.8f;
+    v->filter_cutoff = 0.0f;
+    v->filter_env_amount = 1.0f;
+}
+
+/* SynthVoice::UpdateConfig -> Update (SynthVoice.h:55-98) */
+static void voice_update(voice_t *v, const float *p, float sr)
+{
+    v->filter_cutoff = p[OVC_FILTER_CUTOFF];
+    v->filter_env_amount = p[OVC_FILTER_ENV_AMOUNT];
+    v->amp_env_amount = p[OVC_AMP_ENV_AMOUNT];
+    /* Svf::SetRes, Svf::SetDrive */
+    v->res = fclampf(p[OVC_FILTER_RESONANCE], 0.f, 1.f);
+    v->drive = v->pre_drive * v->res;
+    v->pre_drive = fclampf(p[OVC_FILTER_DRIVE] * 0.1f, 0.f, 1.f);
+    v->drive = v->pre_drive * v->res;
+    adsr_attack(&v->filt_env, p[OVC_FILTER_ATTACK], p[OVC_FILTER_ATTACK_SHAPE], sr);
+    v->filt_env.dec_d0 = adsr_tc(p[OVC_FILTER_DECAY], sr);
+    v->filt_env.sus = adsr_sus(p[OVC_FILTER_SUSTAIN]);
+    v->filt_env.rel_d0 = adsr_tc(p[OVC_FILTER_RELEASE], sr);
+    adsr_attack(&v->amp_env, p[OVC_AMP_ATTACK], p[OVC_AMP_ATTACK_SHAPE], sr);
+    v->amp_env.dec_d0 = adsr_tc(p[OVC_AMP_DECAY], sr);
+    v->amp_env.sus = adsr_sus(p[OVC_AMP_SUSTAIN]);
+    v->amp_env.rel_d0 = adsr_tc(p[OVC_AMP_RELEASE], sr);
+    v->port_coef = expf(-1.0f / (p[OVC_PORTAMENTO] * sr));
+}
+
+static float voice_tick(voice_t *v)
+{
+    float amp = adsr_process(&v->amp_env, v->gate);
+    amp *= v->amp_env_amount;
+    /* Port::Process, Oscillator::SetFreq */
+    v->port_z = v->freq + v->port_coef * (v->port_z - v->freq);
+    const float inc = v->port_z * v->sr_recip;
+    /* Oscillator::Process (WAVE_POLYBLEP_SAW) */
+    float o = (2.0f * v->phase) - 1.0f;
+    o -= polyblep(inc, v->phase);
+    o *= -1.0f;
+    v->phase += inc;
+    if (v->phase > 1.0f) v->phase -= 1.0f;
+    const float src = o * 0.5f;
+    /* filter envelope -> Svf::SetFreq */
+    const float fc_in = v->filter_cutoff + ((adsr_process(&v->filt_env, v->gate) * 20000) * v->filter_env_amount);
+    const float fc = fclampf(fc_in, 1.0e-6f, v->fc_max);
+    const float fq = 2.0f * sinf(3.1415927410125732f * MINF(0.25f, fc / (v->sr * 2.0f)));
+    const float damp = MINF(2.0f * (1.0f - powf(v->res, 0.25f)), MINF(2.0f, 2.0f / fq - fq * 0.5f));
+    /* Svf::Process + Low() */
+    float notch = src - damp * v->band;
+    v->low = v->low + fq * v->band;
+    float high = notch - v->low;
+    v->band = fq * high + v->band - v->drive * v->band * v->band * v->band;
+    float out_low = 0.5f * v->low;
+    notch = src - damp * v->band;
+    v->low = v->low + fq * v->band;
+    high = notch - v->low;
+    v->band = fq * high + v->band - v->drive * v->band * v->band * v->band;
+    out_low += 0.5f * v->low;
+    return out_low * amp;
+}
+
+oracle_voice *oracle_voice_create(int n_inst, float sample_rate)
+{
+    if (n_inst <= 0) return NULL;
+    oracle_voice *o = (oracle_voice *)calloc(1, sizeof(*o));
+    if (!o) return NULL;
+    o->n = n_inst;
+    o->sr = sample_rate;
+    o->v = (voice_t *)calloc((size_t)n_inst, sizeof(voice_t));
+    o->params = (float *)calloc((size_t)n_inst * OVC_NPARAMS, sizeof(float));
+    if (!o->v || !o->params) { oracle_voice_destroy(o); return NULL; }
+    for (int i = 0; i < n_inst; i++) voice_init(&o->v[i], sample_rate);
+    return o;
+}
+
+void oracle_voice_destroy(oracle_voice *o)
+{
+    if (!o) return;
+    free(o->v); free(o->params); free(o);
+}
+
+/* values: [OVC_NPARAMS] = a full Voice::Config (UpdateConfig semantics) */
+int oracle_voice_config(oracle_voice *o, int inst, const float *values)
+{
+    if (!o || inst < 0 || inst >= o->n || !values) return -1;
+    memcpy(o->params + (size_t)inst * OVC_NPARAMS, values, sizeof(float) * OVC_NPARAMS);
+    voice_update(&o->v[inst], values, o->sr);
+    return 0;
+}
+
+int oracle_voice_note(oracle_voice *o, int inst, int on, int note)
+{
+    if (!o || inst < 0 || inst >= o->n) return -1;
+    voice_t *v = &o->v[inst];
+    if (on) {
+        v->gate = 1;
+        v->freq = powf(2.f, ((float)note - 69.0f) / 12.0f) * 440.0f;
+        v->amp_env.mode = SEG_ATTACK; v->amp_env.x = 0.f;     /* Retrigger(true) */
+        v->filt_env.mode = SEG_ATTACK; v->filt_env.x = 0.f;
+    } else {
+        v->gate = 0;
+    }
+    return 0;
+}
+
+/* out [n_frames][n] */
+int oracle_voice_process(oracle_voice *o, float *out, int n_frames, int n_threads)
+{
+    if (!o || n_frames < 0) return -1;
+    const long n = o->n;
+    (void)n_threads;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) num_threads(n_threads > 0 ? n_threads : 1)
+#endif
+    for (long i = 0; i < n; i++)
+        for (int f = 0; f < n_frames; f++) out[(long)f * n + i] = voice_tick(&o->v[i]);
+    return 0;
+}

@@ -1,0 +1,341 @@
+"""GPU parity: the HIP kernels (through the C-ABI) against the CPU oracle and the golden fixtures.
+
+Bars: dattorro, chorus, pitch-shift and the chain are BIT-EXACT (integer-exact fp32 sequence,
+-ffp-contract=off on both sides); the voice is within rel 1e-5 of max(|ref|, rms(ref)) because
+Svf::SetFreq calls sinf every sample (device ocml vs host glibc may differ by an ulp).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import (bits_equal, chorus_params, dt_params, fast_noise, first_mismatch, noise_block,
+                     rel_err, voice_configs)
+
+pytestmark = pytest.mark.gpu
+
+VOICE_TOL = 1e-5
+
+
+def engine(kind, n, **kw):
+    import ol_dsp_amd as ofx
+    return ofx.Engine(kind, n, **kw)
+
+
+def run_gpu(eng, x: np.ndarray, blocks, cuda):
+    """Feed x [ch][frames][n] block by block through device buffers; return host array."""
+    import torch
+    outs = []
+    f0 = 0
+    for b in blocks:
+        xb = torch.from_numpy(np.ascontiguousarray(x[:, f0:f0 + b])).to(cuda)
+        outs.append(eng.process(xb).cpu().numpy())
+        f0 += b
+    torch.cuda.synchronize()
+    return np.concatenate(outs, axis=1)
+
+
+# ------------------------------------------------------------------------------------ dattorro
+def test_dattorro_impulse_golden(cuda, golden):
+    e = engine("dattorro", 1)
+    x = np.zeros((2, 48000, 1), np.float32)
+    x[:, 0, 0] = 1.0                               # (1+1)/2 = 1: the mono C-API impulse
+    y = run_gpu(e, x, [256] * 187 + [128], cuda)
+    import os
+    first = np.load(os.path.join(os.path.dirname(__file__), "golden", "dattorro_impulse_4096.npy"))
+    assert bits_equal(y[:, :4096, 0], first), first_mismatch(y[:, :4096, 0], first)
+    g = golden["dattorro_impulse"]
+    assert f"{O.fnv1a64_lr(y[0, :, 0], y[1, :, 0]):016x}" == g["fnv1a64"]
+
+
+def test_dattorro_noise_10s_kat(cuda, golden):
+    g = golden["dattorro_noise_10s"]
+    x1 = O.xorshift_noise(g["seed"], g["frames"])
+    x = np.stack([x1, x1])[:, :, None]
+    e = engine("dattorro", 1)
+    y = run_gpu(e, x, [4096] * 117 + [768], cuda)
+    assert f"{O.fnv1a64_lr(y[0, :, 0], y[1, :, 0]):016x}" == g["fnv1a64"]
+
+
+def test_dattorro_reference_sweeps(cuda, golden):
+    """Hashes produced by the REAL reference (oracle/_ref) for random params, 4 pre-delays."""
+    for g in golden["dattorro_sweep"]:
+        p = np.asarray(g["params"], np.float32)
+        e = engine("dattorro", g["n"])
+        e.set_params(0, p)
+        x = noise_block(g["n"], g["frames"], g["input_base"])
+        frames = g["frames"]
+        blocks = [256] * (frames // 256) + ([frames % 256] if frames % 256 else [])
+        y = run_gpu(e, x, blocks, cuda)
+        got = [f"{O.fnv1a64_lr(y[0, :, i], y[1, :, i]):016x}" for i in range(g["n"])]
+        assert got == g["fnv1a64"], g["pre_delay"]
+
+
+@pytest.mark.parametrize("n", [1, 63, 300])
+def test_dattorro_ragged_vs_oracle(cuda, n):
+    rng = np.random.default_rng(n)
+    p = dt_params(rng, n, 0.1)
+    x = fast_noise(n, 1536, seed=n)
+    e = engine("dattorro", n)
+    e.set_params(0, p)
+    y = run_gpu(e, x, [256, 512, 4, 764], cuda)
+    ref = O.Dattorro(n)
+    for i in range(n):
+        for f in range(7):
+            ref.set(i, f, float(p[f, i]))
+    yr = ref.process(x, threads=8)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
+def test_dattorro_long_run_wraps(cuda):
+    """70,000 frames: the modulation turn at t = 32768 and the uint16 wrap of t at 65536."""
+    n = 64
+    rng = np.random.default_rng(3)
+    p = dt_params(rng, n, 0.25)
+    x = fast_noise(n, 70000, seed=9)
+    e = engine("dattorro", n)
+    e.set_params(0, p)
+    y = run_gpu(e, x, [4096] * 17 + [368], cuda)
+    ref = O.Dattorro(n)
+    for i in range(n):
+        for f in range(7):
+            ref.set(i, f, float(p[f, i]))
+    yr = ref.process(x, threads=8)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
+def test_dattorro_param_change_between_blocks(cuda):
+    n = 40
+    x = fast_noise(n, 1024, seed=4)
+    rng = np.random.default_rng(4)
+    p1, p2 = dt_params(rng, n, 0.0), dt_params(rng, n, 0.0)
+    e = engine("dattorro", n)
+    ref = O.Dattorro(n)
+    e.set_params(0, p1)
+    for i in range(n):
+        for f in range(7):
+            ref.set(i, f, float(p1[f, i]))
+    ya = run_gpu(e, x[:, :512], [512], cuda)
+    yra = ref.process(x[:, :512])
+    e.set_params(1, p2[1:])           # fields 1..6, keep pre-delay
+    for i in range(n):
+        for f in range(1, 7):
+            ref.set(i, f, float(p2[f, i]))
+    yb = run_gpu(e, x[:, 512:], [512], cuda)
+    yrb = ref.process(x[:, 512:])
+    assert bits_equal(np.concatenate([ya, yb], 1), np.concatenate([yra, yrb], 1))
+
+
+def test_dattorro_host_io_equals_device_io(cuda):
+    n = 100
+    x = fast_noise(n, 512, seed=5)
+    e1, e2 = engine("dattorro", n), engine("dattorro", n)
+    yd = run_gpu(e1, x, [512], cuda)
+    yh = e2.process(x)                      # numpy in/out: pinned staging inside libolfx
+    assert bits_equal(yd, yh)
+
+
+def test_dattorro_reset(cuda):
+    n = 8
+    x = fast_noise(n, 512, seed=6)
+    e = engine("dattorro", n)
+    a = run_gpu(e, x, [512], cuda)
+    e.reset()
+    b = run_gpu(e, x, [512], cuda)
+    assert bits_equal(a, b) and e.frames_processed == 512
+
+
+def test_dattorro_full_size_properties(cuda):
+    """65,536 instances (BASELINE config 3): sampled instances match the oracle exactly, and
+    instances sharing params and input produce identical output (checksum of checksums)."""
+    import torch
+    n, frames = 65536, 512
+    rng = np.random.default_rng(11)
+    p = dt_params(rng, n, 0.1)
+    p[:, 1::2] = p[:, 0:1]                        # odd instances clone instance 0's params
+    g = torch.Generator(device=cuda).manual_seed(0)
+    x = torch.rand((2, frames, n), generator=g, device=cuda) - 0.5
+    x[:, :, 1::2] = x[:, :, 0:1]                  # ... and its input
+    e = engine("dattorro", n)
+    e.set_params(0, p)
+    y = torch.cat([e.process(x[:, :256].contiguous()), e.process(x[:, 256:].contiguous())], 1)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    assert torch.equal(y[:, :, 1::2], y[:, :, 0:1].expand(-1, -1, n // 2))
+    idx = np.array([0, 2, 4097, 30000, 65534], np.int64)
+    xs = x[:, :, idx].cpu().numpy()
+    ref = O.Dattorro(len(idx))
+    for k, i in enumerate(idx):
+        for f in range(7):
+            ref.set(k, f, float(p[f, i]))
+    yr = ref.process(np.ascontiguousarray(xs))
+    assert bits_equal(y[:, :, idx].cpu().numpy(), yr)
+
+
+# ------------------------------------------------------------------------------- chorus / pitch
+@pytest.mark.parametrize("kind,mode", [("chorus", 0), ("pitchshift", 1)])
+def test_chorus_golden(cuda, golden, kind, mode):
+    g = golden[kind]
+    p = np.asarray(g["params"], np.float32)
+    e = engine(kind, g["n"])
+    if kind == "chorus":
+        e.set_params(0, p)
+    else:
+        e.set_params(0, p[[0, 7]])          # shift = pitch, window
+    x = noise_block(g["n"], g["frames"], g["input_base"])
+    y = run_gpu(e, x, [256] * (g["frames"] // 256) + [g["frames"] % 256], cuda)
+    got = [f"{O.fnv1a64_lr(y[0, :, i], y[1, :, i]):016x}" for i in range(g["n"])]
+    assert got == g["fnv1a64"]
+
+
+@pytest.mark.parametrize("n", [1, 200])
+def test_chorus_vs_oracle(cuda, n):
+    rng = np.random.default_rng(100 + n)
+    p = chorus_params(rng, n)
+    x = fast_noise(n, 4096, seed=n + 1)
+    e = engine("chorus", n)
+    e.set_params(0, p)
+    y = run_gpu(e, x, [256] * 8 + [2048], cuda)
+    ref = O.Chorus(n)
+    for i in range(n):
+        for f in range(8):
+            ref.set(i, f, float(p[f, i]))
+    yr = ref.process(x, threads=8)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
+def test_chorus_defaults_and_edges(cuda):
+    """RNBO defaults, params clamped to @min/@max (out-of-range values), mix 0 == dry."""
+    n = 5
+    e = engine("chorus", n)
+    ref = O.Chorus(n)
+    edits = [(1, "rate", 5.0), (2, "depth", 0.0), (3, "mix", 0.0), (4, "pitch", -2.0), (4, "q", 1.0)]
+    for i, f, v in edits:
+        e.set_param(i, f, v)
+        ref.set(i, f, v)
+    x = fast_noise(n, 2048, seed=3)
+    y = run_gpu(e, x, [1024, 1024], cuda)
+    assert bits_equal(y, ref.process(x))
+    assert bits_equal(y[:, :, 3], x[:, :, 3])
+
+
+def test_chorus_full_size_properties(cuda):
+    """65,536 chorus instances (BASELINE config 2): sampled instances exact vs oracle."""
+    import torch
+    n, frames = 65536, 512
+    rng = np.random.default_rng(12)
+    p = chorus_params(rng, n)
+    g = torch.Generator(device=cuda).manual_seed(1)
+    x = torch.rand((2, frames, n), generator=g, device=cuda) - 0.5
+    e = engine("chorus", n)
+    e.set_params(0, p)
+    y = torch.cat([e.process(x[:, :256].contiguous()), e.process(x[:, 256:].contiguous())], 1)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    idx = np.array([0, 1, 63, 64, 40000, 65535], np.int64)
+    ref = O.Chorus(len(idx))
+    for k, i in enumerate(idx):
+        for f in range(8):
+            ref.set(k, f, float(p[f, i]))
+    yr = ref.process(np.ascontiguousarray(x[:, :, idx].cpu().numpy()))
+    assert bits_equal(y[:, :, idx].cpu().numpy(), yr)
+
+
+# ------------------------------------------------------------------------------------- voice
+def _voice_pair(n, cfg, notes, on=True):
+    e = engine("voice", n)
+    ref = O.Voice(n)
+    if cfg is not None:
+        e.set_params(0, cfg)
+        for i in range(n):
+            ref.config(i, cfg[:, i])
+    if on:
+        e.note_events([(i, 1, notes[i]) for i in range(n)])
+        for i in range(n):
+            ref.note(i, True, notes[i])
+    return e, ref
+
+
+def _voice_run(e, frames, cuda):
+    import torch
+    out = torch.empty((1, frames, e.n), device=cuda)
+    e.process(None, out=out)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def test_voice_vs_oracle(cuda):
+    n = 256
+    rng = np.random.default_rng(21)
+    cfg = voice_configs(rng, n)
+    notes = [int(v) for v in rng.integers(36, 97, n)]
+    e, ref = _voice_pair(n, cfg, notes)
+    ya = np.concatenate([_voice_run(e, 256, cuda) for _ in range(8)], 1)
+    yra = ref.process(2048)
+    e.note_events([(i, 0, notes[i]) for i in range(n)])
+    for i in range(n):
+        ref.note(i, False, notes[i])
+    yb = np.concatenate([_voice_run(e, 256, cuda) for _ in range(8)], 1)
+    yrb = ref.process(2048)
+    y, yr = np.concatenate([ya, yb], 1), np.concatenate([yra, yrb], 1)
+    assert np.all(np.isfinite(y))
+    assert rel_err(y[0].T, yr[0].T) <= VOICE_TOL
+
+
+def test_voice_golden_and_pins(cuda, golden):
+    g = golden["voice"]
+    p = np.asarray(g["params"], np.float32)
+    e, _ = _voice_pair(g["n"], p, g["notes"])
+    ya = _voice_run(e, g["note_off_at"], cuda)
+    e.note_events([(i, 0, g["notes"][i]) for i in range(g["n"])])
+    yb = _voice_run(e, g["frames"] - g["note_off_at"], cuda)
+    y = np.concatenate([ya, yb], 1)
+    vo = O.Voice(g["n"])
+    for i in range(g["n"]):
+        vo.config(i, p[:, i])
+        vo.note(i, True, g["notes"][i])
+    yr = vo.process(g["note_off_at"])
+    for i in range(g["n"]):
+        vo.note(i, False, g["notes"][i])
+    yr = np.concatenate([yr, vo.process(g["frames"] - g["note_off_at"])], 1)
+    assert rel_err(y[0].T, yr[0].T) <= VOICE_TOL
+    # synth_test.cpp:102-148 pins, on the GPU: NoteOn, NoteOff, first sample == 0
+    e2 = engine("voice", 1)
+    e2.note_events([(0, 1, 60), (0, 0, 60)])
+    assert _voice_run(e2, 4, cuda)[0, 0, 0] == 0
+    e2.note_events([(0, 1, 60)])
+    v = _voice_run(e2, 4, cuda)[0, :, 0]
+    assert v[1] != 0 and v[1] != 1
+
+
+def test_voice_unconfigured_defaults(cuda):
+    """Init without Update: DaisySP defaults in envelopes and Svf (SynthVoice.h:31-39)."""
+    n = 4
+    notes = [40, 60, 72, 90]
+    e, ref = _voice_pair(n, None, notes)
+    y = np.concatenate([_voice_run(e, 512, cuda) for _ in range(4)], 1)
+    yr = ref.process(2048)
+    assert rel_err(y[0].T, yr[0].T) <= VOICE_TOL
+
+
+# ------------------------------------------------------------------------------------- chain
+def test_chain_vs_composed_oracle(cuda):
+    n = 96
+    rng = np.random.default_rng(31)
+    pc = chorus_params(rng, n)
+    pp = chorus_params(rng, n)[[0, 7]]
+    pd = dt_params(rng, n, 0.1)
+    p = np.concatenate([pc, pp, pd], 0)
+    x = fast_noise(n, 2048, seed=31)
+    e = engine("chain", n)
+    e.set_params(0, p)
+    y = run_gpu(e, x, [256] * 8, cuda)
+    c1, c2, d = O.Chorus(n), O.Chorus(n, mode=1), O.Dattorro(n)
+    for i in range(n):
+        for f in range(8):
+            c1.set(i, f, float(pc[f, i]))
+        c2.set(i, "pitch", float(pp[0, i]))
+        c2.set(i, "window", float(pp[1, i]))
+        for f in range(7):
+            d.set(i, f, float(pd[f, i]))
+    yr = d.process(c2.process(c1.process(x)))
+    assert bits_equal(y, yr), first_mismatch(y, yr)

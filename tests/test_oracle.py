@@ -1,0 +1,213 @@
+"""CPU tests: the oracle against the reference's golden vectors and the reference itself.
+
+Dattorro is PINNED: the C restatement must be bit-identical to the real reference
+(libs/dattorro-verb/verb.cpp, compiled into oracle/_ref by oracle/Makefile) and to the committed
+fixtures it produced.  Chorus / pitch-shift / voice are UNPINNED spec oracles: their fixtures
+freeze the restatement, and the voice reproduces the qualitative pins of
+test/synth_test.cpp:102-148.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import bits_equal, first_mismatch, noise_block
+
+
+# ---------------------------------------------------------------- dattorro, vs golden fixtures
+def test_dattorro_impulse_kats(golden):
+    imp = np.zeros((1, 48000, 1), np.float32)
+    imp[0, 0, 0] = 1.0
+    y = O.Dattorro(1).process(imp)
+    g = golden["dattorro_impulse"]
+    for n, (l, r) in g["kat"].items():
+        assert np.float32(y[0, int(n), 0]) == np.float32(l), n
+        assert np.float32(y[1, int(n), 0]) == np.float32(r), n
+    assert f"{O.fnv1a64_lr(y[0, :, 0], y[1, :, 0]):016x}" == g["fnv1a64"]
+    first = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden",
+                                                "dattorro_impulse_4096.npy"))
+    assert bits_equal(y[:, :4096, 0], first)
+
+
+def test_dattorro_impulse_matches_survey_values():
+    # SURVEY.md section 8c KAT values (measured there with g++ -O2 -ffp-contract=off)
+    kat = {1000: (-5.06734239e-07, -2.88859817e-23), 2000: (0.00382412504, -0.00750800269),
+           4800: (0.00366625283, 0.0275579803), 12800: (-0.00399901532, 0.00456911325),
+           20800: (-0.00629576156, -0.00478657521), 28800: (0.00383224664, -0.00649412163),
+           36800: (-0.00555869937, 0.000979059027), 44800: (-0.000748623977, 0.00146027002),
+           47999: (-0.0020442456, 0.00166539999)}
+    imp = np.zeros((1, 48000, 1), np.float32)
+    imp[0, 0, 0] = 1.0
+    y = O.Dattorro(1).process(imp)
+    for n in (0, 1, 479, 480, 481):
+        assert y[0, n, 0] == 0 and y[1, n, 0] == 0
+    for n, (l, r) in kat.items():
+        assert abs(y[0, n, 0] - l) <= 1e-8 * max(1.0, abs(l)) * 10 + abs(l) * 1e-8, n
+        assert abs(y[1, n, 0] - r) <= abs(r) * 1e-8 + 1e-12, n
+
+
+def test_dattorro_noise_10s_kat(golden):
+    g = golden["dattorro_noise_10s"]
+    x = O.xorshift_noise(g["seed"], g["frames"])
+    y = O.Dattorro(1).process(x[None, :, None])
+    assert f"{O.fnv1a64_lr(y[0, :, 0], y[1, :, 0]):016x}" == g["fnv1a64"]
+    s = float(np.sum(y[0, :, 0].astype(np.float64) ** 2))
+    assert s == pytest.approx(g["sum_l2"], rel=0, abs=0)
+    assert round(s, 3) == g["survey_sum_l2"]
+
+
+def test_dattorro_param_sweep_golden(golden):
+    for g in golden["dattorro_sweep"]:
+        p = np.asarray(g["params"], np.float32)
+        x = noise_block(g["n"], g["frames"], g["input_base"])
+        bank = O.Dattorro(g["n"])
+        for i in range(g["n"]):
+            for f in range(7):
+                bank.set(i, f, float(p[f, i]))
+        y = bank.process(x)
+        got = [f"{O.fnv1a64_lr(y[0, :, i], y[1, :, i]):016x}" for i in range(g["n"])]
+        assert got == g["fnv1a64"], g["pre_delay"]
+
+
+def test_dattorro_blocked_equals_unblocked():
+    """Streaming in 256-frame blocks == one long call (state carried exactly)."""
+    x = noise_block(3, 2048, 7)
+    a = O.Dattorro(3).process(x)
+    b = O.Dattorro(3)
+    y = np.concatenate([b.process(x[:, k:k + 256]) for k in range(0, 2048, 256)], axis=1)
+    assert bits_equal(a, y)
+
+
+# ---------------------------------------------------------------- dattorro, vs the reference itself
+ref = pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref not built (reference absent)")
+
+
+@ref
+def test_dattorro_port_equals_reference_random_params():
+    rng = np.random.default_rng(5)
+    n, frames = 16, 70000            # crosses t = 32768 (modulation turn) and the uint16 wrap
+    p = np.empty((7, n), np.float32)
+    p[0] = rng.uniform(0, 1, n)      # per-instance pre-delay is fine on the CPU
+    p[1:] = rng.uniform(0.05, 0.95, (6, n))
+    x = (rng.random((2, frames, n), dtype=np.float32) - 0.5)
+    banks = [O.Dattorro(n), O.Dattorro(n, ref=True)]
+    for b in banks:
+        for i in range(n):
+            for f in range(7):
+                b.set(i, f, float(p[f, i]))
+    ya, yb = (b.process(x, threads=4) for b in banks)
+    assert bits_equal(ya, yb), first_mismatch(ya, yb)
+
+
+@ref
+def test_dattorro_port_equals_reference_edge_params():
+    """Extremes of the setters: zero pre-delay, decay clamp both ends, zero/unit gains."""
+    cases = [[0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0],
+             [1.0, 0.0, 1.0, 1.0, 1.0, 1.0, 1.0],
+             [0.5, 0.5, 0.5, 0.5, 0.5, 0.1, 0.5],
+             [0.99, 0.9, 0.9, 0.9, 0.9, 0.99, 0.01]]
+    n = len(cases)
+    x = noise_block(n, 5000, 99)
+    banks = [O.Dattorro(n), O.Dattorro(n, ref=True)]
+    for b in banks:
+        for i, c in enumerate(cases):
+            for f, v in enumerate(c):
+                b.set(i, f, v)
+    ya, yb = (b.process(x) for b in banks)
+    assert np.all(np.isfinite(ya))
+    assert bits_equal(ya, yb), first_mismatch(ya, yb)
+
+
+@ref
+def test_dattorro_reference_O0_equals_O2():
+    x = noise_block(2, 3000, 3)
+    assert bits_equal(O.Dattorro(2, ref=True).process(x), O.Dattorro(2, ref=True, o0=True).process(x))
+
+
+def test_dattorro_empty_block():
+    b = O.Dattorro(2)
+    y = b.process(np.zeros((2, 0, 2), np.float32))
+    assert y.shape == (2, 0, 2)
+
+
+# ---------------------------------------------------------------- chorus / pitch-shift (unpinned)
+@pytest.mark.parametrize("key,mode", [("chorus", 0), ("pitchshift", 1)])
+def test_chorus_frozen_golden(golden, key, mode):
+    g = golden[key]
+    p = np.asarray(g["params"], np.float32)
+    x = noise_block(g["n"], g["frames"], g["input_base"])
+    ch = O.Chorus(g["n"], 48000.0, mode)
+    for i in range(g["n"]):
+        for f in range(8):
+            ch.set(i, f, float(p[f, i]))
+    y = ch.process(x)
+    assert [f"{O.fnv1a64_lr(y[0, :, i], y[1, :, i]):016x}" for i in range(g["n"])] == g["fnv1a64"]
+
+
+def test_cos2pi_accuracy():
+    xs = np.linspace(-3, 3, 20001).astype(np.float32)
+    got = np.array([O.lib().oracle_cos2pi(float(v)) for v in xs], np.float64)
+    assert np.max(np.abs(got - np.cos(2 * np.pi * xs.astype(np.float64)))) < 3e-7
+
+
+def test_chorus_behaviour():
+    """Mix 0 is exactly dry; pitch 0 makes the shifter a fixed W/2 delay; outputs finite."""
+    n = 3
+    x = noise_block(n, 4000, 11)
+    ch = O.Chorus(n)
+    ch.set(0, "mix", 0.0)
+    ch.set(1, "pitch", 0.0)
+    y = ch.process(x)
+    assert np.array_equal(y[:, :, 0], x[:, :, 0])
+    assert np.all(np.isfinite(y))
+    ps = O.Chorus(n, mode=1)   # pitch 0: taps at delay 1 (gain cos(-pi/2) ~ 0) and W/2 = 240 (gain 1)
+    yp = ps.process(x)
+    np.testing.assert_allclose(yp[:, 300:, 0], x[:, 300 - 240:4000 - 240, 0], atol=2e-6)
+
+
+def test_chorus_blocked_equals_unblocked():
+    x = noise_block(4, 2048, 21)
+    a = O.Chorus(4).process(x)
+    b = O.Chorus(4)
+    y = np.concatenate([b.process(x[:, k:k + 128]) for k in range(0, 2048, 128)], axis=1)
+    assert bits_equal(a, y)
+
+
+# ---------------------------------------------------------------- voice (unpinned) + reference pins
+def test_voice_frozen_golden(golden):
+    g = golden["voice"]
+    p = np.asarray(g["params"], np.float32)
+    vo = O.Voice(g["n"])
+    for i in range(g["n"]):
+        vo.config(i, p[:, i])
+        vo.note(i, True, g["notes"][i])
+    ya = vo.process(g["note_off_at"])
+    for i in range(g["n"]):
+        vo.note(i, False, g["notes"][i])
+    yb = vo.process(g["frames"] - g["note_off_at"])
+    y = np.concatenate([ya, yb], axis=1)
+    assert [f"{O.fnv1a64_lr(y[0, :, i], y[0, :, i]):016x}" for i in range(g["n"])] == g["fnv1a64"]
+
+
+def test_voice_reference_pins_synth_test():
+    """test/synth_test.cpp:102-148 (TEST(Synth, VoiceDefaultConstructor)), restated."""
+    vo = O.Voice(1)
+    # NoteOn, NoteOff, then first Process -> exactly 0 (first polyBLEP saw sample is 0)
+    vo.note(0, True, 60)
+    vo.note(0, False, 60)
+    assert vo.process(1)[0, 0, 0] == 0
+    vo.note(0, True, 60)
+    v = vo.process(2)[0, :, 0]
+    assert v[-1] != 0 and v[-1] != 1
+    # amp_env_amount = 0 -> 0; = 1 -> != 0
+    cfg = np.asarray(O.VOICE_DEFAULTS, np.float32)
+    cfg[O.VC_FIELDS.index("amp_env_amount")] = 0.0
+    vo.config(0, cfg)
+    assert vo.process(1)[0, 0, 0] == 0
+    cfg[O.VC_FIELDS.index("amp_env_amount")] = 1.0
+    vo.config(0, cfg)
+    assert vo.process(1)[0, 0, 0] != 0
+
+
+def test_voice_silent_until_note():
+    vo = O.Voice(2)
+    assert np.all(vo.process(512) == 0)
