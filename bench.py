@@ -147,7 +147,8 @@ def main():
     out = torch.empty((och, B, n), device=dev)
     if kind == "voice":   # NoteOn for every voice at block 0
         eng.note_events([(i, 1, 36 + (i * 7) % 61) for i in range(n)])
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)        # dedicated non-default stream: events see the kernels
+    torch.cuda.synchronize(dev)
 
     def step(k):
         eng.process(pool[k % pool_n], out=out, n_frames=B, stream=stream.cuda_stream)

@@ -158,13 +158,16 @@ int olfx_get_param(olfx_engine *e, uint32_t inst, uint32_t field, float *value);
 /* Queue note events (voices); applied in order at the start of the next olfx_process. */
 int olfx_note_events(olfx_engine *e, const olfx_event *ev, uint32_t n);
 
-/* Process n_frames (multiple of 4) for all instances.  `stream` is a hipStream_t (NULL = the
-   engine's own stream).  With OLFX_IO_DEVICE the call is asynchronous on that stream. */
+/* Process n_frames (multiple of 4) for all instances.  `stream` is a hipStream_t; NULL is the
+   HIP default (null) stream, as everywhere in HIP; olfx_stream(e) is the engine's own stream.
+   With OLFX_IO_DEVICE the call is asynchronous on that stream. */
 int olfx_process(olfx_engine *e, const float *in, float *out, uint32_t n_frames, int io_flags,
                  void *stream);
 
 /* Block until all work queued by this engine is done. */
 int olfx_sync(olfx_engine *e);
+/* The engine's own non-blocking hipStream_t (valid until olfx_destroy). */
+void *olfx_stream(const olfx_engine *e);
 
 /* Engine facts. */
 uint32_t olfx_num_instances(const olfx_engine *e);

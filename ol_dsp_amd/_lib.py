@@ -77,6 +77,7 @@ SIGNATURES = {
     "olfx_note_events": (ctypes.c_int, [_P, ctypes.POINTER(Event), _U32]),
     "olfx_process": (ctypes.c_int, [_P, _P, _P, _U32, ctypes.c_int, _P]),
     "olfx_sync": (ctypes.c_int, [_P]),
+    "olfx_stream": (_P, [_P]),
     "olfx_num_instances": (_U32, [_P]),
     "olfx_kind": (ctypes.c_int, [_P]),
     "olfx_frames_processed": (ctypes.c_uint64, [_P]),

@@ -784,7 +784,7 @@ int olfx_process(olfx_engine *e, const float *in, float *out, uint32_t n_frames,
     if (io_flags != OLFX_IO_DEVICE && io_flags != OLFX_IO_HOST)
         return e->fail(OLFX_E_ARG, "olfx_process: bad io_flags");
     HIPCHK(e, hipSetDevice(e->device));
-    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    hipStream_t s = (hipStream_t)stream;   // NULL = the HIP default (null) stream
     int rc = upload_params(e, s);
     if (rc) return rc;
     if (e->kind == OLFX_KIND_VOICE) {
@@ -820,6 +820,8 @@ int olfx_sync(olfx_engine *e) {
     HIPCHK(e, hipDeviceSynchronize());
     return OLFX_OK;
 }
+
+void *olfx_stream(const olfx_engine *e) { return e ? (void *)e->stream : nullptr; }
 
 uint32_t olfx_num_instances(const olfx_engine *e) { return e ? e->n : 0; }
 int olfx_kind(const olfx_engine *e) { return e ? e->kind : 0; }

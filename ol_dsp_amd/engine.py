@@ -138,8 +138,8 @@ class Engine:
 
         x: [in_ch][frames][n] torch CUDA tensor or numpy array (None for voices).
         out: optional preallocated output of the same kind; returned.
-        stream: hipStream_t as int (torch.cuda.Stream.cuda_stream) or None = torch's current
-        stream for tensors, the engine's stream for numpy.
+        stream: hipStream_t as int (torch.cuda.Stream.cuda_stream; 0 = the null stream) or
+        None = torch's current stream for tensors, the engine's own stream for numpy.
         """
         ich, och = self.info.in_channels, self.info.out_channels
         ref = x if x is not None else out
@@ -171,9 +171,11 @@ class Engine:
             assert xin.shape == (ich, n_frames, self.n), (xin.shape, (ich, n_frames, self.n))
         if out is None:
             out = np.empty((och, n_frames, self.n), dtype=np.float32)
+        if stream is None:
+            stream = self.lib.olfx_stream(self._h)
         check(self.lib.olfx_process(self._h, ctypes.c_void_p(xin.ctypes.data if xin is not None else 0),
                                     ctypes.c_void_p(out.ctypes.data), int(n_frames), _lib.IO_HOST,
-                                    ctypes.c_void_p(stream or 0)), self._h)
+                                    ctypes.c_void_p(stream)), self._h)
         return out
 
     def sync(self) -> None:
