@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libolfx.so")
+# OLFX_LIB may point at an experimental build of the same library (tools/, A/B timing only)
+LIB_PATH = os.environ.get("OLFX_LIB") or os.path.join(_HERE, "libolfx.so")
 
 # status codes (olfx.h)
 OLFX_OK = 0

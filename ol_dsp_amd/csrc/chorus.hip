@@ -12,12 +12,16 @@
 // Mapping: one lane = one (instance, channel); a 256-thread workgroup = 2 x 64 instances x 2
 // channels, channel-major per wave so audio I/O ([ch][frame][inst]) is 256-B coalesced.
 // Rings are lane-private and contiguous ([inst][ch][size]) because every tap is modulated per
-// instance.  The block is processed in chunks of 16 frames: per chunk each lane computes its 16
-// tap delays up front, then stages the <= 24-float window each of its 3 taps touches into LDS with
-// 6 x 16-B loads (the window moves ~1 position per frame, so consecutive chunks stream through the
-// ring), and the serial recurrence reads the taps from LDS.  LDS is laid out [slot][thread] so the
-// per-lane fractional reads are bank-conflict free.  Windows that cannot cover a chunk (the
-// pitch-shifter phasor wrap, once per 1/shift s) fall back to direct ring reads for that lane.
+// instance.  The block is processed in chunks of 16 frames.  Each tap of a chunk touches a window
+// of <= 24 consecutive ring positions (the pitch taps are monotone inside a chunk unless the
+// phasor wraps; the chorus tap moves < 0.6 positions per chunk for every legal depth/rate), so per
+// chunk a lane stages 3 windows = 18 x 16-B loads into LDS and the serial recurrence reads its
+// fractional taps from LDS ([slot][thread] layout: bank-conflict free).
+// Software pipeline (one chunk ahead): while chunk c computes, chunk c+1's inputs and windows are
+// already in flight; the few window positions that chunk c / c+1 themselves produce (inputs not yet
+// in the pitch ring, chorus outputs not yet in the chorus ring) are patched into LDS from
+// registers.  A pitch window that cannot cover its chunk (phasor wrap, once per 1/shift s) falls
+// back to direct ring reads for that lane and chunk.
 #include "olfx_internal.h"
 
 namespace olfx {
@@ -40,11 +44,56 @@ __device__ __forceinline__ void split_delay(float d, float dmin, float dmax, int
     fr = d - (float)u;
 }
 
+__device__ __forceinline__ int floor_delay(float d, float dmin, float dmax) {
+    return (int)(uint32_t)fminf(fmaxf(d, dmin), dmax);
+}
+
 __device__ __forceinline__ float lerp_pair(float x0, float x1, float fr) { return x0 + fr * (x1 - x0); }
+
+// Window geometry of one chunk for one lane: starts (relative to the chunk's first write
+// position, multiples of 4) of the two pitch windows and the chorus window.
+struct Plan {
+    int sA, sB, sC;
+    bool okA, okB;
+};
+
+__device__ __forceinline__ Plan plan_chunk(uint32_t lfo_acc, uint32_t lfo_inc, uint32_t lfo_off, uint32_t ps_acc,
+                                           uint32_t ps_inc, int C, float D, float W, float pmax, float cmax,
+                                           bool full) {
+    Plan p;
+    const uint32_t last = (uint32_t)(C - 1);
+    // pitch taps: d = p W is monotone in p; p is monotone over the chunk unless its phasor wraps
+    {
+        const uint32_t a0 = ps_acc, a1 = ps_acc + last * ps_inc;
+        const int d0 = floor_delay(unit24(a0) * W, 1.0f, pmax), d1 = floor_delay(unit24(a1) * W, 1.0f, pmax);
+        const int lo = -d1 - 1, hi = (int)last - d0;
+        p.sA = lo & ~3;
+        p.okA = a1 >= a0 && hi - p.sA < kWin;
+    }
+    {
+        const uint32_t a0 = ps_acc + 0x80000000u, a1 = a0 + last * ps_inc;
+        const int d0 = floor_delay(unit24(a0) * W, 1.0f, pmax), d1 = floor_delay(unit24(a1) * W, 1.0f, pmax);
+        const int lo = -d1 - 1, hi = (int)last - d0;
+        p.sB = lo & ~3;
+        p.okB = a1 >= a0 && hi - p.sB < kWin;
+    }
+    // chorus tap: |d'| <= 2 pi D f_lfo / sr <= 0.038 frame/frame for depth <= 12 ms, rate <= 0.5 Hz,
+    // so every frame of the chunk lies within +-1 of the endpoint delays
+    p.sC = 0;
+    if (full) {
+        const float e0 = cos2pi(unit24(lfo_acc + lfo_off)) * D + D;
+        const float e1 = cos2pi(unit24(lfo_acc + last * lfo_inc + lfo_off)) * D + D;
+        const int dlo = floor_delay(fminf(e0, e1) - 1.0f, 0.0f, cmax);
+        const int dhi = floor_delay(fmaxf(e0, e1) + 1.0f, 0.0f, cmax);
+        p.sC = (-dhi - 1) & ~3;
+        (void)dlo;
+    }
+    return p;
+}
 
 }  // namespace
 
-__global__ __launch_bounds__(kThreads, 2) void chorus_block_v2(ChorusArgs a) {
+__global__ __launch_bounds__(kThreads, 2) void chorus_block_v3(ChorusArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];   // [3 taps][kWin][kThreads]
     const uint32_t tid = threadIdx.x;
     const uint32_t g = blockIdx.x * kThreads + tid;
@@ -83,111 +132,125 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v2(ChorusArgs a) {
     float *wP1 = lds + 1 * kWin * kThreads + tid;
     float *wC = lds + 2 * kWin * kThreads + tid;
 
-    for (uint32_t f0 = 0; f0 < a.n_frames; f0 += kChunk) {
+    const uint32_t nf = a.n_frames;
+    // ---- prologue: chunk 0's inputs go to the pitch ring before its windows are loaded ----
+    float x[kChunk], xn[kChunk], psv[kChunk];
+    int C = (int)min((uint32_t)kChunk, nf);
+#pragma unroll
+    for (int k = 0; k < kChunk; ++k) x[k] = k < C ? in[(size_t)k * n] : 0.f;
+#pragma unroll
+    for (int k = 0; k < kChunk; k += 4)
+        if (k < C) *(float4 *)(pring + ((a.t0 + k) & pmask)) = make_float4(x[k], x[k + 1], x[k + 2], x[k + 3]);
+    Plan pl = plan_chunk(lfo_acc, lfo_inc, lfo_off, ps_acc, ps_inc, C, D, W, pmax, cmax, full);
+    float4 vA[kWin / 4], vB[kWin / 4], vC[kWin / 4];
+#pragma unroll
+    for (int m = 0; m < kWin / 4; ++m) {
+        vA[m] = *(const float4 *)(pring + ((a.t0 + pl.sA + 4 * m) & pmask));
+        vB[m] = *(const float4 *)(pring + ((a.t0 + pl.sB + 4 * m) & pmask));
+        if (full) vC[m] = *(const float4 *)(cring + ((a.t0 + pl.sC + 4 * m) & cmask));
+    }
+
+    for (uint32_t f0 = 0; f0 < nf; f0 += kChunk) {
         const uint32_t w0 = a.t0 + f0;
-        const int C = (int)min((uint32_t)kChunk, a.n_frames - f0);   // multiple of 4
+        C = (int)min((uint32_t)kChunk, nf - f0);            // multiple of 4
+        const Plan cur = pl;
 
-        // ---- inputs of the chunk, written to the pitch ring first (taps read delay >= 1) ----
-        float x[kChunk];
+        // ---- 1. staged windows -> LDS, patched with positions still held in registers ----
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k) x[k] = k < C ? in[(size_t)(f0 + k) * n] : 0.f;
+        for (int m = 0; m < kWin / 4; ++m) {
+            wP0[(4 * m + 0) * kThreads] = vA[m].x; wP0[(4 * m + 1) * kThreads] = vA[m].y;
+            wP0[(4 * m + 2) * kThreads] = vA[m].z; wP0[(4 * m + 3) * kThreads] = vA[m].w;
+            wP1[(4 * m + 0) * kThreads] = vB[m].x; wP1[(4 * m + 1) * kThreads] = vB[m].y;
+            wP1[(4 * m + 2) * kThreads] = vB[m].z; wP1[(4 * m + 3) * kThreads] = vB[m].w;
+            if (full) {
+                wC[(4 * m + 0) * kThreads] = vC[m].x; wC[(4 * m + 1) * kThreads] = vC[m].y;
+                wC[(4 * m + 2) * kThreads] = vC[m].z; wC[(4 * m + 3) * kThreads] = vC[m].w;
+            }
+        }
+        if (f0 > 0) {
+            // this chunk's inputs were not in the pitch ring when its windows were loaded
+            if (cur.sA > -kWin) {
 #pragma unroll
-        for (int k = 0; k < kChunk; k += 4)
-            if (k < C) *(float4 *)(pring + ((w0 + k) & pmask)) = make_float4(x[k], x[k + 1], x[k + 2], x[k + 3]);
+                for (int k = 0; k < kChunk; ++k)
+                    if (k < C && k - cur.sA < kWin) wP0[(k - cur.sA) * kThreads] = x[k];
+            }
+            if (cur.sB > -kWin) {
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k)
+                    if (k < C && k - cur.sB < kWin) wP1[(k - cur.sB) * kThreads] = x[k];
+            }
+            // nor were the previous chunk's pitch-shifter outputs in the chorus ring
+            if (full && cur.sC > -kWin - kChunk) {
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) {
+                    const int j = k - kChunk - cur.sC;
+                    if (j >= 0 && j < kWin) wC[j * kThreads] = psv[k];
+                }
+            }
+        }
+        // ---- 2. this chunk's inputs -> pitch ring (chunk 0 did it in the prologue) ----
+        if (f0 > 0) {
+#pragma unroll
+            for (int k = 0; k < kChunk; k += 4)
+                if (k < C) *(float4 *)(pring + ((w0 + k) & pmask)) = make_float4(x[k], x[k + 1], x[k + 2], x[k + 3]);
+        }
 
-        // ---- per-frame control signals of the chunk (LFO, phasor, window gains) ----
-        float dC[kChunk], dA[kChunk], dB[kChunk], gA[kChunk], gB[kChunk];
-        int loA = 1 << 30, hiA = -(1 << 30), loB = 1 << 30, hiB = -(1 << 30), loC = 1 << 30, hiC = -(1 << 30);
+        // ---- 3. issue the next chunk's input and window loads (consumed next iteration) ----
+        const uint32_t lfo_next = lfo_acc + (uint32_t)C * lfo_inc, ps_next = ps_acc + (uint32_t)C * ps_inc;
+        const bool more = f0 + kChunk < nf;
+        if (more) {
+            const int Cn = (int)min((uint32_t)kChunk, nf - f0 - kChunk);
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) xn[k] = k < Cn ? in[(size_t)(f0 + kChunk + k) * n] : 0.f;
+            pl = plan_chunk(lfo_next, lfo_inc, lfo_off, ps_next, ps_inc, Cn, D, W, pmax, cmax, full);
+            const uint32_t wn = w0 + kChunk;
+#pragma unroll
+            for (int m = 0; m < kWin / 4; ++m) {
+                vA[m] = *(const float4 *)(pring + ((wn + pl.sA + 4 * m) & pmask));
+                vB[m] = *(const float4 *)(pring + ((wn + pl.sB + 4 * m) & pmask));
+                if (full) vC[m] = *(const float4 *)(cring + ((wn + pl.sC + 4 * m) & cmask));
+            }
+        }
+
+        // ---- 4. the serial recurrence over this chunk ----
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) {
-            const float lfo = cos2pi(unit24(lfo_acc + lfo_off));
-            dC[k] = lfo * D + D;
-            const float p0 = unit24(ps_acc);
-            const float p1 = unit24(ps_acc + 0x80000000u);
-            gA[k] = cos2pi((p0 - 0.5f) * 0.5f);
-            gB[k] = cos2pi((p1 - 0.5f) * 0.5f);
-            dA[k] = p0 * W;
-            dB[k] = p1 * W;
             if (k < C) {
+                const float lfo = cos2pi(unit24(lfo_acc + lfo_off));
+                const float dch = lfo * D + D;
+                const float p0 = unit24(ps_acc);
+                const float p1 = unit24(ps_acc + 0x80000000u);
+                const float gA = cos2pi((p0 - 0.5f) * 0.5f);
+                const float gB = cos2pi((p1 - 0.5f) * 0.5f);
                 lfo_acc += lfo_inc;
                 ps_acc += ps_inc;
                 int di; float fr;
-                split_delay(dA[k], 1.0f, pmax, di, fr);
-                loA = min(loA, k - di - 1); hiA = max(hiA, k - di);
-                split_delay(dB[k], 1.0f, pmax, di, fr);
-                loB = min(loB, k - di - 1); hiB = max(hiB, k - di);
-                split_delay(dC[k], 0.0f, cmax, di, fr);
-                loC = min(loC, k - di - 1); hiC = max(hiC, k - di);
-            }
-        }
-        const int sA = loA & ~3, sB = loB & ~3, sC = loC & ~3;   // window starts rel. to w0
-        const bool okA = hiA - sA < kWin, okB = hiB - sB < kWin, okC = hiC - sC < kWin;
-
-        // ---- stage the tap windows into LDS (6 x 16 B each) ----
-        if (okA) {
-#pragma unroll
-            for (int m = 0; m < kWin; m += 4) {
-                const float4 v = *(const float4 *)(pring + ((w0 + sA + m) & pmask));
-                wP0[(m + 0) * kThreads] = v.x; wP0[(m + 1) * kThreads] = v.y;
-                wP0[(m + 2) * kThreads] = v.z; wP0[(m + 3) * kThreads] = v.w;
-            }
-        }
-        if (okB) {
-#pragma unroll
-            for (int m = 0; m < kWin; m += 4) {
-                const float4 v = *(const float4 *)(pring + ((w0 + sB + m) & pmask));
-                wP1[(m + 0) * kThreads] = v.x; wP1[(m + 1) * kThreads] = v.y;
-                wP1[(m + 2) * kThreads] = v.z; wP1[(m + 3) * kThreads] = v.w;
-            }
-        }
-        if (full && okC) {
-#pragma unroll
-            for (int m = 0; m < kWin; m += 4) {
-                const float4 v = *(const float4 *)(cring + ((w0 + sC + m) & cmask));
-                wC[(m + 0) * kThreads] = v.x; wC[(m + 1) * kThreads] = v.y;
-                wC[(m + 2) * kThreads] = v.z; wC[(m + 3) * kThreads] = v.w;
-            }
-        }
-
-        // ---- the serial recurrence over the chunk ----
-        float ps[kChunk];
-#pragma unroll
-        for (int k = 0; k < kChunk; ++k) {
-            if (k < C) {
-                int di; float fr;
                 float tA, tB;
-                split_delay(dA[k], 1.0f, pmax, di, fr);
-                if (okA) {
-                    const int j = k - di - sA;
+                split_delay(p0 * W, 1.0f, pmax, di, fr);
+                if (cur.okA) {
+                    const int j = k - di - cur.sA;
                     tA = lerp_pair(wP0[j * kThreads], wP0[(j - 1) * kThreads], fr);
                 } else {
                     const uint32_t q = w0 + k - di;
                     tA = lerp_pair(pring[q & pmask], pring[(q - 1u) & pmask], fr);
                 }
-                split_delay(dB[k], 1.0f, pmax, di, fr);
-                if (okB) {
-                    const int j = k - di - sB;
+                split_delay(p1 * W, 1.0f, pmax, di, fr);
+                if (cur.okB) {
+                    const int j = k - di - cur.sB;
                     tB = lerp_pair(wP1[j * kThreads], wP1[(j - 1) * kThreads], fr);
                 } else {
                     const uint32_t q = w0 + k - di;
                     tB = lerp_pair(pring[q & pmask], pring[(q - 1u) & pmask], fr);
                 }
-                const float p = tB * gB[k] + tA * gA[k];
-                ps[k] = p;
+                const float p = tB * gB + tA * gA;
+                psv[k] = p;
                 float y = p;
                 if (full) {
                     // delay~ writes before it reads: this frame's sample is visible at delay 0
-                    split_delay(dC[k], 0.0f, cmax, di, fr);
-                    float wet;
-                    if (okC) {
-                        if (k - sC < kWin) wC[(k - sC) * kThreads] = p;
-                        const int j = k - di - sC;
-                        wet = lerp_pair(wC[j * kThreads], wC[(j - 1) * kThreads], fr);
-                    } else {   // unreachable for |LFO slope| <= 0.04 frame/frame; kept exact
-                        cring[(w0 + k) & cmask] = p;
-                        const uint32_t q = w0 + k - di;
-                        wet = lerp_pair(cring[q & cmask], cring[(q - 1u) & cmask], fr);
-                    }
+                    if (k - cur.sC < kWin) wC[(k - cur.sC) * kThreads] = p;
+                    split_delay(dch, 0.0f, cmax, di, fr);
+                    const int j = k - di - cur.sC;
+                    const float wet = lerp_pair(wC[j * kThreads], wC[(j - 1) * kThreads], fr);
                     const float lp = b0 * wet + z1;
                     z1 = (b1 * wet - a1 * lp) + z2;
                     z2 = b2 * wet - a2 * lp;
@@ -195,14 +258,16 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v2(ChorusArgs a) {
                 }
                 out[(size_t)(f0 + k) * n] = y;
             } else {
-                ps[k] = 0.f;
+                psv[k] = 0.f;
             }
         }
         if (full) {
 #pragma unroll
             for (int k = 0; k < kChunk; k += 4)
-                if (k < C) *(float4 *)(cring + ((w0 + k) & cmask)) = make_float4(ps[k], ps[k + 1], ps[k + 2], ps[k + 3]);
+                if (k < C) *(float4 *)(cring + ((w0 + k) & cmask)) = make_float4(psv[k], psv[k + 1], psv[k + 2], psv[k + 3]);
         }
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k) x[k] = xn[k];
     }
 
     if (ch == 0) {
@@ -215,10 +280,11 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v2(ChorusArgs a) {
 
 hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
+    if (a.n_frames & 3u) return hipErrorInvalidValue;
     const uint32_t groups = (a.n + 63) / 64;            // 64-instance groups, 2 waves each
     const uint32_t blocks = (groups * 2 * 64 + kThreads - 1) / kThreads;
     const size_t lds = (size_t)3 * kWin * kThreads * sizeof(float);
-    hipLaunchKernelGGL(chorus_block_v2, dim3(blocks), dim3(kThreads), lds, s, a);
+    hipLaunchKernelGGL(chorus_block_v3, dim3(blocks), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 

@@ -81,31 +81,23 @@ struct DattorroArgs {
 
 // ----------------------------------------------------------------------------------------------
 // Deterministic cos(2*pi*x): used by the chorus LFO (RNBO cycle~) and the pitch-shifter
-// crossfade windows (gen~ cos).  Only +,-,*, rint and compares, evaluated in a fixed order, so the
-// host (oracle) and gfx950 produce identical bits under -ffp-contract=off.  |err| < 2e-7.
+// crossfade windows (gen~ cos).  Branch-free (selects only, no lane divergence): reduce to
+// b in [0, 1/4] exactly, then one Taylor polynomial of cos to theta^14 on [0, pi/2].  Only
+// +, -, *, rint and compares in a fixed order, so the host (oracle) and gfx950 produce identical
+// bits under -ffp-contract=off.  |err| < 3e-7.
 // ----------------------------------------------------------------------------------------------
 OLFX_HD float cos2pi(float x) {
-    float u = x - rintf(x);                 // exact, u in [-0.5, 0.5]
-    float a = u < 0.0f ? -u : u;            // cos is even
-    float sgn = 1.0f;
-    if (a > 0.25f) { a = 0.5f - a; sgn = -1.0f; }   // cos(2pi(1/2 - a)) = -cos(2pi a), exact
-    float r;
-    if (a <= 0.125f) {
-        float th = a * 6.28318530717958647692f;
-        float t2 = th * th;
-        // cos, Taylor to th^10 on [0, pi/4]
-        r = 1.0f + t2 * (-0.5f + t2 * (4.16666666666666666667e-2f + t2 * (-1.38888888888888888889e-3f +
-            t2 * (2.48015873015873015873e-5f + t2 * (-2.75573192239858906526e-7f)))));
-    } else {
-        float b = 0.25f - a;                // exact
-        float th = b * 6.28318530717958647692f;
-        float t2 = th * th;
-        // sin, Taylor to th^11 on [0, pi/4]
-        r = th * (1.0f + t2 * (-1.66666666666666666667e-1f + t2 * (8.33333333333333333333e-3f +
-            t2 * (-1.98412698412698412698e-4f + t2 * (2.75573192239858906526e-6f +
-            t2 * (-2.50521083854417187751e-8f))))));
-    }
-    return sgn * r;
+    const float u = x - rintf(x);                  // exact, u in [-0.5, 0.5]
+    const float a = u < 0.0f ? -u : u;             // cos is even
+    const bool hi = a > 0.25f;
+    const float b = hi ? 0.5f - a : a;             // exact (Sterbenz); cos(2pi(1/2-b)) = -cos(2pi b)
+    const float th = b * 6.28318530717958647692f;
+    const float t2 = th * th;
+    const float r = 1.0f + t2 * (-0.5f + t2 * (4.16666666666666666667e-2f +
+                    t2 * (-1.38888888888888888889e-3f + t2 * (2.48015873015873015873e-5f +
+                    t2 * (-2.75573192239858906526e-7f + t2 * (2.08767569878680989792e-9f +
+                    t2 * (-1.14707455977297247139e-11f)))))));
+    return hi ? -r : r;
 }
 
 // ----------------------------------------------------------------------------------------------

@@ -46,28 +46,21 @@ static uint32_t fix_inc(double hz, double sr)
 
 static float unit24(uint32_t acc) { return (float)(acc >> 8) * 5.9604644775390625e-8f; }
 
-/* cos(2 pi x) by reduction to [0, 1/8] and Taylor polynomials (identical op order on the GPU) */
+/* cos(2 pi x): reduce to b in [0, 1/4] (exact), one Taylor polynomial of cos to theta^14 on
+   [0, pi/2]; same operations in the same order as the GPU (spec choice) */
 float oracle_cos2pi(float x)
 {
-    float u = x - rintf(x);
-    float a = u < 0.0f ? -u : u;
-    float sgn = 1.0f;
-    if (a > 0.25f) { a = 0.5f - a; sgn = -1.0f; }
-    float r;
-    if (a <= 0.125f) {
-        float th = a * 6.28318530717958647692f;
-        float t2 = th * th;
-        r = 1.0f + t2 * (-0.5f + t2 * (4.16666666666666666667e-2f + t2 * (-1.38888888888888888889e-3f +
-            t2 * (2.48015873015873015873e-5f + t2 * (-2.75573192239858906526e-7f)))));
-    } else {
-        float b = 0.25f - a;
-        float th = b * 6.28318530717958647692f;
-        float t2 = th * th;
-        r = th * (1.0f + t2 * (-1.66666666666666666667e-1f + t2 * (8.33333333333333333333e-3f +
-            t2 * (-1.98412698412698412698e-4f + t2 * (2.75573192239858906526e-6f +
-            t2 * (-2.50521083854417187751e-8f))))));
-    }
-    return sgn * r;
+    const float u = x - rintf(x);
+    const float a = u < 0.0f ? -u : u;
+    const int hi = a > 0.25f;
+    const float b = hi ? 0.5f - a : a;
+    const float th = b * 6.28318530717958647692f;
+    const float t2 = th * th;
+    const float r = 1.0f + t2 * (-0.5f + t2 * (4.16666666666666666667e-2f +
+                    t2 * (-1.38888888888888888889e-3f + t2 * (2.48015873015873015873e-5f +
+                    t2 * (-2.75573192239858906526e-7f + t2 * (2.08767569878680989792e-9f +
+                    t2 * (-1.14707455977297247139e-11f)))))));
+    return hi ? -r : r;
 }
 
 typedef struct {

@@ -15,7 +15,8 @@ passes=(
   "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"
   "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
 )
-k=0
+if [ -n "${PASSES:-}" ]; then IFS=';' read -r -a passes <<< "$PASSES"; fi
+k=${PASS_BASE:-0}
 for p in "${passes[@]}"; do
   k=$((k+1))
   echo "== pass $k: $p"
