@@ -11,17 +11,23 @@
 //
 // Mapping: one lane = one (instance, channel); a 256-thread workgroup = 2 x 64 instances x 2
 // channels, channel-major per wave so audio I/O ([ch][frame][inst]) is 256-B coalesced.
-// Rings are lane-private and contiguous ([inst][ch][size]) because every tap is modulated per
+// Rings are instance-private and contiguous ([inst][ch][size]) because every tap is modulated per
 // instance.  The block is processed in chunks of 16 frames.  Each tap of a chunk touches a window
 // of <= 24 consecutive ring positions (the pitch taps are monotone inside a chunk unless the
-// phasor wraps; the chorus tap moves < 0.6 positions per chunk for every legal depth/rate), so per
-// chunk a lane stages 3 windows = 18 x 16-B loads into LDS and the serial recurrence reads its
-// fractional taps from LDS ([slot][thread] layout: bank-conflict free).
+// phasor wraps; the chorus tap moves < 0.6 positions per chunk for every legal depth/rate).
+//
+// Window staging is COOPERATIVE: a wave loads its 64 lanes' 3 x 64 windows (96 B each) with 18
+// wave-loads in which 6 consecutive lanes fetch one owner's contiguous window (the owners' window
+// starts are broadcast with ds_bpermute).  Each load instruction therefore touches ~11 contiguous
+// 96-B segments instead of 64 scattered 16-B pieces -- the per-lane pattern saturated the TA/TCP
+// with one L2 request per 16 B (profiles/r1: TA busy 87 %, TCP pending-stall 85 %).  The windows
+// land in LDS as [tap][slot][thread], which keeps the per-frame fractional reads of the serial
+// recurrence bank-conflict free (x0/x1 one ds_read2st64 apart).
 // Software pipeline (one chunk ahead): while chunk c computes, chunk c+1's inputs and windows are
-// already in flight; the few window positions that chunk c / c+1 themselves produce (inputs not yet
-// in the pitch ring, chorus outputs not yet in the chorus ring) are patched into LDS from
-// registers.  A pitch window that cannot cover its chunk (phasor wrap, once per 1/shift s) falls
-// back to direct ring reads for that lane and chunk.
+// in flight; window positions that chunk c / c+1 themselves produce (inputs not yet in the pitch
+// ring, chorus outputs not yet in the chorus ring) are patched into LDS from registers.  A pitch
+// window that cannot cover its chunk (phasor wrap, once per 1/shift s) falls back to direct ring
+// reads for that lane and chunk.
 #include "olfx_internal.h"
 
 namespace olfx {
@@ -30,7 +36,11 @@ namespace {
 
 constexpr int kChunk = 16;      // frames per chunk
 constexpr int kWin = 24;        // floats staged per tap window (6 x float4)
+constexpr int kParts = kWin / 4;
 constexpr int kThreads = 256;
+constexpr int kRow = 64;                    // LDS slot stride: one wave's lanes
+constexpr int kRegion = 3 * kWin * kRow;    // floats of LDS per wave (>= 64 lanes x 32 staging)
+static_assert(kRegion >= 64 * 32, "staging area must fit in the window region");
 
 __device__ __forceinline__ float unit24(uint32_t acc) {
     return (float)(acc >> 8) * 5.9604644775390625e-8f;   // exact: 24-bit fraction in [0,1)
@@ -83,25 +93,26 @@ __device__ __forceinline__ Plan plan_chunk(uint32_t lfo_acc, uint32_t lfo_inc, u
     if (full) {
         const float e0 = cos2pi(unit24(lfo_acc + lfo_off)) * D + D;
         const float e1 = cos2pi(unit24(lfo_acc + last * lfo_inc + lfo_off)) * D + D;
-        const int dlo = floor_delay(fminf(e0, e1) - 1.0f, 0.0f, cmax);
         const int dhi = floor_delay(fmaxf(e0, e1) + 1.0f, 0.0f, cmax);
         p.sC = (-dhi - 1) & ~3;
-        (void)dlo;
     }
     return p;
 }
 
 }  // namespace
 
-__global__ __launch_bounds__(kThreads, 2) void chorus_block_v3(ChorusArgs a) {
+__global__ __launch_bounds__(kThreads, 2) void chorus_block_v6(ChorusArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];   // [3 taps][kWin][kThreads]
     const uint32_t tid = threadIdx.x;
     const uint32_t g = blockIdx.x * kThreads + tid;
     const uint32_t wave = g >> 6, lane = g & 63u;
     const uint32_t ch = wave & 1u;
-    const uint32_t i = (wave >> 1) * 64u + lane;
-    if (i >= a.n) return;
+    const uint32_t inst0 = (wave >> 1) * 64u;          // first instance of this wave
     const uint32_t n = a.n;
+    if (inst0 >= n) return;                            // whole wave idle (wave-uniform)
+    const uint32_t i_raw = inst0 + lane;
+    const bool valid = i_raw < n;                      // invalid lanes still help load windows
+    const uint32_t i = valid ? i_raw : n - 1;
     const bool full = a.mode == 0;
 
     const uint32_t lfo_inc = a.coef[CHC_LFO_INC * n + i];
@@ -128,9 +139,70 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v3(ChorusArgs a) {
     float *cring = a.chorus_ring + ((size_t)i * 2 + ch) * a.csize;
     const float *in = a.in + (size_t)ch * a.n_frames * n + i;
     float *out = a.out + (size_t)ch * a.n_frames * n + i;
-    float *wP0 = lds + 0 * kWin * kThreads + tid;
-    float *wP1 = lds + 1 * kWin * kThreads + tid;
-    float *wC = lds + 2 * kWin * kThreads + tid;
+    // this wave's LDS region: windows [tap][slot][lane]; between uses it also stages ring stores
+    // as [lane][32] (x in 0..15, pitch-shifter outputs in 16..31)
+    float *region = lds + (tid >> 6) * kRegion;
+    float *wP0 = region + 0 * kWin * kRow + lane;
+    float *wP1 = region + 1 * kWin * kRow + lane;
+    float *wC = region + 2 * kWin * kRow + lane;
+    float *stage = region + lane * 32u;
+
+    // cooperative-load geometry: in part-load r (0..5) of a tap, this lane fetches float4 m of
+    // owner lane o's window, with 6 consecutive lanes covering one owner (compile-time r)
+    // (recomputed where used: cheap integer ops instead of 30+ live registers)
+    auto owner = [&](int r) { return ((uint32_t)r * 64u + lane) / kParts; };
+    auto piece = [&](int r) { return ((uint32_t)r * 64u + lane) % kParts; };
+    float4 vA[kParts], vB[kParts], vC[kParts];
+    auto load_windows = [&](const Plan &pl, uint32_t wpos) {
+#pragma unroll
+        for (int r = 0; r < kParts; ++r) {
+            const uint32_t o = owner(r), m4 = 4u * piece(r);
+            const int oA = __builtin_amdgcn_ds_bpermute((int)(o << 2), pl.sA);
+            const int oB = __builtin_amdgcn_ds_bpermute((int)(o << 2), pl.sB);
+            const int oC = __builtin_amdgcn_ds_bpermute((int)(o << 2), pl.sC);
+            const uint32_t oi = inst0 + o;
+            if (oi < n) {
+                const float *op = a.pitch_ring + ((size_t)oi * 2 + ch) * a.psize;
+                vA[r] = *(const float4 *)(op + ((wpos + oA + m4) & pmask));
+                vB[r] = *(const float4 *)(op + ((wpos + oB + m4) & pmask));
+                if (full) {
+                    const float *oc = a.chorus_ring + ((size_t)oi * 2 + ch) * a.csize;
+                    vC[r] = *(const float4 *)(oc + ((wpos + oC + m4) & cmask));
+                }
+            }
+        }
+    };
+    auto stage_windows = [&]() {
+#pragma unroll
+        for (int r = 0; r < kParts; ++r) {
+            float *pA = region + owner(r) + 4u * piece(r) * kRow;
+            float *pB = pA + kWin * kRow, *pC = pA + 2 * kWin * kRow;
+            pA[0] = vA[r].x; pA[kRow] = vA[r].y; pA[2 * kRow] = vA[r].z; pA[3 * kRow] = vA[r].w;
+            pB[0] = vB[r].x; pB[kRow] = vB[r].y; pB[2 * kRow] = vB[r].z; pB[3 * kRow] = vB[r].w;
+            if (full) {
+                pC[0] = vC[r].x; pC[kRow] = vC[r].y; pC[2 * kRow] = vC[r].z; pC[3 * kRow] = vC[r].w;
+            }
+        }
+    };
+    // Cooperative ring store of a chunk: every lane has staged its C consecutive samples at
+    // stage[base..base+C); 4 consecutive lanes then write one owner's 64 B with 16-B stores, so a
+    // store instruction covers 16 owners' contiguous runs instead of 64 scattered 16-B pieces.
+    auto coop_store = [&](bool pitch, uint32_t base, uint32_t wpos, int C) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t q = (uint32_t)r * 64u + lane, o = q >> 2, p4 = 4u * (q & 3u);
+            const float4 v = *(const float4 *)(region + o * 32u + base + p4);
+            const uint32_t oi = inst0 + o;
+            if (oi < n && (int)p4 < C) {
+                if (pitch) *(float4 *)(a.pitch_ring + ((size_t)oi * 2 + ch) * a.psize + ((wpos + p4) & pmask)) = v;
+                else *(float4 *)(a.chorus_ring + ((size_t)oi * 2 + ch) * a.csize + ((wpos + p4) & cmask)) = v;
+            }
+        }
+    };
+    auto stage_run = [&](const float (&v)[kChunk], uint32_t base) {
+#pragma unroll
+        for (int k = 0; k < kChunk; k += 4) *(float4 *)(stage + base + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+    };
 
     const uint32_t nf = a.n_frames;
     // ---- prologue: chunk 0's inputs go to the pitch ring before its windows are loaded ----
@@ -138,78 +210,54 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v3(ChorusArgs a) {
     int C = (int)min((uint32_t)kChunk, nf);
 #pragma unroll
     for (int k = 0; k < kChunk; ++k) x[k] = k < C ? in[(size_t)k * n] : 0.f;
-#pragma unroll
-    for (int k = 0; k < kChunk; k += 4)
-        if (k < C) *(float4 *)(pring + ((a.t0 + k) & pmask)) = make_float4(x[k], x[k + 1], x[k + 2], x[k + 3]);
+    stage_run(x, 0);
+    coop_store(true, 0, a.t0, C);
     Plan pl = plan_chunk(lfo_acc, lfo_inc, lfo_off, ps_acc, ps_inc, C, D, W, pmax, cmax, full);
-    float4 vA[kWin / 4], vB[kWin / 4], vC[kWin / 4];
-#pragma unroll
-    for (int m = 0; m < kWin / 4; ++m) {
-        vA[m] = *(const float4 *)(pring + ((a.t0 + pl.sA + 4 * m) & pmask));
-        vB[m] = *(const float4 *)(pring + ((a.t0 + pl.sB + 4 * m) & pmask));
-        if (full) vC[m] = *(const float4 *)(cring + ((a.t0 + pl.sC + 4 * m) & cmask));
-    }
+    load_windows(pl, a.t0);
 
     for (uint32_t f0 = 0; f0 < nf; f0 += kChunk) {
         const uint32_t w0 = a.t0 + f0;
         C = (int)min((uint32_t)kChunk, nf - f0);            // multiple of 4
         const Plan cur = pl;
 
-        // ---- 1. staged windows -> LDS, patched with positions still held in registers ----
-#pragma unroll
-        for (int m = 0; m < kWin / 4; ++m) {
-            wP0[(4 * m + 0) * kThreads] = vA[m].x; wP0[(4 * m + 1) * kThreads] = vA[m].y;
-            wP0[(4 * m + 2) * kThreads] = vA[m].z; wP0[(4 * m + 3) * kThreads] = vA[m].w;
-            wP1[(4 * m + 0) * kThreads] = vB[m].x; wP1[(4 * m + 1) * kThreads] = vB[m].y;
-            wP1[(4 * m + 2) * kThreads] = vB[m].z; wP1[(4 * m + 3) * kThreads] = vB[m].w;
-            if (full) {
-                wC[(4 * m + 0) * kThreads] = vC[m].x; wC[(4 * m + 1) * kThreads] = vC[m].y;
-                wC[(4 * m + 2) * kThreads] = vC[m].z; wC[(4 * m + 3) * kThreads] = vC[m].w;
-            }
+        // ---- 1. this chunk's inputs -> pitch ring (cooperative; chunk 0 did it in the prologue),
+        //         using the wave's LDS region while it is free ----
+        if (f0 > 0) {
+            stage_run(x, 0);
+            coop_store(true, 0, w0, C);
         }
+        // ---- 2. staged windows -> LDS, patched with positions still held in registers ----
+        stage_windows();
         if (f0 > 0) {
             // this chunk's inputs were not in the pitch ring when its windows were loaded
             if (cur.sA > -kWin) {
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k)
-                    if (k < C && k - cur.sA < kWin) wP0[(k - cur.sA) * kThreads] = x[k];
+                    if (k < C && k - cur.sA < kWin) wP0[(k - cur.sA) * kRow] = x[k];
             }
             if (cur.sB > -kWin) {
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k)
-                    if (k < C && k - cur.sB < kWin) wP1[(k - cur.sB) * kThreads] = x[k];
+                    if (k < C && k - cur.sB < kWin) wP1[(k - cur.sB) * kRow] = x[k];
             }
             // nor were the previous chunk's pitch-shifter outputs in the chorus ring
             if (full && cur.sC > -kWin - kChunk) {
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) {
                     const int j = k - kChunk - cur.sC;
-                    if (j >= 0 && j < kWin) wC[j * kThreads] = psv[k];
+                    if (j >= 0 && j < kWin) wC[j * kRow] = psv[k];
                 }
             }
-        }
-        // ---- 2. this chunk's inputs -> pitch ring (chunk 0 did it in the prologue) ----
-        if (f0 > 0) {
-#pragma unroll
-            for (int k = 0; k < kChunk; k += 4)
-                if (k < C) *(float4 *)(pring + ((w0 + k) & pmask)) = make_float4(x[k], x[k + 1], x[k + 2], x[k + 3]);
         }
 
         // ---- 3. issue the next chunk's input and window loads (consumed next iteration) ----
         const uint32_t lfo_next = lfo_acc + (uint32_t)C * lfo_inc, ps_next = ps_acc + (uint32_t)C * ps_inc;
-        const bool more = f0 + kChunk < nf;
-        if (more) {
+        if (f0 + kChunk < nf) {
             const int Cn = (int)min((uint32_t)kChunk, nf - f0 - kChunk);
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) xn[k] = k < Cn ? in[(size_t)(f0 + kChunk + k) * n] : 0.f;
             pl = plan_chunk(lfo_next, lfo_inc, lfo_off, ps_next, ps_inc, Cn, D, W, pmax, cmax, full);
-            const uint32_t wn = w0 + kChunk;
-#pragma unroll
-            for (int m = 0; m < kWin / 4; ++m) {
-                vA[m] = *(const float4 *)(pring + ((wn + pl.sA + 4 * m) & pmask));
-                vB[m] = *(const float4 *)(pring + ((wn + pl.sB + 4 * m) & pmask));
-                if (full) vC[m] = *(const float4 *)(cring + ((wn + pl.sC + 4 * m) & cmask));
-            }
+            load_windows(pl, w0 + kChunk);
         }
 
         // ---- 4. the serial recurrence over this chunk ----
@@ -229,7 +277,7 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v3(ChorusArgs a) {
                 split_delay(p0 * W, 1.0f, pmax, di, fr);
                 if (cur.okA) {
                     const int j = k - di - cur.sA;
-                    tA = lerp_pair(wP0[j * kThreads], wP0[(j - 1) * kThreads], fr);
+                    tA = lerp_pair(wP0[j * kRow], wP0[(j - 1) * kRow], fr);
                 } else {
                     const uint32_t q = w0 + k - di;
                     tA = lerp_pair(pring[q & pmask], pring[(q - 1u) & pmask], fr);
@@ -237,7 +285,7 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v3(ChorusArgs a) {
                 split_delay(p1 * W, 1.0f, pmax, di, fr);
                 if (cur.okB) {
                     const int j = k - di - cur.sB;
-                    tB = lerp_pair(wP1[j * kThreads], wP1[(j - 1) * kThreads], fr);
+                    tB = lerp_pair(wP1[j * kRow], wP1[(j - 1) * kRow], fr);
                 } else {
                     const uint32_t q = w0 + k - di;
                     tB = lerp_pair(pring[q & pmask], pring[(q - 1u) & pmask], fr);
@@ -247,29 +295,29 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v3(ChorusArgs a) {
                 float y = p;
                 if (full) {
                     // delay~ writes before it reads: this frame's sample is visible at delay 0
-                    if (k - cur.sC < kWin) wC[(k - cur.sC) * kThreads] = p;
+                    if (k - cur.sC < kWin) wC[(k - cur.sC) * kRow] = p;
                     split_delay(dch, 0.0f, cmax, di, fr);
                     const int j = k - di - cur.sC;
-                    const float wet = lerp_pair(wC[j * kThreads], wC[(j - 1) * kThreads], fr);
+                    const float wet = lerp_pair(wC[j * kRow], wC[(j - 1) * kRow], fr);
                     const float lp = b0 * wet + z1;
                     z1 = (b1 * wet - a1 * lp) + z2;
                     z2 = b2 * wet - a2 * lp;
                     y = x[k] * dry + lp * mix;
                 }
-                out[(size_t)(f0 + k) * n] = y;
+                if (valid) out[(size_t)(f0 + k) * n] = y;
             } else {
                 psv[k] = 0.f;
             }
         }
-        if (full) {
-#pragma unroll
-            for (int k = 0; k < kChunk; k += 4)
-                if (k < C) *(float4 *)(cring + ((w0 + k) & cmask)) = make_float4(psv[k], psv[k + 1], psv[k + 2], psv[k + 3]);
+        if (full) {   // the chunk's windows are dead: stage its pitch-shifter outputs, store cooperatively
+            stage_run(psv, 16);
+            coop_store(false, 16, w0, C);
         }
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) x[k] = xn[k];
     }
 
+    if (!valid) return;
     if (ch == 0) {
         a.state[CHS_LFO_ACC * n + i] = lfo_acc;
         a.state[CHS_PS_ACC * n + i] = ps_acc;
@@ -284,7 +332,7 @@ hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s) {
     const uint32_t groups = (a.n + 63) / 64;            // 64-instance groups, 2 waves each
     const uint32_t blocks = (groups * 2 * 64 + kThreads - 1) / kThreads;
     const size_t lds = (size_t)3 * kWin * kThreads * sizeof(float);
-    hipLaunchKernelGGL(chorus_block_v3, dim3(blocks), dim3(kThreads), lds, s, a);
+    hipLaunchKernelGGL(chorus_block_v6, dim3(blocks), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 

@@ -194,7 +194,7 @@ def test_chorus_vs_oracle(cuda, n):
     x = fast_noise(n, 4096, seed=n + 1)
     e = engine("chorus", n)
     e.set_params(0, p)
-    y = run_gpu(e, x, [256] * 8 + [2048], cuda)
+    y = run_gpu(e, x, [256] * 7 + [4, 12, 240, 2048], cuda)   # tails exercise chorus_tail
     ref = O.Chorus(n)
     for i in range(n):
         for f in range(8):
