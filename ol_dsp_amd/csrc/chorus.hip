@@ -16,13 +16,15 @@
 // of <= 24 consecutive ring positions (the pitch taps are monotone inside a chunk unless the
 // phasor wraps; the chorus tap moves < 0.6 positions per chunk for every legal depth/rate).
 //
-// Window staging is COOPERATIVE: a wave loads its 64 lanes' 3 x 64 windows (96 B each) with 18
-// wave-loads in which 6 consecutive lanes fetch one owner's contiguous window (the owners' window
-// starts are broadcast with ds_bpermute).  Each load instruction therefore touches ~11 contiguous
-// 96-B segments instead of 64 scattered 16-B pieces -- the per-lane pattern saturated the TA/TCP
-// with one L2 request per 16 B (profiles/r1: TA busy 87 %, TCP pending-stall 85 %).  The windows
-// land in LDS as [tap][slot][thread], which keeps the per-frame fractional reads of the serial
-// recurrence bank-conflict free (x0/x1 one ds_read2st64 apart).
+// Memory shape (profiles/r1): per-lane scattered 16-B accesses saturated the TA/TCP with one L2
+// request per 16 B (TA busy 87 %, TCP pending-stall 85 %), so both directions are COOPERATIVE:
+//   * window loads: 6 consecutive lanes fetch one owner's contiguous 96-B window (owners' window
+//     starts broadcast with ds_bpermute), ~11 contiguous segments per wave-load;
+//   * ring stores: each lane stages its 16 new samples in its wave's LDS region, then 4 lanes
+//     write one owner's 64-B run, 16 runs per wave-store.
+// Windows land in LDS as [wave][tap][slot][lane]: the per-frame fractional reads of the serial
+// recurrence are bank-conflict free (x0/x1 one ds_read2st64 apart).  All global traffic uses
+// buffer ops with 32-bit offsets (frame offsets in SGPRs): fewer VGPRs, no 64-bit address math.
 // Software pipeline (one chunk ahead): while chunk c computes, chunk c+1's inputs and windows are
 // in flight; window positions that chunk c / c+1 themselves produce (inputs not yet in the pitch
 // ring, chorus outputs not yet in the chorus ring) are patched into LDS from registers.  A pitch
@@ -34,13 +36,36 @@ namespace olfx {
 
 namespace {
 
-constexpr int kChunk = 16;      // frames per chunk
-constexpr int kWin = 24;        // floats staged per tap window (6 x float4)
+constexpr int kChunk = 16;                  // frames per chunk
+constexpr int kWin = 24;                    // floats staged per tap window (6 x float4)
 constexpr int kParts = kWin / 4;
 constexpr int kThreads = 256;
 constexpr int kRow = 64;                    // LDS slot stride: one wave's lanes
 constexpr int kRegion = 3 * kWin * kRow;    // floats of LDS per wave (>= 64 lanes x 32 staging)
 static_assert(kRegion >= 64 * 32, "staging area must fit in the window region");
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+__device__ __forceinline__ Rsrc rsrc(const void *p, uint64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0,
+                                             (int)(uint32_t)(bytes > 0xFFFFFFFFull ? 0xFFFFFFFFull : bytes), 0x00020000);
+}
+__device__ __forceinline__ float ld1(Rsrc r, uint32_t voff, uint32_t soff) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ void st1(Rsrc r, uint32_t voff, uint32_t soff, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
+}
+__device__ __forceinline__ float4 ld4(Rsrc r, uint32_t voff) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ void st4(Rsrc r, uint32_t voff, float4 v) {
+    u32x4 u;
+    u.x = __float_as_uint(v.x); u.y = __float_as_uint(v.y); u.z = __float_as_uint(v.z); u.w = __float_as_uint(v.w);
+    __builtin_amdgcn_raw_buffer_store_b128(u, r, voff, 0, 0);
+}
 
 __device__ __forceinline__ float unit24(uint32_t acc) {
     return (float)(acc >> 8) * 5.9604644775390625e-8f;   // exact: 24-bit fraction in [0,1)
@@ -101,8 +126,8 @@ __device__ __forceinline__ Plan plan_chunk(uint32_t lfo_acc, uint32_t lfo_inc, u
 
 }  // namespace
 
-__global__ __launch_bounds__(kThreads, 2) void chorus_block_v6(ChorusArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];   // [3 taps][kWin][kThreads]
+__global__ __launch_bounds__(kThreads, 2) void chorus_block_v7(ChorusArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];   // [wave][3 taps][kWin][kRow]
     const uint32_t tid = threadIdx.x;
     const uint32_t g = blockIdx.x * kThreads + tid;
     const uint32_t wave = g >> 6, lane = g & 63u;
@@ -133,12 +158,17 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v6(ChorusArgs a) {
     float z1 = __uint_as_float(a.state[(ch ? CHS_Z1R : CHS_Z1L) * n + i]);
     float z2 = __uint_as_float(a.state[(ch ? CHS_Z2R : CHS_Z2L) * n + i]);
 
+    const uint32_t nf = a.n_frames;
     const uint32_t pmask = a.psize - 1u, cmask = a.csize - 1u;
     const float pmax = (float)(a.psize - 2u), cmax = (float)(a.csize - 2u);
-    float *pring = a.pitch_ring + ((size_t)i * 2 + ch) * a.psize;
-    float *cring = a.chorus_ring + ((size_t)i * 2 + ch) * a.csize;
-    const float *in = a.in + (size_t)ch * a.n_frames * n + i;
-    float *out = a.out + (size_t)ch * a.n_frames * n + i;
+    // buffer descriptors (wave-uniform); offsets in bytes, < 2^32 (launch_chorus checks)
+    const Rsrc rP = rsrc(a.pitch_ring, (uint64_t)n * 2 * a.psize * 4);
+    const Rsrc rC = rsrc(a.chorus_ring, (uint64_t)n * 2 * a.csize * 4);
+    const Rsrc rIn = rsrc(a.in + (size_t)ch * nf * n, (uint64_t)nf * n * 4);
+    const Rsrc rOut = rsrc(a.out + (size_t)ch * nf * n, (uint64_t)nf * n * 4);
+    const uint32_t io_v = i * 4u, frame_b = n * 4u;
+    const uint32_t own_pb = (i * 2u + ch) * a.psize * 4u;   // this lane's pitch ring, bytes
+
     // this wave's LDS region: windows [tap][slot][lane]; between uses it also stages ring stores
     // as [lane][32] (x in 0..15, pitch-shifter outputs in 16..31)
     float *region = lds + (tid >> 6) * kRegion;
@@ -148,8 +178,7 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v6(ChorusArgs a) {
     float *stage = region + lane * 32u;
 
     // cooperative-load geometry: in part-load r (0..5) of a tap, this lane fetches float4 m of
-    // owner lane o's window, with 6 consecutive lanes covering one owner (compile-time r)
-    // (recomputed where used: cheap integer ops instead of 30+ live registers)
+    // owner lane o's window, 6 consecutive lanes per owner
     auto owner = [&](int r) { return ((uint32_t)r * 64u + lane) / kParts; };
     auto piece = [&](int r) { return ((uint32_t)r * 64u + lane) % kParts; };
     float4 vA[kParts], vB[kParts], vC[kParts];
@@ -160,16 +189,11 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v6(ChorusArgs a) {
             const int oA = __builtin_amdgcn_ds_bpermute((int)(o << 2), pl.sA);
             const int oB = __builtin_amdgcn_ds_bpermute((int)(o << 2), pl.sB);
             const int oC = __builtin_amdgcn_ds_bpermute((int)(o << 2), pl.sC);
-            const uint32_t oi = inst0 + o;
-            if (oi < n) {
-                const float *op = a.pitch_ring + ((size_t)oi * 2 + ch) * a.psize;
-                vA[r] = *(const float4 *)(op + ((wpos + oA + m4) & pmask));
-                vB[r] = *(const float4 *)(op + ((wpos + oB + m4) & pmask));
-                if (full) {
-                    const float *oc = a.chorus_ring + ((size_t)oi * 2 + ch) * a.csize;
-                    vC[r] = *(const float4 *)(oc + ((wpos + oC + m4) & cmask));
-                }
-            }
+            const uint32_t oi = min(inst0 + o, n - 1);   // lanes past n load a harmless duplicate
+            const uint32_t pb = (oi * 2u + ch) * a.psize * 4u;
+            vA[r] = ld4(rP, pb + ((wpos + oA + m4) & pmask) * 4u);
+            vB[r] = ld4(rP, pb + ((wpos + oB + m4) & pmask) * 4u);
+            if (full) vC[r] = ld4(rC, (oi * 2u + ch) * a.csize * 4u + ((wpos + oC + m4) & cmask) * 4u);
         }
     };
     auto stage_windows = [&]() {
@@ -185,8 +209,7 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v6(ChorusArgs a) {
         }
     };
     // Cooperative ring store of a chunk: every lane has staged its C consecutive samples at
-    // stage[base..base+C); 4 consecutive lanes then write one owner's 64 B with 16-B stores, so a
-    // store instruction covers 16 owners' contiguous runs instead of 64 scattered 16-B pieces.
+    // stage[base..base+C); 4 consecutive lanes then write one owner's 64 B with 16-B stores.
     auto coop_store = [&](bool pitch, uint32_t base, uint32_t wpos, int C) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -194,8 +217,8 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v6(ChorusArgs a) {
             const float4 v = *(const float4 *)(region + o * 32u + base + p4);
             const uint32_t oi = inst0 + o;
             if (oi < n && (int)p4 < C) {
-                if (pitch) *(float4 *)(a.pitch_ring + ((size_t)oi * 2 + ch) * a.psize + ((wpos + p4) & pmask)) = v;
-                else *(float4 *)(a.chorus_ring + ((size_t)oi * 2 + ch) * a.csize + ((wpos + p4) & cmask)) = v;
+                if (pitch) st4(rP, (oi * 2u + ch) * a.psize * 4u + ((wpos + p4) & pmask) * 4u, v);
+                else st4(rC, (oi * 2u + ch) * a.csize * 4u + ((wpos + p4) & cmask) * 4u, v);
             }
         }
     };
@@ -204,12 +227,11 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v6(ChorusArgs a) {
         for (int k = 0; k < kChunk; k += 4) *(float4 *)(stage + base + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
     };
 
-    const uint32_t nf = a.n_frames;
     // ---- prologue: chunk 0's inputs go to the pitch ring before its windows are loaded ----
     float x[kChunk], xn[kChunk], psv[kChunk];
     int C = (int)min((uint32_t)kChunk, nf);
 #pragma unroll
-    for (int k = 0; k < kChunk; ++k) x[k] = k < C ? in[(size_t)k * n] : 0.f;
+    for (int k = 0; k < kChunk; ++k) x[k] = k < C ? ld1(rIn, io_v, (uint32_t)k * frame_b) : 0.f;
     stage_run(x, 0);
     coop_store(true, 0, a.t0, C);
     Plan pl = plan_chunk(lfo_acc, lfo_inc, lfo_off, ps_acc, ps_inc, C, D, W, pmax, cmax, full);
@@ -251,12 +273,13 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v6(ChorusArgs a) {
         }
 
         // ---- 3. issue the next chunk's input and window loads (consumed next iteration) ----
-        const uint32_t lfo_next = lfo_acc + (uint32_t)C * lfo_inc, ps_next = ps_acc + (uint32_t)C * ps_inc;
         if (f0 + kChunk < nf) {
             const int Cn = (int)min((uint32_t)kChunk, nf - f0 - kChunk);
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) xn[k] = k < Cn ? in[(size_t)(f0 + kChunk + k) * n] : 0.f;
-            pl = plan_chunk(lfo_next, lfo_inc, lfo_off, ps_next, ps_inc, Cn, D, W, pmax, cmax, full);
+            for (int k = 0; k < kChunk; ++k)
+                xn[k] = k < Cn ? ld1(rIn, io_v, (f0 + kChunk + (uint32_t)k) * frame_b) : 0.f;
+            pl = plan_chunk(lfo_acc + (uint32_t)C * lfo_inc, lfo_inc, lfo_off, ps_acc + (uint32_t)C * ps_inc,
+                            ps_inc, Cn, D, W, pmax, cmax, full);
             load_windows(pl, w0 + kChunk);
         }
 
@@ -280,7 +303,7 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v6(ChorusArgs a) {
                     tA = lerp_pair(wP0[j * kRow], wP0[(j - 1) * kRow], fr);
                 } else {
                     const uint32_t q = w0 + k - di;
-                    tA = lerp_pair(pring[q & pmask], pring[(q - 1u) & pmask], fr);
+                    tA = lerp_pair(ld1(rP, own_pb + (q & pmask) * 4u, 0), ld1(rP, own_pb + ((q - 1u) & pmask) * 4u, 0), fr);
                 }
                 split_delay(p1 * W, 1.0f, pmax, di, fr);
                 if (cur.okB) {
@@ -288,7 +311,7 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v6(ChorusArgs a) {
                     tB = lerp_pair(wP1[j * kRow], wP1[(j - 1) * kRow], fr);
                 } else {
                     const uint32_t q = w0 + k - di;
-                    tB = lerp_pair(pring[q & pmask], pring[(q - 1u) & pmask], fr);
+                    tB = lerp_pair(ld1(rP, own_pb + (q & pmask) * 4u, 0), ld1(rP, own_pb + ((q - 1u) & pmask) * 4u, 0), fr);
                 }
                 const float p = tB * gB + tA * gA;
                 psv[k] = p;
@@ -304,7 +327,7 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v6(ChorusArgs a) {
                     z2 = b2 * wet - a2 * lp;
                     y = x[k] * dry + lp * mix;
                 }
-                if (valid) out[(size_t)(f0 + k) * n] = y;
+                if (valid) st1(rOut, io_v, (f0 + (uint32_t)k) * frame_b, y);
             } else {
                 psv[k] = 0.f;
             }
@@ -329,10 +352,13 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v6(ChorusArgs a) {
 hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
     if (a.n_frames & 3u) return hipErrorInvalidValue;
+    // 32-bit buffer offsets: rings and each audio plane must stay below 4 GiB
+    if ((uint64_t)a.n * 2 * a.csize * 4 >= (1ull << 32) || (uint64_t)a.n_frames * a.n * 4 >= (1ull << 32))
+        return hipErrorInvalidValue;
     const uint32_t groups = (a.n + 63) / 64;            // 64-instance groups, 2 waves each
     const uint32_t blocks = (groups * 2 * 64 + kThreads - 1) / kThreads;
-    const size_t lds = (size_t)3 * kWin * kThreads * sizeof(float);
-    hipLaunchKernelGGL(chorus_block_v6, dim3(blocks), dim3(kThreads), lds, s, a);
+    const size_t lds = (size_t)(kThreads / 64) * kRegion * sizeof(float);
+    hipLaunchKernelGGL(chorus_block_v7, dim3(blocks), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 
