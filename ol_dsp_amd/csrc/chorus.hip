@@ -30,6 +30,8 @@
 // ring, chorus outputs not yet in the chorus ring) are patched into LDS from registers.  A pitch
 // window that cannot cover its chunk (phasor wrap, once per 1/shift s) falls back to direct ring
 // reads for that lane and chunk.
+#include <type_traits>
+
 #include "olfx_internal.h"
 
 namespace olfx {
@@ -41,7 +43,8 @@ constexpr int kWin = 24;                    // floats staged per tap window (6 x
 constexpr int kParts = kWin / 4;
 constexpr int kThreads = 256;
 constexpr int kRow = 64;                    // LDS slot stride: one wave's lanes
-constexpr int kRegion = 3 * kWin * kRow;    // floats of LDS per wave (>= 64 lanes x 32 staging)
+constexpr int kSlots = kWin + 1;            // + one junk slot per tap (branch-free guarded stores)
+constexpr int kRegion = 3 * kSlots * kRow;  // floats of LDS per wave (>= 64 lanes x 32 staging)
 static_assert(kRegion >= 64 * 32, "staging area must fit in the window region");
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -126,7 +129,8 @@ __device__ __forceinline__ Plan plan_chunk(uint32_t lfo_acc, uint32_t lfo_inc, u
 
 }  // namespace
 
-__global__ __launch_bounds__(kThreads, 2) void chorus_block_v7(ChorusArgs a) {
+template <bool FULL>
+__global__ __launch_bounds__(kThreads, 2) void chorus_block_v8(ChorusArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];   // [wave][3 taps][kWin][kRow]
     const uint32_t tid = threadIdx.x;
     const uint32_t g = blockIdx.x * kThreads + tid;
@@ -138,7 +142,7 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v7(ChorusArgs a) {
     const uint32_t i_raw = inst0 + lane;
     const bool valid = i_raw < n;                      // invalid lanes still help load windows
     const uint32_t i = valid ? i_raw : n - 1;
-    const bool full = a.mode == 0;
+    constexpr bool full = FULL;
 
     const uint32_t lfo_inc = a.coef[CHC_LFO_INC * n + i];
     const uint32_t lfo_off = a.coef[CHC_LFO_OFF * n + i];
@@ -167,14 +171,15 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v7(ChorusArgs a) {
     const Rsrc rIn = rsrc(a.in + (size_t)ch * nf * n, (uint64_t)nf * n * 4);
     const Rsrc rOut = rsrc(a.out + (size_t)ch * nf * n, (uint64_t)nf * n * 4);
     const uint32_t io_v = i * 4u, frame_b = n * 4u;
+    const uint32_t out_v = valid ? io_v : 0xFFFFFFF0u;   // invalid lanes: buffer range check drops
     const uint32_t own_pb = (i * 2u + ch) * a.psize * 4u;   // this lane's pitch ring, bytes
 
     // this wave's LDS region: windows [tap][slot][lane]; between uses it also stages ring stores
     // as [lane][32] (x in 0..15, pitch-shifter outputs in 16..31)
     float *region = lds + (tid >> 6) * kRegion;
-    float *wP0 = region + 0 * kWin * kRow + lane;
-    float *wP1 = region + 1 * kWin * kRow + lane;
-    float *wC = region + 2 * kWin * kRow + lane;
+    float *wP0 = region + 0 * kSlots * kRow + lane;
+    float *wP1 = region + 1 * kSlots * kRow + lane;
+    float *wC = region + 2 * kSlots * kRow + lane;
     float *stage = region + lane * 32u;
 
     // cooperative-load geometry: in part-load r (0..5) of a tap, this lane fetches float4 m of
@@ -200,7 +205,7 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v7(ChorusArgs a) {
 #pragma unroll
         for (int r = 0; r < kParts; ++r) {
             float *pA = region + owner(r) + 4u * piece(r) * kRow;
-            float *pB = pA + kWin * kRow, *pC = pA + 2 * kWin * kRow;
+            float *pB = pA + kSlots * kRow, *pC = pA + 2 * kSlots * kRow;
             pA[0] = vA[r].x; pA[kRow] = vA[r].y; pA[2 * kRow] = vA[r].z; pA[3 * kRow] = vA[r].w;
             pB[0] = vB[r].x; pB[kRow] = vB[r].y; pB[2 * kRow] = vB[r].z; pB[3 * kRow] = vB[r].w;
             if (full) {
@@ -284,53 +289,61 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v7(ChorusArgs a) {
         }
 
         // ---- 4. the serial recurrence over this chunk ----
-#pragma unroll
-        for (int k = 0; k < kChunk; ++k) {
-            if (k < C) {
-                const float lfo = cos2pi(unit24(lfo_acc + lfo_off));
-                const float dch = lfo * D + D;
-                const float p0 = unit24(ps_acc);
-                const float p1 = unit24(ps_acc + 0x80000000u);
-                const float gA = cos2pi((p0 - 0.5f) * 0.5f);
-                const float gB = cos2pi((p1 - 0.5f) * 0.5f);
-                lfo_acc += lfo_inc;
-                ps_acc += ps_inc;
-                int di; float fr;
-                float tA, tB;
-                split_delay(p0 * W, 1.0f, pmax, di, fr);
-                if (cur.okA) {
-                    const int j = k - di - cur.sA;
-                    tA = lerp_pair(wP0[j * kRow], wP0[(j - 1) * kRow], fr);
-                } else {
-                    const uint32_t q = w0 + k - di;
-                    tA = lerp_pair(ld1(rP, own_pb + (q & pmask) * 4u, 0), ld1(rP, own_pb + ((q - 1u) & pmask) * 4u, 0), fr);
-                }
-                split_delay(p1 * W, 1.0f, pmax, di, fr);
-                if (cur.okB) {
-                    const int j = k - di - cur.sB;
-                    tB = lerp_pair(wP1[j * kRow], wP1[(j - 1) * kRow], fr);
-                } else {
-                    const uint32_t q = w0 + k - di;
-                    tB = lerp_pair(ld1(rP, own_pb + (q & pmask) * 4u, 0), ld1(rP, own_pb + ((q - 1u) & pmask) * 4u, 0), fr);
-                }
-                const float p = tB * gB + tA * gA;
-                psv[k] = p;
-                float y = p;
-                if (full) {
-                    // delay~ writes before it reads: this frame's sample is visible at delay 0
-                    if (k - cur.sC < kWin) wC[(k - cur.sC) * kRow] = p;
-                    split_delay(dch, 0.0f, cmax, di, fr);
-                    const int j = k - di - cur.sC;
-                    const float wet = lerp_pair(wC[j * kRow], wC[(j - 1) * kRow], fr);
-                    const float lp = b0 * wet + z1;
-                    z1 = (b1 * wet - a1 * lp) + z2;
-                    z2 = b2 * wet - a2 * lp;
-                    y = x[k] * dry + lp * mix;
-                }
-                if (valid) st1(rOut, io_v, (f0 + (uint32_t)k) * frame_b, y);
+        // GENERIC = partial chunk or some lane's pitch window misses (phasor wrap): per-frame
+        // guards and per-lane fallback reads.  The common case runs branch-free, so the 16 frames
+        // form one basic block and their independent control math interleaves.
+        auto frame = [&](auto generic_tag, int k) {
+            constexpr bool GENERIC = decltype(generic_tag)::value;
+            if (GENERIC && k >= C) { psv[k] = 0.f; return; }
+            const float lfo = cos2pi(unit24(lfo_acc + lfo_off));
+            const float dch = lfo * D + D;
+            const float p0 = unit24(ps_acc);
+            const float p1 = unit24(ps_acc + 0x80000000u);
+            const float gA = cos2pi((p0 - 0.5f) * 0.5f);
+            const float gB = cos2pi((p1 - 0.5f) * 0.5f);
+            lfo_acc += lfo_inc;
+            ps_acc += ps_inc;
+            int di; float fr;
+            float tA, tB;
+            split_delay(p0 * W, 1.0f, pmax, di, fr);
+            if (GENERIC && !cur.okA) {
+                const uint32_t q = w0 + k - di;
+                tA = lerp_pair(ld1(rP, own_pb + (q & pmask) * 4u, 0), ld1(rP, own_pb + ((q - 1u) & pmask) * 4u, 0), fr);
             } else {
-                psv[k] = 0.f;
+                const int j = k - di - cur.sA;
+                tA = lerp_pair(wP0[j * kRow], wP0[(j - 1) * kRow], fr);
             }
+            split_delay(p1 * W, 1.0f, pmax, di, fr);
+            if (GENERIC && !cur.okB) {
+                const uint32_t q = w0 + k - di;
+                tB = lerp_pair(ld1(rP, own_pb + (q & pmask) * 4u, 0), ld1(rP, own_pb + ((q - 1u) & pmask) * 4u, 0), fr);
+            } else {
+                const int j = k - di - cur.sB;
+                tB = lerp_pair(wP1[j * kRow], wP1[(j - 1) * kRow], fr);
+            }
+            const float p = tB * gB + tA * gA;
+            psv[k] = p;
+            float y = p;
+            if (FULL) {
+                // delay~ writes before it reads: this frame's sample is visible at delay 0; slots
+                // past the window land in the junk slot (no branch)
+                wC[min(k - cur.sC, kWin) * kRow] = p;
+                split_delay(dch, 0.0f, cmax, di, fr);
+                const int j = k - di - cur.sC;
+                const float wet = lerp_pair(wC[j * kRow], wC[(j - 1) * kRow], fr);
+                const float lp = b0 * wet + z1;
+                z1 = (b1 * wet - a1 * lp) + z2;
+                z2 = b2 * wet - a2 * lp;
+                y = x[k] * dry + lp * mix;
+            }
+            st1(rOut, out_v, (f0 + (uint32_t)k) * frame_b, y);   // out-of-range voffset = dropped
+        };
+        if (C == kChunk && __all(cur.okA && cur.okB)) {
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) frame(std::false_type{}, k);
+        } else {
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) frame(std::true_type{}, k);
         }
         if (full) {   // the chunk's windows are dead: stage its pitch-shifter outputs, store cooperatively
             stage_run(psv, 16);
@@ -358,7 +371,8 @@ hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s) {
     const uint32_t groups = (a.n + 63) / 64;            // 64-instance groups, 2 waves each
     const uint32_t blocks = (groups * 2 * 64 + kThreads - 1) / kThreads;
     const size_t lds = (size_t)(kThreads / 64) * kRegion * sizeof(float);
-    hipLaunchKernelGGL(chorus_block_v7, dim3(blocks), dim3(kThreads), lds, s, a);
+    if (a.mode == 0) hipLaunchKernelGGL(chorus_block_v8<true>, dim3(blocks), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL(chorus_block_v8<false>, dim3(blocks), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 
