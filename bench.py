@@ -122,9 +122,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from ol_dsp_amd.dist import RunStats, env_ranks, reduce_stats
+    rank, world, local = env_ranks()
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -172,14 +171,10 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
-    frames = float(n) * B * args.steps
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms, frames], dtype=torch.float64, device=dev)
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t.clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed, kern_ms, frames = float(tmax[0]), float(tmax[1]), float(tsum[2])
+    # the single collective of the run (RCCL over xGMI when world > 1): outside the timed region
+    checksum = float(out.abs().sum().item())
+    stats = reduce_stats(RunStats(elapsed, kern_ms, float(n) * B * args.steps, checksum), device=dev)
+    elapsed, kern_ms, frames = stats.elapsed_s, stats.kernel_ms, stats.frames
 
     if rank == 0:
         value = frames / elapsed
@@ -221,6 +216,7 @@ def main():
                          "kernel": eng.kernel_name, "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_frame": bpf, "frames_per_launch": n * B},
             "cpu_baseline": cpu,
+            "output_checksum": stats.checksum,
         }
         print(json.dumps(res), flush=True)
     if world > 1:
