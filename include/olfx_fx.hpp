@@ -1,0 +1,185 @@
+/*
+ * include/olfx_fx.hpp -- C++ operator surface over the olfx C-ABI (header-only).
+ *
+ * These classes give reference callers the method names and argument meanings of the reference
+ * effect operators. Each object holds N instances and processes whole blocks on the GPU:
+ *
+ *   olfx::ReverbBank  <- ol::fx::Reverb (modules/fxlib/Reverb.h:43-66) backed by DattorroVerb
+ *                        (libs/dattorro-verb/verb.h:5-26). The stereo -> (l+r)/2 -> L/R glue
+ *                        follows ReverbFx.cpp:11-27.
+ *   olfx::ChorusBank  <- ChorusEffect (README.md:114-128: init / setDepth / setRate / process),
+ *                        which wraps the RNBO stereo chorus. Its params follow
+ *                        modules/rnbo/patcher/mono-chorus.rnbopat.
+ *   olfx::PitchShiftBank <- gen~ pitchshift (modules/rnbo/patcher/pitchshift.gendsp)
+ *   olfx::VoiceBank   <- ol::synth::SynthVoice (modules/synthlib/SynthVoice.h:31-98, :245-256):
+ *                        Init / UpdateConfig / NoteOn / NoteOff / Process.
+ *
+ * Each per-instance setter takes the same value as the reference setter and applies it at the
+ * next Process call (block-boundary parameter updates, modules/juce/host/host.cpp:646-653).
+ *
+ * Error behaviour: the reference's setters and Process return void, and DattorroVerb_create
+ * returns NULL on failure (verb.cpp:227). Here every failing C-ABI call throws olfx::Error,
+ * carrying the OLFX_E_* code and olfx_last_error()'s text. Nothing fails silently, and there is
+ * no CPU fallback: without a GPU, construction throws OLFX_E_NODEVICE.
+ *
+ * Audio buffers are [channel][frame][instance] float32. They are host pointers by default
+ * (OLFX_IO_HOST: staged through pinned memory, PCIe-inclusive) or device pointers
+ * (OLFX_IO_DEVICE: asynchronous on `stream`, the fast path).
+ */
+#ifndef OLFX_FX_HPP
+#define OLFX_FX_HPP
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "olfx.h"
+
+namespace olfx {
+
+class Error : public std::runtime_error {
+public:
+    Error(int code, const std::string &what) : std::runtime_error(what), code_(code) {}
+    int code() const { return code_; }
+private:
+    int code_;
+};
+
+inline void check(int rc, const olfx_engine *e, const char *call) {
+    if (rc != OLFX_OK) {
+        const char *msg = olfx_last_error(e);
+        throw Error(rc, std::string(call) + ": " + (msg ? msg : "") + " (code " + std::to_string(rc) + ")");
+    }
+}
+
+/* RAII owner of one engine: one effect kind x N instances on one GPU. */
+class Engine {
+public:
+    Engine(int kind, uint32_t n_inst, float sample_rate, uint32_t block = 256, int device = 0) {
+        check(olfx_create(kind, device, n_inst, sample_rate, block, &e_), nullptr, "olfx_create");
+    }
+    ~Engine() { if (e_) olfx_destroy(e_); }
+    Engine(const Engine &) = delete;
+    Engine &operator=(const Engine &) = delete;
+    Engine(Engine &&o) noexcept : e_(std::exchange(o.e_, nullptr)) {}
+    Engine &operator=(Engine &&o) noexcept {
+        if (this != &o) { if (e_) olfx_destroy(e_); e_ = std::exchange(o.e_, nullptr); }
+        return *this;
+    }
+
+    olfx_engine *handle() const { return e_; }
+    uint32_t size() const { return olfx_num_instances(e_); }
+    uint64_t frames_processed() const { return olfx_frames_processed(e_); }
+    const char *kernel_name() const { return olfx_kernel_name(e_); }
+
+    void set(uint32_t inst, uint32_t field, float v) {
+        check(olfx_set_param(e_, inst, field, v), e_, "olfx_set_param");
+    }
+    float get(uint32_t inst, uint32_t field) const {
+        float v = 0.f;
+        check(olfx_get_param(e_, inst, field, &v), e_, "olfx_get_param");
+        return v;
+    }
+    /* values: field-major [n_fields][count] for instances [first, first+count). */
+    void set_block(uint32_t first, uint32_t count, uint32_t field0, uint32_t n_fields, const float *values) {
+        check(olfx_set_params(e_, first, count, field0, n_fields, values), e_, "olfx_set_params");
+    }
+    /* One field, the same value for every instance. */
+    void set_all(uint32_t field, float v) {
+        std::vector<float> vals(size(), v);
+        set_block(0, size(), field, 1, vals.data());
+    }
+    void process(const float *in, float *out, uint32_t n_frames, int io = OLFX_IO_HOST, void *stream = nullptr) {
+        check(olfx_process(e_, in, out, n_frames, io, stream), e_, "olfx_process");
+    }
+    void sync() { check(olfx_sync(e_), e_, "olfx_sync"); }
+    void reset() { check(olfx_reset(e_), e_, "olfx_reset"); }
+
+protected:
+    olfx_engine *e_ = nullptr;
+};
+
+/* ol::fx::Reverb over N Dattorro plates (Reverb.h:43-66; setters verb.cpp:137-170). */
+class ReverbBank : public Engine {
+public:
+    ReverbBank(uint32_t n_inst, float sample_rate, uint32_t block = 256, int device = 0)
+        : Engine(OLFX_KIND_DATTORRO, n_inst, sample_rate, block, device) {}
+    /* Engine-wide: a uniform pre-delay keeps the rings' tap loads coalesced. */
+    void SetPredelay(float v) { set_all(OLFX_DT_PREDELAY, v); }
+    void SetPrefilter(uint32_t i, float v) { set(i, OLFX_DT_PREFILTER, v); }
+    void SetInputDiffusion1(uint32_t i, float v) { set(i, OLFX_DT_INPUT_DIFFUSION1, v); }
+    void SetInputDiffusion2(uint32_t i, float v) { set(i, OLFX_DT_INPUT_DIFFUSION2, v); }
+    void SetDecayDiffusion(uint32_t i, float v) { set(i, OLFX_DT_DECAY_DIFFUSION, v); }
+    void SetDecay(uint32_t i, float v) { set(i, OLFX_DT_DECAY, v); }
+    void SetDamping(uint32_t i, float v) { set(i, OLFX_DT_DAMPING, v); }
+    /* frame_in [2][F][N] -> frame_out [2][F][N]; in = (l+r)/2 like ReverbFx::dattorro_process. */
+    void Process(const float *frame_in, float *frame_out, uint32_t n_frames,
+                 int io = OLFX_IO_HOST, void *stream = nullptr) {
+        process(frame_in, frame_out, n_frames, io, stream);
+    }
+};
+
+/* ChorusEffect (README.md:114-128) over N stereo RNBO choruses. Values are RNBO param values,
+   clamped to @min/@max like RNBO (include/olfx.h OLFX_CH_*). */
+class ChorusBank : public Engine {
+public:
+    ChorusBank(uint32_t n_inst, float sample_rate, uint32_t block = 256, int device = 0)
+        : Engine(OLFX_KIND_CHORUS, n_inst, sample_rate, block, device) {}
+    void setDepth(uint32_t i, float v) { set(i, OLFX_CH_DEPTH, v); }
+    void setRate(uint32_t i, float v) { set(i, OLFX_CH_RATE, v); }
+    void setMix(uint32_t i, float v) { set(i, OLFX_CH_MIX, v); }
+    void setCutoff(uint32_t i, float v) { set(i, OLFX_CH_CUTOFF, v); }
+    void setQ(uint32_t i, float v) { set(i, OLFX_CH_Q, v); }
+    void setPitch(uint32_t i, float v) { set(i, OLFX_CH_PITCH, v); }
+    void setPhase(uint32_t i, float v) { set(i, OLFX_CH_PHASE, v); }
+    void setWindow(uint32_t i, float v) { set(i, OLFX_CH_WINDOW, v); }
+    /* [2][F][N] stereo in -> [2][F][N] stereo out */
+    void process(const float *in, float *out, uint32_t n_frames, int io = OLFX_IO_HOST, void *stream = nullptr) {
+        Engine::process(in, out, n_frames, io, stream);
+    }
+};
+
+/* gen~ pitchshift (pitchshift.gendsp), stereo. */
+class PitchShiftBank : public Engine {
+public:
+    PitchShiftBank(uint32_t n_inst, float sample_rate, uint32_t block = 256, int device = 0)
+        : Engine(OLFX_KIND_PITCHSHIFT, n_inst, sample_rate, block, device) {}
+    void SetShift(uint32_t i, float hz) { set(i, OLFX_PS_SHIFT, hz); }
+    void SetWindow(uint32_t i, float ms) { set(i, OLFX_PS_WINDOW, ms); }
+};
+
+/* ol::synth::SynthVoice over N voices (SynthVoice.h). The config array is in Voice::Config field
+   order (modules/synthlib/Voice.h:14-31 == OLFX_VC_*). Note events queue up and take effect at
+   the next Process, in call order. */
+class VoiceBank : public Engine {
+public:
+    VoiceBank(uint32_t n_inst, float sample_rate, uint32_t block = 256, int device = 0)
+        : Engine(OLFX_KIND_VOICE, n_inst, sample_rate, block, device) {}
+    /* SynthVoice::UpdateConfig + Update (SynthVoice.h:55-98) */
+    void UpdateConfig(uint32_t i, const float config[OLFX_VC_NPARAMS]) {
+        set_block(i, 1, 0, OLFX_VC_NPARAMS, config);   /* [16][1] field-major == the config array */
+    }
+    void NoteOn(uint32_t i, uint8_t midi_note, uint8_t velocity) { push(i, OLFX_EV_NOTE_ON, midi_note, velocity); }
+    void NoteOff(uint32_t i, uint8_t midi_note, uint8_t velocity) { push(i, OLFX_EV_NOTE_OFF, midi_note, velocity); }
+    /* frame_out [1][F][N] */
+    void Process(float *frame_out, uint32_t n_frames, int io = OLFX_IO_HOST, void *stream = nullptr) {
+        if (!events_.empty()) {
+            check(olfx_note_events(e_, events_.data(), (uint32_t)events_.size()), e_, "olfx_note_events");
+            events_.clear();
+        }
+        process(nullptr, frame_out, n_frames, io, stream);
+    }
+
+private:
+    void push(uint32_t i, uint8_t type, uint8_t note, uint8_t vel) {
+        olfx_event ev{};
+        ev.inst = i; ev.type = type; ev.note = note; ev.velocity = vel;
+        events_.push_back(ev);
+    }
+    std::vector<olfx_event> events_;
+};
+
+}  // namespace olfx
+#endif  // OLFX_FX_HPP

@@ -1,0 +1,234 @@
+/*
+ * tests/cpp/test_operators.cpp -- GPU parity of the C++ operator surface (include/olfx_fx.hpp).
+ *
+ * Written in the style of the reference's gtest suites (test/synth_test.cpp, test/fx_test.cpp):
+ * the operators are driven through the same method names as the reference and compared with the
+ * CPU oracle (oracle/liboracle.so, TEST INFRASTRUCTURE) on identical inputs. Dattorro, chorus
+ * and pitch-shift must be bit-exact. The voice must be within 1e-5 of max(|ref|, rms(ref)), the
+ * tolerance tests/test_gpu_parity.py documents for Svf's per-sample sinf.
+ *
+ * gtest is not in the image, so a small TEST/EXPECT harness stands in. The binary exits non-zero
+ * on any failure. It needs a GPU; run it through tests/test_cpp_operators.py (-m gpu).
+ */
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "olfx_fx.hpp"
+#include "../../oracle/oracle.h"
+
+namespace {
+struct Case { const char *suite, *name; std::function<void()> fn; };
+std::vector<Case> &cases() { static std::vector<Case> c; return c; }
+int g_failures = 0;
+struct Reg { Reg(const char *s, const char *n, std::function<void()> f) { cases().push_back({s, n, std::move(f)}); } };
+#define TEST(S, N) static void S##_##N(); static Reg reg_##S##_##N(#S, #N, S##_##N); static void S##_##N()
+#define EXPECT_TRUE(c) do { if (!(c)) { ++g_failures; std::printf("  FAILED %s:%d: %s\n", __FILE__, __LINE__, #c); } } while (0)
+#define EXPECT_EQ(a, b) EXPECT_TRUE((a) == (b))
+
+/* xorshift32 white noise in [-1,1): the SURVEY section 8c KAT generator, one seed per instance */
+std::vector<float> noise(uint32_t ch, uint32_t frames, uint32_t n, uint32_t seed) {
+    std::vector<float> x((size_t)ch * frames * n);
+    for (uint32_t c = 0; c < ch; ++c)
+        for (uint32_t i = 0; i < n; ++i)
+            oracle_xorshift_noise(seed + 7919u * i + 104729u * c, x.data() + (size_t)c * frames * n + i,
+                                  frames, n);
+    return x;
+}
+
+struct Lcg {   /* deterministic parameter draws */
+    uint64_t s;
+    explicit Lcg(uint64_t seed) : s(seed) {}
+    float uni(float lo, float hi) {
+        s = s * 6364136223846793005ull + 1442695040888963407ull;
+        return lo + (hi - lo) * (float)((s >> 40) * (1.0 / 16777216.0));
+    }
+};
+
+size_t first_bit_mismatch(const std::vector<float> &a, const std::vector<float> &b) {
+    for (size_t k = 0; k < a.size(); ++k)
+        if (std::memcmp(&a[k], &b[k], 4) != 0) return k;
+    return (size_t)-1;
+}
+
+/* Process `frames` frames through `op` in blocks of `block` frames; layout [ch][frames][n]. */
+template <class F>
+std::vector<float> run_blocks(F &&proc, const std::vector<float> &x, uint32_t ich, uint32_t och,
+                              uint32_t frames, uint32_t n, uint32_t block) {
+    std::vector<float> y((size_t)och * frames * n), xin((size_t)ich * block * n), yb((size_t)och * block * n);
+    for (uint32_t f0 = 0; f0 < frames; f0 += block) {
+        uint32_t b = std::min(block, frames - f0);
+        for (uint32_t c = 0; c < ich; ++c)
+            std::memcpy(&xin[(size_t)c * b * n], &x[((size_t)c * frames + f0) * n], (size_t)b * n * 4);
+        proc(xin.data(), yb.data(), b);
+        for (uint32_t c = 0; c < och; ++c)
+            std::memcpy(&y[((size_t)c * frames + f0) * n], &yb[(size_t)c * b * n], (size_t)b * n * 4);
+    }
+    return y;
+}
+}  // namespace
+
+/* ol::fx::Reverb surface over N plates vs the bit-exact Dattorro oracle. */
+TEST(Reverb, BankMatchesOracleBitExact) {
+    const uint32_t n = 129, frames = 2048;
+    olfx::ReverbBank verb(n, 48000.f);
+    oracle_dattorro *ref = oracle_dattorro_create((int)n);
+    Lcg r(11);
+    verb.SetPredelay(0.1f);
+    for (uint32_t i = 0; i < n; ++i) {
+        float pf = r.uni(.3f, 1.f), d1 = r.uni(.5f, .9f), d2 = r.uni(.4f, .8f), dd = r.uni(.4f, .9f);
+        float dec = r.uni(.25f, .95f), damp = r.uni(.05f, .95f);
+        verb.SetPrefilter(i, pf); verb.SetInputDiffusion1(i, d1); verb.SetInputDiffusion2(i, d2);
+        verb.SetDecayDiffusion(i, dd); verb.SetDecay(i, dec); verb.SetDamping(i, damp);
+        const float v[ODT_NPARAMS] = {0.1f, pf, d1, d2, dd, dec, damp};
+        for (int f = 0; f < ODT_NPARAMS; ++f) oracle_dattorro_set(ref, (int)i, f, v[f]);
+    }
+    std::vector<float> x = noise(2, frames, n, 5);
+    std::vector<float> y = run_blocks([&](const float *a, float *b, uint32_t f) { verb.Process(a, b, f); },
+                                      x, 2, 2, frames, n, 256);
+    std::vector<float> yr(y.size());
+    oracle_dattorro_process(ref, x.data(), 2, yr.data(), (int)frames, 8);
+    size_t k = first_bit_mismatch(y, yr);
+    if (k != (size_t)-1) std::printf("  first mismatch at %zu: %.9g vs %.9g\n", k, y[k], yr[k]);
+    EXPECT_TRUE(k == (size_t)-1);
+    EXPECT_EQ(verb.frames_processed(), (uint64_t)frames);
+    oracle_dattorro_destroy(ref);
+}
+
+/* ChorusEffect init / setDepth / setRate / process vs the chorus spec oracle (bit-exact). */
+TEST(ChorusEffect, BankMatchesOracleBitExact) {
+    const uint32_t n = 257, frames = 1024;
+    olfx::ChorusBank chorus(n, 48000.f);
+    oracle_chorus *ref = oracle_chorus_create((int)n, 48000.f, 0);
+    Lcg r(12);
+    for (uint32_t i = 0; i < n; ++i) {
+        float v[OCH_NPARAMS] = {r.uni(0, 3), r.uni(0, 1), r.uni(0, .95f), r.uni(0, 1),
+                                r.uni(0, 1), r.uni(.08f, 1), r.uni(.01f, 1), r.uni(4, 10)};
+        chorus.setPitch(i, v[OCH_PITCH]); chorus.setMix(i, v[OCH_MIX]); chorus.setQ(i, v[OCH_Q]);
+        chorus.setCutoff(i, v[OCH_CUTOFF]); chorus.setPhase(i, v[OCH_PHASE]);
+        chorus.setDepth(i, v[OCH_DEPTH]); chorus.setRate(i, v[OCH_RATE]); chorus.setWindow(i, v[OCH_WINDOW]);
+        for (int f = 0; f < OCH_NPARAMS; ++f) oracle_chorus_set(ref, (int)i, f, v[f]);
+    }
+    std::vector<float> x = noise(2, frames, n, 6);
+    std::vector<float> y = run_blocks([&](const float *a, float *b, uint32_t f) { chorus.process(a, b, f); },
+                                      x, 2, 2, frames, n, 256);
+    std::vector<float> yr(y.size());
+    oracle_chorus_process(ref, x.data(), yr.data(), (int)frames, 8);
+    EXPECT_TRUE(first_bit_mismatch(y, yr) == (size_t)-1);
+    oracle_chorus_destroy(ref);
+}
+
+TEST(PitchShift, BankMatchesOracleBitExact) {
+    const uint32_t n = 64, frames = 1024;
+    olfx::PitchShiftBank ps(n, 48000.f);
+    oracle_chorus *ref = oracle_chorus_create((int)n, 48000.f, 1);
+    Lcg r(13);
+    for (uint32_t i = 0; i < n; ++i) {
+        float s = r.uni(0, 3), w = r.uni(4, 10);
+        ps.SetShift(i, s); ps.SetWindow(i, w);
+        oracle_chorus_set(ref, (int)i, OCH_PITCH, s);
+        oracle_chorus_set(ref, (int)i, OCH_WINDOW, w);
+    }
+    std::vector<float> x = noise(2, frames, n, 7);
+    std::vector<float> y = run_blocks([&](const float *a, float *b, uint32_t f) { ps.process(a, b, f); },
+                                      x, 2, 2, frames, n, 128);
+    std::vector<float> yr(y.size());
+    oracle_chorus_process(ref, x.data(), yr.data(), (int)frames, 8);
+    EXPECT_TRUE(first_bit_mismatch(y, yr) == (size_t)-1);
+    oracle_chorus_destroy(ref);
+}
+
+/* SynthVoice Init / UpdateConfig / NoteOn / NoteOff / Process vs the DaisySP restatement. */
+TEST(Synth, VoiceBankMatchesOracle) {
+    const uint32_t n = 96, half = 1024;
+    olfx::VoiceBank voices(n, 48000.f);
+    oracle_voice *ref = oracle_voice_create((int)n, 48000.f);
+    Lcg r(14);
+    std::vector<uint8_t> notes(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        float c[OLFX_VC_NPARAMS] = {r.uni(100, 8000), r.uni(0, .9f), r.uni(0, 1), r.uni(0, 1),
+                                    r.uni(.001f, .5f), r.uni(0, 1), r.uni(.001f, .5f), r.uni(0, 1),
+                                    r.uni(.001f, .5f), r.uni(.2f, 1), r.uni(.001f, .5f), r.uni(0, 1),
+                                    r.uni(.001f, .5f), r.uni(0, 1), r.uni(.001f, .5f), r.uni(0, .05f)};
+        notes[i] = (uint8_t)(36 + (i * 7) % 61);
+        voices.UpdateConfig(i, c);
+        voices.NoteOn(i, notes[i], 100);
+        oracle_voice_config(ref, (int)i, c);
+        oracle_voice_note(ref, (int)i, 1, notes[i]);
+    }
+    std::vector<float> y(2 * (size_t)half * n), yr(y.size());
+    voices.Process(y.data(), half);
+    oracle_voice_process(ref, yr.data(), (int)half, 8);
+    for (uint32_t i = 0; i < n; ++i) {
+        voices.NoteOff(i, notes[i], 0);
+        oracle_voice_note(ref, (int)i, 0, notes[i]);
+    }
+    voices.Process(y.data() + (size_t)half * n, half);
+    oracle_voice_process(ref, yr.data() + (size_t)half * n, (int)half, 8);
+    for (uint32_t i = 0; i < n; ++i) {          /* per voice: |y - ref| <= 1e-5 * max(|ref|, rms) */
+        double ss = 0, mx = 0, err = 0;
+        for (uint32_t f = 0; f < 2 * half; ++f) {
+            double a = yr[(size_t)f * n + i];
+            ss += a * a; mx = std::max(mx, std::fabs(a));
+            err = std::max(err, std::fabs((double)y[(size_t)f * n + i] - a));
+        }
+        double scale = std::max(mx, std::sqrt(ss / (2 * half)));
+        EXPECT_TRUE(std::isfinite(err) && err <= 1e-5 * std::max(scale, 1e-30));
+    }
+    oracle_voice_destroy(ref);
+}
+
+/* test/synth_test.cpp:102-148 pins: the first sample after NoteOn is exactly 0, and later
+   samples are neither 0 nor 1. */
+TEST(Synth, VoiceNoteOnOffPins) {
+    olfx::VoiceBank v(1, 48000.f);
+    float y[4];
+    v.NoteOn(0, 60, 100);
+    v.NoteOff(0, 60, 0);
+    v.Process(y, 4);
+    EXPECT_EQ(y[0], 0.f);
+    v.NoteOn(0, 60, 100);
+    v.Process(y, 4);
+    EXPECT_TRUE(y[1] != 0.f && y[1] != 1.f);
+}
+
+/* Error behaviour: failures throw olfx::Error carrying the C-ABI code; nothing is silent. */
+TEST(Boundary, ErrorsThrowWithCode) {
+    int code = 0;
+    try { olfx::Engine bad(99, 4, 48000.f); } catch (const olfx::Error &e) { code = e.code(); }
+    EXPECT_EQ(code, OLFX_E_KIND);
+    olfx::ChorusBank c(8, 48000.f);
+    code = 0;
+    try { c.setDepth(8, 0.5f); } catch (const olfx::Error &e) { code = e.code(); }   /* out of range */
+    EXPECT_EQ(code, OLFX_E_ARG);
+    std::vector<float> buf(2 * 6 * 8);
+    code = 0;
+    try { c.process(buf.data(), buf.data(), 6); } catch (const olfx::Error &e) { code = e.code(); }  /* not x4 */
+    EXPECT_EQ(code, OLFX_E_ARG);
+    /* RNBO clamps to @max: depth 5 behaves as depth 1 (the host shadow keeps the value as set) */
+    olfx::ChorusBank two(2, 48000.f);
+    two.setDepth(0, 5.f);
+    two.setDepth(1, 1.f);
+    EXPECT_EQ(two.get(0, OLFX_CH_DEPTH), 5.f);
+    std::vector<float> x = noise(2, 512, 1, 9), x2(2 * 512 * 2), y2(x2.size());
+    for (size_t k = 0; k < x.size(); ++k) x2[2 * k] = x2[2 * k + 1] = x[k];
+    two.process(x2.data(), y2.data(), 512);
+    bool same = true;
+    for (size_t k = 0; k < x.size(); ++k) same &= std::memcmp(&y2[2 * k], &y2[2 * k + 1], 4) == 0;
+    EXPECT_TRUE(same);
+}
+
+int main() {
+    for (auto &c : cases()) {
+        int before = g_failures;
+        std::printf("[ RUN      ] %s.%s\n", c.suite, c.name);
+        try { c.fn(); } catch (const std::exception &e) { ++g_failures; std::printf("  exception: %s\n", e.what()); }
+        std::printf("[ %s ] %s.%s\n", g_failures == before ? "      OK" : " FAILED ", c.suite, c.name);
+    }
+    std::printf("%zu tests, %d failures\n", cases().size(), g_failures);
+    return g_failures ? 1 : 0;
+}

@@ -1,0 +1,38 @@
+"""The C++ operator surface (include/olfx_fx.hpp) driven from C++ as a reference caller would:
+ReverbBank / ChorusBank / PitchShiftBank / VoiceBank against the CPU oracle
+(tests/cpp/test_operators.cpp, gtest-style, in the manner of the reference's test/synth_test.cpp).
+"""
+import os
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CPP = os.path.join(HERE, "cpp")
+BIN = os.path.join(CPP, "test_operators")
+
+
+def _build():
+    r = subprocess.run(["make", "-s", "-C", CPP], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return BIN
+
+
+def test_cpp_operator_test_builds_and_fails_loudly_without_gpu():
+    """Builds against the plain C ABI (g++ only, no HIP headers). Off-GPU every operator must
+    throw OLFX_E_NODEVICE: there is no silent CPU path behind the surface."""
+    _build()
+    if os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK | os.W_OK):
+        pytest.skip("GPU visible: covered by the -m gpu run")
+    r = subprocess.run([BIN], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1
+    assert "no HIP device" in r.stdout and "(code -4)" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_operators_on_gpu():
+    _build()
+    r = subprocess.run([BIN], capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "6 tests, 0 failures" in r.stdout
