@@ -4,7 +4,7 @@ and the HBM traffic per launch with the gfx950 corrections of MI355X_MICROARCH.m
   FETCH_SIZE reads 1/2 of the bytes of a wide coalesced streaming read -> x2 (read side);
   WRITE_SIZE reads exact for 16-B streaming stores.
 Both are in KB (rocprofv3 derived counters).  Usage:
-  python tools/pmc_traffic.py <workload> <instances> <block> [kernel-substring] [--out json]
+  python tools/pmc_traffic.py <workload> <instances> <block> [kernel-substring] [--fetch-scale X] [--out json]
 """
 import csv
 import glob
@@ -31,6 +31,10 @@ def main():
     out = None
     if "--out" in sys.argv:
         out = sys.argv[sys.argv.index("--out") + 1]
+    # FETCH_SIZE correction: x2 for wide coalesced streaming reads (MI355X_MICROARCH.md), x1 for
+    # the chorus' 96-B segment reads -- calibrated per kernel against its known staged bytes
+    # 
+    fscale = float(sys.argv[sys.argv.index("--fetch-scale") + 1]) if "--fetch-scale" in sys.argv else 2.0
     base = os.path.join("gpurun_out", f"pmc_{wl}")
     agg = {}
     for p in sorted(glob.glob(os.path.join(base, "p*"))):
@@ -43,14 +47,29 @@ def main():
         print(f"{k:28s} {agg[k]:.6g}")
     res = {"workload": wl, "instances": n, "block": block, "counters_per_launch": agg}
     if "FETCH_SIZE" in agg and "WRITE_SIZE" in agg:
-        fetch = agg["FETCH_SIZE"] * 1024 * 2.0      # gfx950: FETCH_SIZE = 1/2 of streamed bytes
+        fetch = agg["FETCH_SIZE"] * 1024 * fscale
         write = agg["WRITE_SIZE"] * 1024
         res.update({"fetch_bytes_corrected": fetch, "write_bytes": write,
                     "hbm_bytes_per_launch": fetch + write,
                     "hbm_bytes_per_frame": (fetch + write) / (n * block),
-                    "note": "FETCH_SIZE x2 per MI355X_MICROARCH.md (wide streaming reads); "
-                            "uncalibrated for 4-B scattered accesses"})
+                    "fetch_scale": fscale,
+                    "note": f"FETCH_SIZE x{fscale:g} (per-kernel calibration, DESIGN.md section 5) + WRITE_SIZE"})
         print(f"HBM bytes/launch {fetch + write:.4g}  per frame {(fetch + write) / (n * block):.2f}")
+    # request-size accounting: the L2's memory-side read/write requests by size (gfx950 has 32-,
+    # 64- and 128-B read requests; RDREQ counts requests of every size)
+    if all(k in agg for k in ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum",
+                              "TCC_EA0_RDREQ_128B_sum")):
+        r32, r64, r128 = agg["TCC_EA0_RDREQ_32B_sum"], agg["TCC_EA0_RDREQ_64B_sum"], agg["TCC_EA0_RDREQ_128B_sum"]
+        rd = 32 * r32 + 64 * r64 + 128 * r128
+        res["read_bytes_by_request_size"] = rd
+        res["read_requests_other"] = agg["TCC_EA0_RDREQ_sum"] - r32 - r64 - r128
+        print(f"read bytes by request size {rd:.4g} (per frame {rd / (n * block):.2f}); "
+              f"unsized requests {res['read_requests_other']:.4g}")
+    if "TCC_EA0_WRREQ_sum" in agg and "TCC_EA0_WRREQ_64B_sum" in agg:
+        w64 = agg["TCC_EA0_WRREQ_64B_sum"]
+        wr = 64 * w64 + 32 * (agg["TCC_EA0_WRREQ_sum"] - w64)
+        res["write_bytes_by_request_size"] = wr
+        print(f"write bytes by request size {wr:.4g} (per frame {wr / (n * block):.2f})")
     if out:
         with open(out, "w") as f:
             json.dump(res, f, indent=1)
