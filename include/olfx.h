@@ -65,7 +65,7 @@ enum {
 /* ---- parameters (field index, value is what the reference setter takes) ---- */
 /* Dattorro: verb.h:10-16 */
 enum {
-    OLFX_DT_PREDELAY = 0,        /* [0,1] x 4800 samples; ENGINE-WIDE (uniform taps keep rings coalesced) */
+    OLFX_DT_PREDELAY = 0,        /* setPreDelay: [0,1] x 4800 samples, per instance */
     OLFX_DT_PREFILTER,           /* setPreFilter */
     OLFX_DT_INPUT_DIFFUSION1,    /* setInputDiffusion1 */
     OLFX_DT_INPUT_DIFFUSION2,    /* setInputDiffusion2 */

@@ -106,7 +106,9 @@ class ReverbBank : public Engine {
 public:
     ReverbBank(uint32_t n_inst, float sample_rate, uint32_t block = 256, int device = 0)
         : Engine(OLFX_KIND_DATTORRO, n_inst, sample_rate, block, device) {}
-    /* Engine-wide: a uniform pre-delay keeps the rings' tap loads coalesced. */
+    /* Per instance, [0,1] x 4800 samples (verb.cpp:137-139); instances of one wave sharing a value
+       keep the pre-delay tap's loads coalesced. */
+    void SetPredelay(uint32_t i, float v) { set(i, OLFX_DT_PREDELAY, v); }
     void SetPredelay(float v) { set_all(OLFX_DT_PREDELAY, v); }
     void SetPrefilter(uint32_t i, float v) { set(i, OLFX_DT_PREFILTER, v); }
     void SetInputDiffusion1(uint32_t i, float v) { set(i, OLFX_DT_INPUT_DIFFUSION1, v); }

@@ -14,9 +14,12 @@
 //     so ~30 x 1 KB loads per wave are in flight while it computes (1 wave per SIMD at 65,536
 //     instances; latency hiding comes from this ILP, not occupancy);
 //   * the 13 ring writes of a chunk leave as one 16-B store per line.
-// Every delay is >= 107 samples, so no chunk reads a group written by itself or by its
-// predecessor; the pre-delay tap, whose delay may be 0..4800, reads frames of the current block
-// from the input buffer and older frames from its ring.  No MFMA: scalar recurrences.
+// Every fixed delay is >= 107 samples, so no chunk reads a group written by itself or by its
+// predecessor.  The pre-delay is per instance (0..4800 samples, verb.cpp:137-139): its tap loads
+// the two groups around t0 - d of the lane's own ring (one 16-B load each; coalesced whenever the
+// wave's instances share d) and takes frames of the current chunk (d < 4) from registers.  Groups
+// written by earlier chunks of this launch are read back by the same lane, in program order.
+// No MFMA: scalar recurrences.
 // Bound: HBM.
 #include "olfx_internal.h"
 
@@ -65,13 +68,19 @@ struct VarTap {
         a0 = *grp<L>(a, q >> 2, i);
         a1 = *grp<L>(a, (q >> 2) + 1u, i);
     }
-    __device__ __forceinline__ void resolve(uint32_t s) {
+    __device__ __forceinline__ void resolve(uint32_t s) {        // s wave-uniform: scalar branch
         switch (s) {
         case 0: v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; break;
         case 1: v[0] = a0.y; v[1] = a0.z; v[2] = a0.w; v[3] = a1.x; break;
         case 2: v[0] = a0.z; v[1] = a0.w; v[2] = a1.x; v[3] = a1.y; break;
         default: v[0] = a0.w; v[1] = a1.x; v[2] = a1.y; v[3] = a1.z; break;
         }
+    }
+    __device__ __forceinline__ void resolve_lane(uint32_t s) {   // s per lane: selects
+        const float w[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            v[k] = s == 0 ? w[k] : (s == 1 ? w[k + 1] : (s == 2 ? w[k + 2] : w[k + 3]));
     }
 };
 
@@ -89,12 +98,12 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v2(DattorroArgs a) {
     const float g_damp = a.coef[DTC_DAMPING * n + i];
     const float g_decay = a.coef[DTC_DECAY * n + i];
     const float g_dd2 = a.coef[DTC_DD2 * n + i];
+    const uint32_t dpre = (uint32_t)a.coef[DTC_PREDELAY * n + i];   // samples, exact integer
     float lp_pre = a.state[DTS_LP_PRE * n + i];
     float lp_a = a.state[DTS_LP_DAMP_A * n + i];
     float lp_b = a.state[DTS_LP_DAMP_B * n + i];
 
     const size_t plane = (size_t)a.n_frames * n;
-    const uint32_t dpre = a.pre_delay;
     const bool stereo = a.in_ch == 2;
 
     // main-time taps (read at t)
@@ -129,8 +138,7 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v2(DattorroArgs a) {
         ap1a.load(a, qa, i);
         ap1b.load(a, qb, i);
         const uint32_t qp = t0 - dpre;
-        const bool pre_ring = f0 < dpre;               // some frame of the chunk predates the block
-        if (pre_ring) pre.load(a, qp, i);
+        pre.load(a, qp, i);                            // groups of earlier chunks (or stale: see below)
         float xin[4], xpd[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -138,26 +146,18 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v2(DattorroArgs a) {
             if (stereo) l = (l + a.in[plane + (size_t)(f0 + k) * n + i]) / 2;
             xin[k] = l;
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t f = f0 + k;
-            if (f >= dpre) {                           // pre-delayed frame lies in this block
-                const uint32_t fs = f - dpre;
-                float l = a.in[(size_t)fs * n + i];
-                if (stereo) l = (l + a.in[plane + (size_t)fs * n + i]) / 2;
-                xpd[k] = l;
-            }
-        }
         // ---- prefetch the fixed taps' next group (consumed by the next chunk) ----
         if (f0 + 4 < a.n_frames) { DT_ALL_TAPS(DT_PREFETCH) }
 
         ap1a.resolve(qa & 3u);
         ap1b.resolve(qb & 3u);
-        if (pre_ring) {
-            pre.resolve(qp & 3u);
+        pre.resolve_lane(qp & 3u);
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (f0 + k < dpre) xpd[k] = pre.v[k];
+        for (int k = 0; k < 4; ++k) {                  // frame t0+k-d lies in this chunk when d <= k
+            float v = pre.v[k];
+#pragma unroll
+            for (int j = 0; j <= k; ++j) v = dpre == (uint32_t)(k - j) ? xin[j] : v;
+            xpd[k] = v;
         }
 
         // ---- the serial recurrence, 4 frames (verb.cpp:273-299, 302-325) ----

@@ -130,6 +130,12 @@ void default_params(int kind, float *p) {
 // ---------------------------------------------------------------------------------------------
 // Coefficient derivation (control rate, host).  These restate the reference setters.
 // ---------------------------------------------------------------------------------------------
+uint32_t dattorro_predelay_samples(float v) {
+    // verb.cpp:137-139: uint16(value * 4800.f); the engine accepts [0, 1]
+    float d = v * 4800.0f;
+    return d <= 0.0f ? 0u : (uint32_t)(uint16_t)d;
+}
+
 void derive_dattorro(const float *p, float *c) {
     c[DTC_PREFILTER] = p[OLFX_DT_PREFILTER];
     c[DTC_IN1] = p[OLFX_DT_INPUT_DIFFUSION1];
@@ -140,12 +146,7 @@ void derive_dattorro(const float *p, float *c) {
     // verb.cpp:49,162-165: clamp(t_sample x, ...) narrows value+0.15 to float
     float x = (float)((double)p[OLFX_DT_DECAY] + 0.15);
     c[DTC_DD2] = x < 0.25f ? 0.25f : (x > 0.5f ? 0.5f : x);
-}
-
-uint32_t dattorro_predelay_samples(float v) {
-    // verb.cpp:137-139: uint16(value * 4800.f); the engine accepts [0, 1]
-    float d = v * 4800.0f;
-    return d <= 0.0f ? 0u : (uint32_t)(uint16_t)d;
+    c[DTC_PREDELAY] = (float)dattorro_predelay_samples(p[OLFX_DT_PREDELAY]);
 }
 
 // chorus: p = [OLFX_CH_*], c = [CHC_*] (u32 words)
@@ -287,7 +288,6 @@ struct olfx_engine {
     float *dt_rings = nullptr;
     float *dt_state = nullptr;
     float *dt_coef = nullptr;
-    uint32_t dt_predelay = 480;
 
     // chorus / pitch-shift (also the chain's first two stages)
     uint32_t psize = 0, csize = 0;
@@ -380,7 +380,6 @@ int upload_params(olfx_engine *e, hipStream_t s) {
             derive_dattorro(p.data() + base, cc);
             for (int k = 0; k < DTC_N; ++k) c[(size_t)k * n + i] = cc[k];
         }
-        e->dt_predelay = dattorro_predelay_samples(e->params[(size_t)(base + OLFX_DT_PREDELAY) * n + 0]);
         HIPCHK(e, hipMemcpyAsync(e->dt_coef, c.data(), c.size() * 4, hipMemcpyHostToDevice, s));
         HIPCHK(e, hipStreamSynchronize(s));
     }
@@ -517,7 +516,6 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hip
         a.n = e->n;
         a.n_frames = n_frames;
         a.t0 = t0 & 0xFFFFu;
-        a.pre_delay = e->dt_predelay;
         a.in_ch = 2;
         return a;
     };
@@ -734,18 +732,15 @@ int olfx_set_params(olfx_engine *e, uint32_t first, uint32_t count, uint32_t fie
         return e->fail(OLFX_E_ARG, "olfx_set_params: range out of bounds");
     for (uint32_t f = 0; f < n_fields; ++f) {
         const uint32_t field = field0 + f;
+        const bool predelay = (e->kind == OLFX_KIND_DATTORRO && field == OLFX_DT_PREDELAY) ||
+                              (e->kind == OLFX_KIND_CHAIN && field == OLFX_CN_VERB0 + OLFX_DT_PREDELAY);
         for (uint32_t k = 0; k < count; ++k) {
             float v = values[(size_t)f * count + k];
             if (!std::isfinite(v)) return e->fail(OLFX_E_ARG, "olfx_set_params: non-finite value");
+            // the pre-delay ring holds MAX_PREDELAY = 4800 samples (verb.cpp:137-139, :177)
+            if (predelay && (v < 0.f || v > 1.f))
+                return e->fail(OLFX_E_ARG, "olfx_set_params: pre-delay outside [0,1]");
             e->params[(size_t)field * e->n + first + k] = v;
-        }
-        // the dattorro pre-delay is engine-wide: uniform taps keep every ring access coalesced
-        const bool predelay = (e->kind == OLFX_KIND_DATTORRO && field == OLFX_DT_PREDELAY) ||
-                              (e->kind == OLFX_KIND_CHAIN && field == OLFX_CN_VERB0 + OLFX_DT_PREDELAY);
-        if (predelay && count) {
-            float v = values[(size_t)f * count];
-            if (v < 0.f || v > 1.f) return e->fail(OLFX_E_ARG, "olfx_set_params: pre-delay outside [0,1]");
-            std::fill(e->params.begin() + (size_t)field * e->n, e->params.begin() + (size_t)(field + 1) * e->n, v);
         }
     }
     if (e->kind == OLFX_KIND_VOICE)

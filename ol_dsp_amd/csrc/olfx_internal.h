@@ -52,7 +52,8 @@ constexpr uint32_t kAp2B_o1 = 335, kAp2B_o2 = 1913;
 constexpr uint32_t kDl2B_o1 = 121, kDl2B_o2 = 1996;
 
 // Derived per-instance coefficients (field-major [DTC_N][n] on the device).
-enum { DTC_PREFILTER = 0, DTC_IN1, DTC_IN2, DTC_DD1, DTC_DAMPING, DTC_DECAY, DTC_DD2, DTC_N };
+// DTC_PREDELAY holds the per-instance pre-delay in samples (an integer 0..4800, exact in fp32).
+enum { DTC_PREFILTER = 0, DTC_IN1, DTC_IN2, DTC_DD1, DTC_DAMPING, DTC_DECAY, DTC_DD2, DTC_PREDELAY, DTC_N };
 // Per-instance recursive scalar state ([DTS_N][n]).
 enum { DTS_LP_PRE = 0, DTS_LP_DAMP_A, DTS_LP_DAMP_B, DTS_N };
 
@@ -75,7 +76,6 @@ struct DattorroArgs {
     uint32_t n;                 // instances
     uint32_t n_frames;
     uint32_t t0;                // stream time (frames since create) of the first frame, mod 2^16
-    uint32_t pre_delay;         // engine-wide pre-delay in samples (0..4800)
     uint32_t in_ch;             // 1 or 2
 };
 

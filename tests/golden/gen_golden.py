@@ -25,7 +25,7 @@ import oracle as O  # noqa: E402
 
 IMPULSE_KAT_FRAMES = [0, 1, 479, 480, 481, 1000, 2000, 4800, 12800, 20800, 28800, 36800, 44800, 47999]
 
-# Dattorro sweep groups: the engine's pre-delay is engine-wide, so each group shares one.
+# Dattorro sweep groups: each group shares one pre-delay (the engine also takes per-instance ones).
 DT_GROUPS = [
     {"pre_delay": 0.1, "n": 8, "frames": 4100, "seed": 1},
     {"pre_delay": 0.0, "n": 8, "frames": 2600, "seed": 2},

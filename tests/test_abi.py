@@ -59,7 +59,7 @@ def test_abi_version_and_kind_info():
     info = ofx.kind_info(ofx.KIND_DATTORRO)
     assert (info.n_params, info.in_channels, info.out_channels) == (7, 2, 2)
     # 42,368 ring floats + 3 recursive scalars + 7 coefficients per instance
-    assert info.state_bytes_per_instance == (42368 + 3 + 7) * 4
+    assert info.state_bytes_per_instance == (42368 + 3 + 8) * 4
     ch = ofx.kind_info(ofx.KIND_CHORUS, 48000.0)
     assert (ch.n_params, ch.in_channels, ch.out_channels) == (8, 2, 2)
     assert ch.state_bytes_per_instance == (2 * (512 + 2048) + 6 + 12) * 4

@@ -86,6 +86,29 @@ def test_dattorro_ragged_vs_oracle(cuda, n):
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
 
+def test_dattorro_per_instance_predelay(cuda):
+    """DattorroVerb_setPreDelay per instance (verb.cpp:137-139): every lane has its own pre-delay
+    tap, including the in-chunk delays 0..3, the chunk edges 4..8, the block edges 255..257 and
+    the maximum 4800; a wave that shares one pre-delay and a wave that mixes them."""
+    edge = np.array([0, 1, 2, 3, 4, 5, 7, 8, 255, 256, 257, 4799, 4800], np.float32) / 4800
+    n = 200
+    rng = np.random.default_rng(77)
+    p = dt_params(rng, n, 0.0)
+    p[0, :64] = 0.3                                               # one uniform wave
+    p[0, 64:64 + len(edge)] = edge
+    p[0, 64 + len(edge):] = rng.uniform(0, 1, n - 64 - len(edge))
+    x = fast_noise(n, 6400, seed=77)
+    e = engine("dattorro", n)
+    e.set_params(0, p)
+    y = run_gpu(e, x, [256] * 20 + [4, 1276], cuda)
+    ref = O.Dattorro(n)
+    for i in range(n):
+        for f in range(7):
+            ref.set(i, f, float(p[f, i]))
+    yr = ref.process(x, threads=8)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
 def test_dattorro_long_run_wraps(cuda):
     """70,000 frames: the modulation turn at t = 32768 and the uint16 wrap of t at 65536."""
     n = 64

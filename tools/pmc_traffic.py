@@ -15,13 +15,15 @@ from collections import defaultdict
 
 
 def load(d, kernel_sub):
-    vals = defaultdict(list)
+    """{kernel: {counter: [per-dispatch values]}} for kernels whose name contains kernel_sub."""
+    vals = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if kernel_sub not in row.get("Kernel_Name", ""):
+                k = row.get("Kernel_Name", "")
+                if kernel_sub not in k:
                     continue
-                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+                vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return vals
 
 
@@ -36,16 +38,21 @@ def main():
     # 
     fscale = float(sys.argv[sys.argv.index("--fetch-scale") + 1]) if "--fetch-scale" in sys.argv else 2.0
     base = os.path.join("gpurun_out", f"pmc_{wl}")
-    agg = {}
+    agg, res_k = {}, {}
     for p in sorted(glob.glob(os.path.join(base, "p*"))):
         if not os.path.isdir(p):
             continue
-        for k, v in load(p, ksub).items():
-            # counter rows are per dispatch (already summed over XCDs/instances by rocprofv3)
-            agg[k] = sum(v) / len(v)
+        # counter rows are per dispatch (already summed over XCDs by rocprofv3); one engine call
+        # launches each matching kernel once (the chain launches three), so per launch =
+        # the sum over kernels of each kernel's per-dispatch mean
+        for kern, cnt in load(p, ksub).items():
+            for k, v in cnt.items():
+                agg[k] = agg.get(k, 0.0) + sum(v) / len(v)
+                res_k.setdefault(kern.split("(")[0], {})[k] = sum(v) / len(v)
     for k in sorted(agg):
         print(f"{k:28s} {agg[k]:.6g}")
-    res = {"workload": wl, "instances": n, "block": block, "counters_per_launch": agg}
+    res = {"workload": wl, "instances": n, "block": block, "counters_per_launch": agg,
+           "counters_per_kernel": res_k}
     if "FETCH_SIZE" in agg and "WRITE_SIZE" in agg:
         fetch = agg["FETCH_SIZE"] * 1024 * fscale
         write = agg["WRITE_SIZE"] * 1024
@@ -70,6 +77,11 @@ def main():
         wr = 64 * w64 + 32 * (agg["TCC_EA0_WRREQ_sum"] - w64)
         res["write_bytes_by_request_size"] = wr
         print(f"write bytes by request size {wr:.4g} (per frame {wr / (n * block):.2f})")
+        if "read_bytes_by_request_size" in res:    # preferred: no width calibration needed
+            tot = res["read_bytes_by_request_size"] + wr
+            res.update({"hbm_bytes_per_launch": tot, "hbm_bytes_per_frame": tot / (n * block),
+                        "method": "TCC_EA0_RDREQ_{32B,64B,128B} x size + TCC_EA0_WRREQ(_64B) x size; "
+                                  "FETCH_SIZE x fetch_scale + WRITE_SIZE kept as the cross-check"})
     if out:
         with open(out, "w") as f:
             json.dump(res, f, indent=1)
