@@ -15,11 +15,10 @@
 //     instances; latency hiding comes from this ILP, not occupancy);
 //   * the 13 ring writes of a chunk leave as one 16-B store per line.
 // Every fixed delay is >= 107 samples, so no chunk reads a group written by itself or by its
-// predecessor.  The pre-delay is per instance (0..4800 samples, verb.cpp:137-139): its tap loads
-// the two groups around t0 - d of the lane's own ring (one 16-B load each; coalesced whenever the
-// wave's instances share d) and takes frames of the current chunk (d < 4) from registers.  Groups
-// written by earlier chunks of this launch are read back by the same lane, in program order.
-// No MFMA: scalar recurrences.
+// predecessor.  The two modulated all-pass taps and the per-instance pre-delay tap are carried
+// the same way (one new group per chunk; see ModTap / PreTap), so every ring byte is read once.
+// Groups written by earlier chunks of this launch are read back by the lane that wrote them, in
+// program order.  No MFMA: scalar recurrences.
 // Bound: HBM.
 #include "olfx_internal.h"
 
@@ -58,35 +57,95 @@ struct Tap {
     }
 };
 
-// A tap whose delay changes at run time (the modulated tank all-passes, the pre-delay ring):
-// both groups are loaded for each chunk (uniform shift chosen with a scalar branch).
-template <int L>
-struct VarTap {
-    float4 a0, a1;
+// A modulated tank all-pass tap (verb.cpp:262-270): delay D + ex(t), with ex wave-uniform and
+// constant for 512 chunks at a time.  Carried like a fixed tap (one new group per chunk); when ex
+// steps, both groups are reloaded (a wave-uniform branch, once per 2048 frames).
+template <int L, uint32_t D>
+struct ModTap {
+    float4 cur, nxt, pre;
     float v[4];
-    __device__ __forceinline__ void load(const DattorroArgs &a, uint32_t q, uint32_t i) {
-        a0 = *grp<L>(a, q >> 2, i);
-        a1 = *grp<L>(a, (q >> 2) + 1u, i);
+    uint32_t q;                                       // position of the chunk's frame 0
+    __device__ __forceinline__ void prime(const DattorroArgs &a, uint32_t t0, uint32_t i) {
+        q = t0 - (D + dt_ap1_extra(t0 & 0xFFFFu));
+        cur = *grp<L>(a, q >> 2, i);
+        nxt = *grp<L>(a, (q >> 2) + 1u, i);
     }
-    __device__ __forceinline__ void resolve(uint32_t s) {        // s wave-uniform: scalar branch
-        switch (s) {
-        case 0: v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; break;
-        case 1: v[0] = a0.y; v[1] = a0.z; v[2] = a0.w; v[3] = a1.x; break;
-        case 2: v[0] = a0.z; v[1] = a0.w; v[2] = a1.x; v[3] = a1.y; break;
-        default: v[0] = a0.w; v[1] = a1.x; v[2] = a1.y; v[3] = a1.z; break;
-        }
+    __device__ __forceinline__ void prefetch(const DattorroArgs &a, uint32_t i) {
+        pre = *grp<L>(a, (q >> 2) + 2u, i);
     }
-    __device__ __forceinline__ void resolve_lane(uint32_t s) {   // s per lane: selects
-        const float w[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    __device__ __forceinline__ void resolve() {       // shift q & 3 (wave-uniform) by selects
+        const uint32_t s = q & 3u;
+        const float w[8] = {cur.x, cur.y, cur.z, cur.w, nxt.x, nxt.y, nxt.z, nxt.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             v[k] = s == 0 ? w[k] : (s == 1 ? w[k + 1] : (s == 2 ? w[k + 2] : w[k + 3]));
     }
+    __device__ __forceinline__ void advance(const DattorroArgs &a, uint32_t t0n, uint32_t i) {
+        const uint32_t qn = t0n - (D + dt_ap1_extra(t0n & 0xFFFFu));
+        if (qn == q + 4u) {
+            cur = nxt; nxt = pre;
+        } else {                                      // ex stepped: the window moved by one
+            cur = *grp<L>(a, qn >> 2, i);
+            nxt = *grp<L>(a, (qn >> 2) + 1u, i);
+        }
+        q = qn;
+    }
+};
+
+// The per-instance pre-delay tap (verb.cpp:137-139, :273).  Delay d is constant over a launch.
+//   d >= 9 : carried ring window with a per-lane shift (t0 - d) & 3: the group prefetched during
+//            chunk c (before chunk c's own store) is ((t0 - d) >> 2) + 2 <= chunk c-1's group;
+//   d <= 8 : frames of this chunk come from registers, older frames of this launch from the input
+//            buffer (re-summed exactly like xin), frames of earlier launches from the ring.  This
+//            branch is skipped by every wave whose lanes all have d >= 9.
+// Lanes of one wave that share d issue coalesced loads.
+struct PreTap {
+    float4 cur, nxt, pre;
+    uint32_t s;
+    __device__ __forceinline__ void prime(const DattorroArgs &a, uint32_t t0, uint32_t d, uint32_t i) {
+        const uint32_t q = t0 - d;
+        s = q & 3u;
+        cur = *grp<DT_PRE>(a, q >> 2, i);
+        nxt = *grp<DT_PRE>(a, (q >> 2) + 1u, i);
+    }
+    __device__ __forceinline__ void prefetch(const DattorroArgs &a, uint32_t t0, uint32_t d, uint32_t i) {
+        pre = *grp<DT_PRE>(a, ((t0 - d) >> 2) + 2u, i);
+    }
+    // xpd[k] = mono input at t0 + k - d
+    __device__ __forceinline__ void resolve(const DattorroArgs &a, const float xin[4], uint32_t f0,
+                                            uint32_t t0, uint32_t d, uint32_t i, bool stereo,
+                                            float xpd[4]) const {
+        const float w[8] = {cur.x, cur.y, cur.z, cur.w, nxt.x, nxt.y, nxt.z, nxt.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            xpd[k] = s == 0 ? w[k] : (s == 1 ? w[k + 1] : (s == 2 ? w[k + 2] : w[k + 3]));
+        if (d <= 8u) {
+            const size_t plane = (size_t)a.n_frames * a.n;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float v;
+                if ((uint32_t)k >= d) {                          // this chunk
+                    v = xin[0];
+#pragma unroll
+                    for (int j = 1; j <= k; ++j) v = (uint32_t)(k - j) == d ? xin[j] : v;
+                } else if (f0 + k >= d) {                        // earlier chunk of this launch
+                    const size_t f = f0 + k - d;
+                    v = a.in[f * a.n + i];
+                    if (stereo) v = (v + a.in[plane + f * a.n + i]) / 2;
+                } else {                                         // an earlier launch
+                    const uint32_t p = t0 + k - d;
+                    v = el(*grp<DT_PRE>(a, p >> 2, i), (int)(p & 3u));
+                }
+                xpd[k] = v;
+            }
+        }
+    }
+    __device__ __forceinline__ void advance() { cur = nxt; nxt = pre; }
 };
 
 }  // namespace
 
-__global__ __launch_bounds__(64, 1) void dattorro_block_v2(DattorroArgs a) {
+__global__ __launch_bounds__(64, 1) void dattorro_block_v3(DattorroArgs a) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
     const uint32_t n = a.n;
@@ -118,7 +177,7 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v2(DattorroArgs a) {
     Tap<DT_DL1A, kDl1A_o1, 1> oR1; Tap<DT_DL1A, kDl1A_o2, 1> oR2; Tap<DT_AP2A, kAp2A_o2, 1> oR3;
     Tap<DT_DL2A, kDl2A_o2, 1> oR4; Tap<DT_DL1B, kDl1B_o3, 1> oR5; Tap<DT_AP2B, kAp2B_o1, 1> oR6;
     Tap<DT_DL2B, kDl2B_o1, 1> oR7;
-    VarTap<DT_AP1A> ap1a; VarTap<DT_AP1B> ap1b; VarTap<DT_PRE> pre;
+    ModTap<DT_AP1A, kDtDelay[DT_AP1A]> ap1a; ModTap<DT_AP1B, kDtDelay[DT_AP1B]> ap1b; PreTap pre;
 
 #define DT_ALL_TAPS(OP) OP(in0) OP(in1) OP(in2) OP(in3) OP(fbA) OP(fbB) OP(dl1a) OP(dl1b) OP(ap2a) OP(ap2b) \
     OP(oL1) OP(oL2) OP(oL3) OP(oL4) OP(oL5) OP(oL6) OP(oL7) OP(oR1) OP(oR2) OP(oR3) OP(oR4) OP(oR5) OP(oR6) OP(oR7)
@@ -127,18 +186,14 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v2(DattorroArgs a) {
 #define DT_ADVANCE(T) T.advance();
 
     DT_ALL_TAPS(DT_PRIME)
+    ap1a.prime(a, a.t0, i);
+    ap1b.prime(a, a.t0, i);
+    pre.prime(a, a.t0, dpre, i);
 
     for (uint32_t f0 = 0; f0 < a.n_frames; f0 += 4) {
         const uint32_t t0 = a.t0 + f0;                 // multiple of 4
-        const uint32_t t16 = t0 & 0xFFFFu;
 
-        // ---- this chunk's variable taps and inputs ----
-        const uint32_t ex = dt_ap1_extra(t16);         // constant over the chunk (changes at 2048k)
-        const uint32_t qa = t0 - (kDtDelay[DT_AP1A] + ex), qb = t0 - (kDtDelay[DT_AP1B] + ex);
-        ap1a.load(a, qa, i);
-        ap1b.load(a, qb, i);
-        const uint32_t qp = t0 - dpre;
-        pre.load(a, qp, i);                            // groups of earlier chunks (or stale: see below)
+        // ---- this chunk's inputs ----
         float xin[4], xpd[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -146,19 +201,16 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v2(DattorroArgs a) {
             if (stereo) l = (l + a.in[plane + (size_t)(f0 + k) * n + i]) / 2;
             xin[k] = l;
         }
-        // ---- prefetch the fixed taps' next group (consumed by the next chunk) ----
-        if (f0 + 4 < a.n_frames) { DT_ALL_TAPS(DT_PREFETCH) }
-
-        ap1a.resolve(qa & 3u);
-        ap1b.resolve(qb & 3u);
-        pre.resolve_lane(qp & 3u);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {                  // frame t0+k-d lies in this chunk when d <= k
-            float v = pre.v[k];
-#pragma unroll
-            for (int j = 0; j <= k; ++j) v = dpre == (uint32_t)(k - j) ? xin[j] : v;
-            xpd[k] = v;
+        // ---- prefetch every tap's next group (consumed by the next chunk) ----
+        if (f0 + 4 < a.n_frames) {
+            DT_ALL_TAPS(DT_PREFETCH)
+            ap1a.prefetch(a, i);
+            ap1b.prefetch(a, i);
+            pre.prefetch(a, t0, dpre, i);
         }
+        ap1a.resolve();
+        ap1b.resolve();
+        pre.resolve(a, xin, f0, t0, dpre, i, stereo, xpd);
 
         // ---- the serial recurrence, 4 frames (verb.cpp:273-299, 302-325) ----
         float w_in0[4], w_in1[4], w_in2[4], w_in3[4], w_ap1a[4], w_dl1a[4], w_ap2a[4], w_dl2a[4];
@@ -226,6 +278,11 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v2(DattorroArgs a) {
             a.out[plane + (size_t)(f0 + k) * n + i] = o_r[k];
         }
         DT_ALL_TAPS(DT_ADVANCE)
+        if (f0 + 4 < a.n_frames) {
+            ap1a.advance(a, t0 + 4u, i);
+            ap1b.advance(a, t0 + 4u, i);
+        }
+        pre.advance();
     }
 #undef DT_ALL_TAPS
 #undef DT_PRIME
@@ -242,7 +299,7 @@ hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s) {
     if ((a.t0 & 3u) || (a.n_frames & 3u)) return hipErrorInvalidValue;   // 4-frame chunks
     const uint32_t threads = 64;      // one wave per workgroup: spreads small engines over all CUs
     const uint32_t blocks = (a.n + threads - 1) / threads;
-    hipLaunchKernelGGL(dattorro_block_v2, dim3(blocks), dim3(threads), 0, s, a);
+    hipLaunchKernelGGL(dattorro_block_v3, dim3(blocks), dim3(threads), 0, s, a);
     return hipGetLastError();
 }
 
