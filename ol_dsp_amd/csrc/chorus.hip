@@ -38,14 +38,25 @@ namespace olfx {
 
 namespace {
 
-constexpr int kChunk = 16;                  // frames per chunk
-constexpr int kWin = 24;                    // floats staged per tap window (6 x float4)
-constexpr int kParts = kWin / 4;
+// Chunk geometry, a compile-time parameter of the kernel: CH frames per chunk, windows of
+// CH + 8 floats per tap.  Bigger chunks touch fewer 128-B lines per frame (the windows of
+// consecutive chunks share lines that L2 no longer holds when the next chunk comes round) but
+// need more LDS per wave.
 constexpr int kThreads = 256;
 constexpr int kRow = 64;                    // LDS slot stride: one wave's lanes
-constexpr int kSlots = kWin + 1;            // + one junk slot per tap (branch-free guarded stores)
-constexpr int kRegion = 3 * kSlots * kRow;  // floats of LDS per wave (>= 64 lanes x 32 staging)
-static_assert(kRegion >= 64 * 32, "staging area must fit in the window region");
+template <int CH>
+struct Geo {
+    static constexpr int kChunk = CH;                   // frames per chunk
+    static constexpr int kWin = CH + 8;                 // floats staged per tap window
+    static constexpr int kParts = kWin / 4;             // float4 pieces per window
+    static constexpr int kSlots = kWin + 1;             // + one junk slot per tap (branch-free stores)
+    static constexpr int kRegion = 3 * kSlots * kRow;   // floats of LDS per wave
+    // per-lane staging: x then pitch outputs; the +4 pad staggers lanes across LDS banks so the
+    // 16-B staging writes (8 lanes per pass) and the cooperative 16-B reads are conflict-free
+    static constexpr int kStage = 2 * CH + 4;
+    static constexpr int kPieces = CH / 4;              // 16-B pieces of one owner's ring run
+    static_assert(kRegion >= 64 * kStage, "staging area must fit in the window region");
+};
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t Rsrc;
@@ -95,6 +106,7 @@ struct Plan {
     bool okA, okB;
 };
 
+template <int kWin>
 __device__ __forceinline__ Plan plan_chunk(uint32_t lfo_acc, uint32_t lfo_inc, uint32_t lfo_off, uint32_t ps_acc,
                                            uint32_t ps_inc, int C, float D, float W, float pmax, float cmax,
                                            bool full) {
@@ -129,12 +141,17 @@ __device__ __forceinline__ Plan plan_chunk(uint32_t lfo_acc, uint32_t lfo_inc, u
 
 }  // namespace
 
-template <bool FULL>
-__global__ __launch_bounds__(kThreads, 2) void chorus_block_v8(ChorusArgs a) {
+template <bool FULL, int CH>
+__global__ __launch_bounds__(kThreads, CH <= 16 ? 2 : 1) void chorus_block_v9(ChorusArgs a) {
+    using G = Geo<CH>;
+    constexpr int kChunk = G::kChunk, kWin = G::kWin, kParts = G::kParts, kSlots = G::kSlots;
+    constexpr int kRegion = G::kRegion, kStage = G::kStage, kPieces = G::kPieces;
     extern __shared__ __attribute__((aligned(16))) float lds[];   // [wave][3 taps][kWin][kRow]
     const uint32_t tid = threadIdx.x;
-    const uint32_t g = blockIdx.x * kThreads + tid;
-    const uint32_t wave = g >> 6, lane = g & 63u;
+    // wave index made provably wave-uniform (SGPR): the buffer descriptors and frame offsets
+    // derived from it stay scalar, so no waterfall loops around the buffer ops
+    const uint32_t wib = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint32_t wave = blockIdx.x * (kThreads / 64) + wib, lane = tid & 63u;
     const uint32_t ch = wave & 1u;
     const uint32_t inst0 = (wave >> 1) * 64u;          // first instance of this wave
     const uint32_t n = a.n;
@@ -175,12 +192,12 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v8(ChorusArgs a) {
     const uint32_t own_pb = (i * 2u + ch) * a.psize * 4u;   // this lane's pitch ring, bytes
 
     // this wave's LDS region: windows [tap][slot][lane]; between uses it also stages ring stores
-    // as [lane][32] (x in 0..15, pitch-shifter outputs in 16..31)
-    float *region = lds + (tid >> 6) * kRegion;
+    // as [lane][2 CH] (x in 0..CH-1, pitch-shifter outputs in CH..2CH-1)
+    float *region = lds + wib * kRegion;
     float *wP0 = region + 0 * kSlots * kRow + lane;
     float *wP1 = region + 1 * kSlots * kRow + lane;
     float *wC = region + 2 * kSlots * kRow + lane;
-    float *stage = region + lane * 32u;
+    float *stage = region + lane * (uint32_t)kStage;
 
     // cooperative-load geometry: in part-load r (0..5) of a tap, this lane fetches float4 m of
     // owner lane o's window, 6 consecutive lanes per owner
@@ -214,12 +231,12 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v8(ChorusArgs a) {
         }
     };
     // Cooperative ring store of a chunk: every lane has staged its C consecutive samples at
-    // stage[base..base+C); 4 consecutive lanes then write one owner's 64 B with 16-B stores.
+    // stage[base..base+C); CH/4 consecutive lanes then write one owner's run with 16-B stores.
     auto coop_store = [&](bool pitch, uint32_t base, uint32_t wpos, int C) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint32_t q = (uint32_t)r * 64u + lane, o = q >> 2, p4 = 4u * (q & 3u);
-            const float4 v = *(const float4 *)(region + o * 32u + base + p4);
+        for (int r = 0; r < kPieces; ++r) {
+            const uint32_t q = (uint32_t)r * 64u + lane, o = q / (uint32_t)kPieces, p4 = 4u * (q % (uint32_t)kPieces);
+            const float4 v = *(const float4 *)(region + o * (uint32_t)kStage + base + p4);
             const uint32_t oi = inst0 + o;
             if (oi < n && (int)p4 < C) {
                 if (pitch) st4(rP, (oi * 2u + ch) * a.psize * 4u + ((wpos + p4) & pmask) * 4u, v);
@@ -239,7 +256,7 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v8(ChorusArgs a) {
     for (int k = 0; k < kChunk; ++k) x[k] = k < C ? ld1(rIn, io_v, (uint32_t)k * frame_b) : 0.f;
     stage_run(x, 0);
     coop_store(true, 0, a.t0, C);
-    Plan pl = plan_chunk(lfo_acc, lfo_inc, lfo_off, ps_acc, ps_inc, C, D, W, pmax, cmax, full);
+    Plan pl = plan_chunk<kWin>(lfo_acc, lfo_inc, lfo_off, ps_acc, ps_inc, C, D, W, pmax, cmax, full);
     load_windows(pl, a.t0);
 
     for (uint32_t f0 = 0; f0 < nf; f0 += kChunk) {
@@ -283,7 +300,7 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v8(ChorusArgs a) {
 #pragma unroll
             for (int k = 0; k < kChunk; ++k)
                 xn[k] = k < Cn ? ld1(rIn, io_v, (f0 + kChunk + (uint32_t)k) * frame_b) : 0.f;
-            pl = plan_chunk(lfo_acc + (uint32_t)C * lfo_inc, lfo_inc, lfo_off, ps_acc + (uint32_t)C * ps_inc,
+            pl = plan_chunk<kWin>(lfo_acc + (uint32_t)C * lfo_inc, lfo_inc, lfo_off, ps_acc + (uint32_t)C * ps_inc,
                             ps_inc, Cn, D, W, pmax, cmax, full);
             load_windows(pl, w0 + kChunk);
         }
@@ -346,8 +363,8 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v8(ChorusArgs a) {
             for (int k = 0; k < kChunk; ++k) frame(std::true_type{}, k);
         }
         if (full) {   // the chunk's windows are dead: stage its pitch-shifter outputs, store cooperatively
-            stage_run(psv, 16);
-            coop_store(false, 16, w0, C);
+            stage_run(psv, kChunk);
+            coop_store(false, kChunk, w0, C);
         }
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) x[k] = xn[k];
@@ -362,17 +379,27 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v8(ChorusArgs a) {
     a.state[(ch ? CHS_Z2R : CHS_Z2L) * n + i] = __float_as_uint(z2);
 }
 
+template <int CH>
+static void launch_geo(const ChorusArgs &a, hipStream_t s) {
+    const uint32_t groups = (a.n + 63) / 64;            // 64-instance groups, 2 waves each
+    const uint32_t blocks = (groups * 2 * 64 + kThreads - 1) / kThreads;
+    const size_t lds = (size_t)(kThreads / 64) * Geo<CH>::kRegion * sizeof(float);
+    if (a.mode == 0) hipLaunchKernelGGL((chorus_block_v9<true, CH>), dim3(blocks), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL((chorus_block_v9<false, CH>), dim3(blocks), dim3(kThreads), lds, s, a);
+}
+
 hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
     if (a.n_frames & 3u) return hipErrorInvalidValue;
     // 32-bit buffer offsets: rings and each audio plane must stay below 4 GiB
     if ((uint64_t)a.n * 2 * a.csize * 4 >= (1ull << 32) || (uint64_t)a.n_frames * a.n * 4 >= (1ull << 32))
         return hipErrorInvalidValue;
-    const uint32_t groups = (a.n + 63) / 64;            // 64-instance groups, 2 waves each
-    const uint32_t blocks = (groups * 2 * 64 + kThreads - 1) / kThreads;
-    const size_t lds = (size_t)(kThreads / 64) * kRegion * sizeof(float);
-    if (a.mode == 0) hipLaunchKernelGGL(chorus_block_v8<true>, dim3(blocks), dim3(kThreads), lds, s, a);
-    else hipLaunchKernelGGL(chorus_block_v8<false>, dim3(blocks), dim3(kThreads), lds, s, a);
+    static const int chunk = [] {
+        const char *e = getenv("OLFX_CHORUS_CHUNK");
+        return e ? atoi(e) : 16;
+    }();
+    if (chunk == 32) launch_geo<32>(a, s);
+    else launch_geo<16>(a, s);
     return hipGetLastError();
 }
 
