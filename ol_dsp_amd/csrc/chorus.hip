@@ -38,25 +38,8 @@ namespace olfx {
 
 namespace {
 
-// Chunk geometry, a compile-time parameter of the kernel: CH frames per chunk, windows of
-// CH + 8 floats per tap.  Bigger chunks touch fewer 128-B lines per frame (the windows of
-// consecutive chunks share lines that L2 no longer holds when the next chunk comes round) but
-// need more LDS per wave.
 constexpr int kThreads = 256;
 constexpr int kRow = 64;                    // LDS slot stride: one wave's lanes
-template <int CH>
-struct Geo {
-    static constexpr int kChunk = CH;                   // frames per chunk
-    static constexpr int kWin = CH + 8;                 // floats staged per tap window
-    static constexpr int kParts = kWin / 4;             // float4 pieces per window
-    static constexpr int kSlots = kWin + 1;             // + one junk slot per tap (branch-free stores)
-    static constexpr int kRegion = 3 * kSlots * kRow;   // floats of LDS per wave
-    // per-lane staging: x then pitch outputs; the +4 pad staggers lanes across LDS banks so the
-    // 16-B staging writes (8 lanes per pass) and the cooperative 16-B reads are conflict-free
-    static constexpr int kStage = 2 * CH + 4;
-    static constexpr int kPieces = CH / 4;              // 16-B pieces of one owner's ring run
-    static_assert(kRegion >= 64 * kStage, "staging area must fit in the window region");
-};
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t Rsrc;
@@ -141,23 +124,22 @@ __device__ __forceinline__ Plan plan_chunk(uint32_t lfo_acc, uint32_t lfo_inc, u
 
 }  // namespace
 
-template <bool FULL, int CH>
-__global__ __launch_bounds__(kThreads, CH <= 16 ? 2 : 1) void chorus_block_v9(ChorusArgs a) {
-    using G = Geo<CH>;
-    constexpr int kChunk = G::kChunk, kWin = G::kWin, kParts = G::kParts, kSlots = G::kSlots;
-    constexpr int kRegion = G::kRegion, kStage = G::kStage, kPieces = G::kPieces;
-    extern __shared__ __attribute__((aligned(16))) float lds[];   // [wave][3 taps][kWin][kRow]
+template <bool FULL>
+__global__ __launch_bounds__(kThreads, 2) void chorus_block_v10(ChorusArgs a) {
+    constexpr int kChunk = 16, kWin = 24, kSlots = kWin + 1;
+    constexpr int kRegion = 3 * kSlots * kRow;          // floats of LDS per wave (4,800)
+    constexpr int kStride = 36;                         // staging floats per instance (32 + pad)
+    static_assert(2 * 32 * kStride <= kRegion, "staging must fit in the window region");
+    extern __shared__ __attribute__((aligned(16))) float lds[];   // [wave][3 taps][kSlots][kRow]
     const uint32_t tid = threadIdx.x;
-    // wave index made provably wave-uniform (SGPR): the buffer descriptors and frame offsets
-    // derived from it stay scalar, so no waterfall loops around the buffer ops
     const uint32_t wib = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
     const uint32_t wave = blockIdx.x * (kThreads / 64) + wib, lane = tid & 63u;
-    const uint32_t ch = wave & 1u;
-    const uint32_t inst0 = (wave >> 1) * 64u;          // first instance of this wave
+    const uint32_t j = lane >> 1, ch = lane & 1u;       // lane = (instance j of the wave, channel)
+    const uint32_t inst0 = wave * 32u;                  // first instance of this wave (uniform)
     const uint32_t n = a.n;
-    if (inst0 >= n) return;                            // whole wave idle (wave-uniform)
-    const uint32_t i_raw = inst0 + lane;
-    const bool valid = i_raw < n;                      // invalid lanes still help load windows
+    if (inst0 >= n) return;
+    const uint32_t i_raw = inst0 + j;
+    const bool valid = i_raw < n;                       // invalid lanes still help load windows
     const uint32_t i = valid ? i_raw : n - 1;
     constexpr bool full = FULL;
 
@@ -182,72 +164,80 @@ __global__ __launch_bounds__(kThreads, CH <= 16 ? 2 : 1) void chorus_block_v9(Ch
     const uint32_t nf = a.n_frames;
     const uint32_t pmask = a.psize - 1u, cmask = a.csize - 1u;
     const float pmax = (float)(a.psize - 2u), cmax = (float)(a.csize - 2u);
-    // buffer descriptors (wave-uniform); offsets in bytes, < 2^32 (launch_chorus checks)
+    // buffer descriptors (wave-uniform); byte offsets < 2^32 (launch_chorus checks)
     const Rsrc rP = rsrc(a.pitch_ring, (uint64_t)n * 2 * a.psize * 4);
     const Rsrc rC = rsrc(a.chorus_ring, (uint64_t)n * 2 * a.csize * 4);
-    const Rsrc rIn = rsrc(a.in + (size_t)ch * nf * n, (uint64_t)nf * n * 4);
-    const Rsrc rOut = rsrc(a.out + (size_t)ch * nf * n, (uint64_t)nf * n * 4);
-    const uint32_t io_v = i * 4u, frame_b = n * 4u;
-    const uint32_t out_v = valid ? io_v : 0xFFFFFFF0u;   // invalid lanes: buffer range check drops
-    const uint32_t own_pb = (i * 2u + ch) * a.psize * 4u;   // this lane's pitch ring, bytes
+    const Rsrc rIn = rsrc(a.in, (uint64_t)2 * nf * n * 4);
+    const Rsrc rOut = rsrc(a.out, (uint64_t)2 * nf * n * 4);
+    const uint32_t io_v = ch * nf * n * 4u + i * 4u, frame_b = n * 4u;
+    const uint32_t out_v = valid ? io_v : 0xFFFFFFF0u;  // invalid lanes: buffer range check drops
+    const uint32_t pstride = a.psize * 8u, cstride = a.csize * 8u;   // bytes per instance ring
+    const uint32_t own_pb = i * pstride + ch * 4u;       // this lane's samples in its pitch ring
 
     // this wave's LDS region: windows [tap][slot][lane]; between uses it also stages ring stores
-    // as [lane][2 CH] (x in 0..CH-1, pitch-shifter outputs in CH..2CH-1)
+    // as [instance][frame][ch] (x at 0, pitch-shifter outputs at 32 * kStride)
     float *region = lds + wib * kRegion;
     float *wP0 = region + 0 * kSlots * kRow + lane;
     float *wP1 = region + 1 * kSlots * kRow + lane;
     float *wC = region + 2 * kSlots * kRow + lane;
-    float *stage = region + lane * (uint32_t)kStage;
 
-    // cooperative-load geometry: in part-load r (0..5) of a tap, this lane fetches float4 m of
-    // owner lane o's window, 6 consecutive lanes per owner
-    auto owner = [&](int r) { return ((uint32_t)r * 64u + lane) / kParts; };
-    auto piece = [&](int r) { return ((uint32_t)r * 64u + lane) % kParts; };
-    float4 vA[kParts], vB[kParts], vC[kParts];
+    // cooperative-load geometry: in part-load r (0..5) of a tap, this lane fetches piece m
+    // (positions 2m, 2m+1 of both channels = 16 B) of instance jj's stereo window; 4 consecutive
+    // lanes cover 64 contiguous bytes of one instance, 16 instances per load
+    auto ljj = [&](int r) { return (((uint32_t)r * 64u + lane) >> 2) & 31u; };
+    auto lm = [&](int r) { return ((((uint32_t)r * 64u + lane) >> 7) << 2) | (lane & 3u); };
+    float4 vA[6], vB[6], vC[6];
     auto load_windows = [&](const Plan &pl, uint32_t wpos) {
 #pragma unroll
-        for (int r = 0; r < kParts; ++r) {
-            const uint32_t o = owner(r), m4 = 4u * piece(r);
-            const int oA = __builtin_amdgcn_ds_bpermute((int)(o << 2), pl.sA);
-            const int oB = __builtin_amdgcn_ds_bpermute((int)(o << 2), pl.sB);
-            const int oC = __builtin_amdgcn_ds_bpermute((int)(o << 2), pl.sC);
-            const uint32_t oi = min(inst0 + o, n - 1);   // lanes past n load a harmless duplicate
-            const uint32_t pb = (oi * 2u + ch) * a.psize * 4u;
-            vA[r] = ld4(rP, pb + ((wpos + oA + m4) & pmask) * 4u);
-            vB[r] = ld4(rP, pb + ((wpos + oB + m4) & pmask) * 4u);
-            if (full) vC[r] = ld4(rC, (oi * 2u + ch) * a.csize * 4u + ((wpos + oC + m4) & cmask) * 4u);
+        for (int r = 0; r < 6; ++r) {
+            const uint32_t jj = ljj(r), m2 = 2u * lm(r);
+            const int src = (int)(jj << 3);              // lane 2 jj holds instance jj's plan
+            const int oA = __builtin_amdgcn_ds_bpermute(src, pl.sA);
+            const int oB = __builtin_amdgcn_ds_bpermute(src, pl.sB);
+            const int oC = __builtin_amdgcn_ds_bpermute(src, pl.sC);
+            const uint32_t oi = min(inst0 + jj, n - 1);   // lanes past n load a harmless duplicate
+            vA[r] = ld4(rP, oi * pstride + ((wpos + oA + m2) & pmask) * 8u);
+            vB[r] = ld4(rP, oi * pstride + ((wpos + oB + m2) & pmask) * 8u);
+            if (full) vC[r] = ld4(rC, oi * cstride + ((wpos + oC + m2) & cmask) * 8u);
         }
     };
+    // de-interleave each piece into the two channel columns of its instance: (L,R) pairs are
+    // adjacent columns of one slot row, one 8-B LDS write per position
     auto stage_windows = [&]() {
 #pragma unroll
-        for (int r = 0; r < kParts; ++r) {
-            float *pA = region + owner(r) + 4u * piece(r) * kRow;
+        for (int r = 0; r < 6; ++r) {
+            float *pA = region + 2u * lm(r) * kRow + 2u * ljj(r);
             float *pB = pA + kSlots * kRow, *pC = pA + 2 * kSlots * kRow;
-            pA[0] = vA[r].x; pA[kRow] = vA[r].y; pA[2 * kRow] = vA[r].z; pA[3 * kRow] = vA[r].w;
-            pB[0] = vB[r].x; pB[kRow] = vB[r].y; pB[2 * kRow] = vB[r].z; pB[3 * kRow] = vB[r].w;
+            *(float2 *)pA = make_float2(vA[r].x, vA[r].y);
+            *(float2 *)(pA + kRow) = make_float2(vA[r].z, vA[r].w);
+            *(float2 *)pB = make_float2(vB[r].x, vB[r].y);
+            *(float2 *)(pB + kRow) = make_float2(vB[r].z, vB[r].w);
             if (full) {
-                pC[0] = vC[r].x; pC[kRow] = vC[r].y; pC[2 * kRow] = vC[r].z; pC[3 * kRow] = vC[r].w;
+                *(float2 *)pC = make_float2(vC[r].x, vC[r].y);
+                *(float2 *)(pC + kRow) = make_float2(vC[r].z, vC[r].w);
             }
         }
     };
-    // Cooperative ring store of a chunk: every lane has staged its C consecutive samples at
-    // stage[base..base+C); CH/4 consecutive lanes then write one owner's run with 16-B stores.
+    // Cooperative ring store of a chunk: the lanes have staged [instance][frame][ch] at
+    // region + base; 8 consecutive lanes then write one instance's 128-B stereo run.
+    auto stage_run = [&](const float (&v)[kChunk], uint32_t base) {
+        float *st = region + base + j * kStride + ch;
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k) st[2 * k] = v[k];
+    };
     auto coop_store = [&](bool pitch, uint32_t base, uint32_t wpos, int C) {
 #pragma unroll
-        for (int r = 0; r < kPieces; ++r) {
-            const uint32_t q = (uint32_t)r * 64u + lane, o = q / (uint32_t)kPieces, p4 = 4u * (q % (uint32_t)kPieces);
-            const float4 v = *(const float4 *)(region + o * (uint32_t)kStage + base + p4);
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t q = (uint32_t)r * 64u + lane, o = q >> 3, f2 = 2u * (q & 7u);
+            const float4 v = *(const float4 *)(region + base + o * kStride + 2u * f2);
             const uint32_t oi = inst0 + o;
-            if (oi < n && (int)p4 < C) {
-                if (pitch) st4(rP, (oi * 2u + ch) * a.psize * 4u + ((wpos + p4) & pmask) * 4u, v);
-                else st4(rC, (oi * 2u + ch) * a.csize * 4u + ((wpos + p4) & cmask) * 4u, v);
+            if (oi < n && (int)f2 < C) {
+                if (pitch) st4(rP, oi * pstride + ((wpos + f2) & pmask) * 8u, v);
+                else st4(rC, oi * cstride + ((wpos + f2) & cmask) * 8u, v);
             }
         }
     };
-    auto stage_run = [&](const float (&v)[kChunk], uint32_t base) {
-#pragma unroll
-        for (int k = 0; k < kChunk; k += 4) *(float4 *)(stage + base + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
-    };
+    constexpr uint32_t kPsvBase = 32u * kStride;
 
     // ---- prologue: chunk 0's inputs go to the pitch ring before its windows are loaded ----
     float x[kChunk], xn[kChunk], psv[kChunk];
@@ -288,8 +278,8 @@ __global__ __launch_bounds__(kThreads, CH <= 16 ? 2 : 1) void chorus_block_v9(Ch
             if (full && cur.sC > -kWin - kChunk) {
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) {
-                    const int j = k - kChunk - cur.sC;
-                    if (j >= 0 && j < kWin) wC[j * kRow] = psv[k];
+                    const int jw = k - kChunk - cur.sC;
+                    if (jw >= 0 && jw < kWin) wC[jw * kRow] = psv[k];
                 }
             }
         }
@@ -301,14 +291,13 @@ __global__ __launch_bounds__(kThreads, CH <= 16 ? 2 : 1) void chorus_block_v9(Ch
             for (int k = 0; k < kChunk; ++k)
                 xn[k] = k < Cn ? ld1(rIn, io_v, (f0 + kChunk + (uint32_t)k) * frame_b) : 0.f;
             pl = plan_chunk<kWin>(lfo_acc + (uint32_t)C * lfo_inc, lfo_inc, lfo_off, ps_acc + (uint32_t)C * ps_inc,
-                            ps_inc, Cn, D, W, pmax, cmax, full);
+                                  ps_inc, Cn, D, W, pmax, cmax, full);
             load_windows(pl, w0 + kChunk);
         }
 
         // ---- 4. the serial recurrence over this chunk ----
         // GENERIC = partial chunk or some lane's pitch window misses (phasor wrap): per-frame
-        // guards and per-lane fallback reads.  The common case runs branch-free, so the 16 frames
-        // form one basic block and their independent control math interleaves.
+        // guards and per-lane fallback reads.  The common case runs branch-free.
         auto frame = [&](auto generic_tag, int k) {
             constexpr bool GENERIC = decltype(generic_tag)::value;
             if (GENERIC && k >= C) { psv[k] = 0.f; return; }
@@ -325,18 +314,18 @@ __global__ __launch_bounds__(kThreads, CH <= 16 ? 2 : 1) void chorus_block_v9(Ch
             split_delay(p0 * W, 1.0f, pmax, di, fr);
             if (GENERIC && !cur.okA) {
                 const uint32_t q = w0 + k - di;
-                tA = lerp_pair(ld1(rP, own_pb + (q & pmask) * 4u, 0), ld1(rP, own_pb + ((q - 1u) & pmask) * 4u, 0), fr);
+                tA = lerp_pair(ld1(rP, own_pb + (q & pmask) * 8u, 0), ld1(rP, own_pb + ((q - 1u) & pmask) * 8u, 0), fr);
             } else {
-                const int j = k - di - cur.sA;
-                tA = lerp_pair(wP0[j * kRow], wP0[(j - 1) * kRow], fr);
+                const int jw = k - di - cur.sA;
+                tA = lerp_pair(wP0[jw * kRow], wP0[(jw - 1) * kRow], fr);
             }
             split_delay(p1 * W, 1.0f, pmax, di, fr);
             if (GENERIC && !cur.okB) {
                 const uint32_t q = w0 + k - di;
-                tB = lerp_pair(ld1(rP, own_pb + (q & pmask) * 4u, 0), ld1(rP, own_pb + ((q - 1u) & pmask) * 4u, 0), fr);
+                tB = lerp_pair(ld1(rP, own_pb + (q & pmask) * 8u, 0), ld1(rP, own_pb + ((q - 1u) & pmask) * 8u, 0), fr);
             } else {
-                const int j = k - di - cur.sB;
-                tB = lerp_pair(wP1[j * kRow], wP1[(j - 1) * kRow], fr);
+                const int jw = k - di - cur.sB;
+                tB = lerp_pair(wP1[jw * kRow], wP1[(jw - 1) * kRow], fr);
             }
             const float p = tB * gB + tA * gA;
             psv[k] = p;
@@ -346,8 +335,8 @@ __global__ __launch_bounds__(kThreads, CH <= 16 ? 2 : 1) void chorus_block_v9(Ch
                 // past the window land in the junk slot (no branch)
                 wC[min(k - cur.sC, kWin) * kRow] = p;
                 split_delay(dch, 0.0f, cmax, di, fr);
-                const int j = k - di - cur.sC;
-                const float wet = lerp_pair(wC[j * kRow], wC[(j - 1) * kRow], fr);
+                const int jw = k - di - cur.sC;
+                const float wet = lerp_pair(wC[jw * kRow], wC[(jw - 1) * kRow], fr);
                 const float lp = b0 * wet + z1;
                 z1 = (b1 * wet - a1 * lp) + z2;
                 z2 = b2 * wet - a2 * lp;
@@ -363,8 +352,8 @@ __global__ __launch_bounds__(kThreads, CH <= 16 ? 2 : 1) void chorus_block_v9(Ch
             for (int k = 0; k < kChunk; ++k) frame(std::true_type{}, k);
         }
         if (full) {   // the chunk's windows are dead: stage its pitch-shifter outputs, store cooperatively
-            stage_run(psv, kChunk);
-            coop_store(false, kChunk, w0, C);
+            stage_run(psv, kPsvBase);
+            coop_store(false, kPsvBase, w0, C);
         }
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) x[k] = xn[k];
@@ -379,27 +368,17 @@ __global__ __launch_bounds__(kThreads, CH <= 16 ? 2 : 1) void chorus_block_v9(Ch
     a.state[(ch ? CHS_Z2R : CHS_Z2L) * n + i] = __float_as_uint(z2);
 }
 
-template <int CH>
-static void launch_geo(const ChorusArgs &a, hipStream_t s) {
-    const uint32_t groups = (a.n + 63) / 64;            // 64-instance groups, 2 waves each
-    const uint32_t blocks = (groups * 2 * 64 + kThreads - 1) / kThreads;
-    const size_t lds = (size_t)(kThreads / 64) * Geo<CH>::kRegion * sizeof(float);
-    if (a.mode == 0) hipLaunchKernelGGL((chorus_block_v9<true, CH>), dim3(blocks), dim3(kThreads), lds, s, a);
-    else hipLaunchKernelGGL((chorus_block_v9<false, CH>), dim3(blocks), dim3(kThreads), lds, s, a);
-}
-
 hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
-    if (a.n_frames & 3u) return hipErrorInvalidValue;
-    // 32-bit buffer offsets: rings and each audio plane must stay below 4 GiB
-    if ((uint64_t)a.n * 2 * a.csize * 4 >= (1ull << 32) || (uint64_t)a.n_frames * a.n * 4 >= (1ull << 32))
+    if ((a.n_frames & 3u) || (a.t0 & 3u)) return hipErrorInvalidValue;
+    // 32-bit buffer offsets: the rings and the two audio planes must stay below 4 GiB
+    if ((uint64_t)a.n * 2 * a.csize * 4 >= (1ull << 32) || (uint64_t)2 * a.n_frames * a.n * 4 >= (1ull << 32))
         return hipErrorInvalidValue;
-    static const int chunk = [] {
-        const char *e = getenv("OLFX_CHORUS_CHUNK");
-        return e ? atoi(e) : 16;
-    }();
-    if (chunk == 32) launch_geo<32>(a, s);
-    else launch_geo<16>(a, s);
+    const uint32_t waves = (a.n + 31) / 32;              // 32 instances x 2 channels per wave
+    const uint32_t blocks = (waves + kThreads / 64 - 1) / (kThreads / 64);
+    const size_t lds = (size_t)(kThreads / 64) * 3 * 25 * kRow * sizeof(float);
+    if (a.mode == 0) hipLaunchKernelGGL(chorus_block_v10<true>, dim3(blocks), dim3(kThreads), lds, s, a);
+    else hipLaunchKernelGGL(chorus_block_v10<false>, dim3(blocks), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 

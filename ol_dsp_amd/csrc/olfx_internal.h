@@ -123,8 +123,8 @@ enum {
 };
 
 struct ChorusArgs {
-    float *pitch_ring;          // [n][2][psize]
-    float *chorus_ring;         // [n][2][csize]
+    float *pitch_ring;          // [n][psize][2]  (stereo-interleaved: L and R share every tap)
+    float *chorus_ring;         // [n][csize][2]
     uint32_t *state;            // [CHS_N][n] (floats stored bitwise)
     const uint32_t *coef;       // [CHC_N][n]
     const float *in;            // [2][n_frames][n]
