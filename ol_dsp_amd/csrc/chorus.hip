@@ -64,6 +64,11 @@ __device__ __forceinline__ void st4(Rsrc r, uint32_t voff, float4 v) {
     __builtin_amdgcn_raw_buffer_store_b128(u, r, voff, 0, 0);
 }
 
+// exchange a value with the neighbouring lane (lanes 2j <-> 2j+1): DPP quad_perm [1,0,3,2]
+__device__ __forceinline__ float swap_pair(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+
 __device__ __forceinline__ float unit24(uint32_t acc) {
     return (float)(acc >> 8) * 5.9604644775390625e-8f;   // exact: 24-bit fraction in [0,1)
 }
@@ -298,15 +303,30 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v10(ChorusArgs a) {
         // ---- 4. the serial recurrence over this chunk ----
         // GENERIC = partial chunk or some lane's pitch window misses (phasor wrap): per-frame
         // guards and per-lane fallback reads.  The common case runs branch-free.
+        // The LFO and the two window gains are the same for both channels of an instance (shared
+        // phasors), and the two lanes of a pair are adjacent: for each frame pair, each lane
+        // evaluates the three cosines of ONE frame (its channel's index) and swaps them with its
+        // partner by DPP -- half the transcendental work, identical bits.
+        float pl_lfo[2], pl_gA[2], pl_gB[2];
         auto frame = [&](auto generic_tag, int k) {
             constexpr bool GENERIC = decltype(generic_tag)::value;
+            if ((k & 1) == 0) {
+                const uint32_t la = lfo_acc + ch * lfo_inc, pa = ps_acc + ch * ps_inc;
+                const float m_lfo = cos2pi(unit24(la + lfo_off));
+                const float m_gA = cos2pi((unit24(pa) - 0.5f) * 0.5f);
+                const float m_gB = cos2pi((unit24(pa + 0x80000000u) - 0.5f) * 0.5f);
+                const float o_lfo = swap_pair(m_lfo), o_gA = swap_pair(m_gA), o_gB = swap_pair(m_gB);
+                pl_lfo[0] = ch ? o_lfo : m_lfo; pl_lfo[1] = ch ? m_lfo : o_lfo;
+                pl_gA[0] = ch ? o_gA : m_gA;    pl_gA[1] = ch ? m_gA : o_gA;
+                pl_gB[0] = ch ? o_gB : m_gB;    pl_gB[1] = ch ? m_gB : o_gB;
+            }
             if (GENERIC && k >= C) { psv[k] = 0.f; return; }
-            const float lfo = cos2pi(unit24(lfo_acc + lfo_off));
+            const float lfo = pl_lfo[k & 1];
             const float dch = lfo * D + D;
             const float p0 = unit24(ps_acc);
             const float p1 = unit24(ps_acc + 0x80000000u);
-            const float gA = cos2pi((p0 - 0.5f) * 0.5f);
-            const float gB = cos2pi((p1 - 0.5f) * 0.5f);
+            const float gA = pl_gA[k & 1];
+            const float gB = pl_gB[k & 1];
             lfo_acc += lfo_inc;
             ps_acc += ps_inc;
             int di; float fr;
