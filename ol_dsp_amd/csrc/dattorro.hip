@@ -190,19 +190,28 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v3(DattorroArgs a) {
     ap1b.prime(a, a.t0, i);
     pre.prime(a, a.t0, dpre, i);
 
+    // raw input frames are prefetched one chunk ahead like the taps
+    float in_l[4], in_r[4], nx_l[4], nx_r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        in_l[k] = a.in[(size_t)k * n + i];
+        in_r[k] = stereo ? a.in[plane + (size_t)k * n + i] : 0.f;
+    }
+
     for (uint32_t f0 = 0; f0 < a.n_frames; f0 += 4) {
         const uint32_t t0 = a.t0 + f0;                 // multiple of 4
 
-        // ---- this chunk's inputs ----
+        // ---- this chunk's inputs: (l + r) / 2, ReverbFx.cpp:13-16 ----
         float xin[4], xpd[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            float l = a.in[(size_t)(f0 + k) * n + i];
-            if (stereo) l = (l + a.in[plane + (size_t)(f0 + k) * n + i]) / 2;
-            xin[k] = l;
-        }
-        // ---- prefetch every tap's next group (consumed by the next chunk) ----
+        for (int k = 0; k < 4; ++k) xin[k] = stereo ? (in_l[k] + in_r[k]) / 2 : in_l[k];
+        // ---- prefetch the next chunk's inputs and every tap's next group ----
         if (f0 + 4 < a.n_frames) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                nx_l[k] = a.in[(size_t)(f0 + 4 + k) * n + i];
+                nx_r[k] = stereo ? a.in[plane + (size_t)(f0 + 4 + k) * n + i] : 0.f;
+            }
             DT_ALL_TAPS(DT_PREFETCH)
             ap1a.prefetch(a, i);
             ap1b.prefetch(a, i);
@@ -283,6 +292,8 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v3(DattorroArgs a) {
             ap1b.advance(a, t0 + 4u, i);
         }
         pre.advance();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { in_l[k] = nx_l[k]; in_r[k] = nx_r[k]; }
     }
 #undef DT_ALL_TAPS
 #undef DT_PRIME
