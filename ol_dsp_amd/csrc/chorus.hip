@@ -172,9 +172,9 @@ __global__ __launch_bounds__(kThreads, 2) void chorus_block_v10(ChorusArgs a) {
     // buffer descriptors (wave-uniform); byte offsets < 2^32 (launch_chorus checks)
     const Rsrc rP = rsrc(a.pitch_ring, (uint64_t)n * 2 * a.psize * 4);
     const Rsrc rC = rsrc(a.chorus_ring, (uint64_t)n * 2 * a.csize * 4);
-    const Rsrc rIn = rsrc(a.in, (uint64_t)2 * nf * n * 4);
-    const Rsrc rOut = rsrc(a.out, (uint64_t)2 * nf * n * 4);
-    const uint32_t io_v = ch * nf * n * 4u + i * 4u, frame_b = n * 4u;
+    const Rsrc rIn = rsrc(a.in, (a.plane + (uint64_t)nf * n) * 4);
+    const Rsrc rOut = rsrc(a.out, (a.plane + (uint64_t)nf * n) * 4);
+    const uint32_t io_v = ch * (uint32_t)a.plane * 4u + i * 4u, frame_b = n * 4u;
     const uint32_t out_v = valid ? io_v : 0xFFFFFFF0u;  // invalid lanes: buffer range check drops
     const uint32_t pstride = a.psize * 8u, cstride = a.csize * 8u;   // bytes per instance ring
     const uint32_t own_pb = i * pstride + ch * 4u;       // this lane's samples in its pitch ring
@@ -392,7 +392,8 @@ hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
     if ((a.n_frames & 3u) || (a.t0 & 3u)) return hipErrorInvalidValue;
     // 32-bit buffer offsets: the rings and the two audio planes must stay below 4 GiB
-    if ((uint64_t)a.n * 2 * a.csize * 4 >= (1ull << 32) || (uint64_t)2 * a.n_frames * a.n * 4 >= (1ull << 32))
+    if ((uint64_t)a.n * 2 * a.csize * 4 >= (1ull << 32) || (a.plane + (uint64_t)a.n_frames * a.n) * 4 >= (1ull << 32) ||
+        a.plane < (uint64_t)a.n_frames * a.n)
         return hipErrorInvalidValue;
     const uint32_t waves = (a.n + 31) / 32;              // 32 instances x 2 channels per wave
     const uint32_t blocks = (waves + kThreads / 64 - 1) / (kThreads / 64);

@@ -120,7 +120,7 @@ struct PreTap {
         for (int k = 0; k < 4; ++k)
             xpd[k] = s == 0 ? w[k] : (s == 1 ? w[k + 1] : (s == 2 ? w[k + 2] : w[k + 3]));
         if (d <= 8u) {
-            const size_t plane = (size_t)a.n_frames * a.n;
+            const size_t plane = a.plane;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 float v;
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v3(DattorroArgs a) {
     float lp_a = a.state[DTS_LP_DAMP_A * n + i];
     float lp_b = a.state[DTS_LP_DAMP_B * n + i];
 
-    const size_t plane = (size_t)a.n_frames * n;
+    const size_t plane = a.plane;
     const bool stereo = a.in_ch == 2;
 
     // main-time taps (read at t)

@@ -513,6 +513,7 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hip
         a.coef = e->dt_coef;
         a.in = in;
         a.out = out;
+        a.plane = (uint64_t)n_frames * e->n;
         a.n = e->n;
         a.n_frames = n_frames;
         a.t0 = t0 & 0xFFFFu;
@@ -528,6 +529,7 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hip
         a.coef = cf;
         a.in = in;
         a.out = out;
+        a.plane = (uint64_t)n_frames * e->n;
         a.n = e->n;
         a.n_frames = n_frames;
         a.t0 = t0;

@@ -71,8 +71,9 @@ struct DattorroArgs {
     float *ring[DT_NLINES];     // ring l: [kDtSize[l]][n]   (position-major, instance fastest)
     float *state;               // [DTS_N][n]
     const float *coef;          // [DTC_N][n]
-    const float *in;            // [2][n_frames][n]
-    float *out;                 // [2][n_frames][n]
+    const float *in;            // [2][..][n], channel planes `plane` floats apart
+    float *out;                 // [2][..][n]
+    uint64_t plane;             // floats between the channel planes of in / out (>= n_frames * n)
     uint32_t n;                 // instances
     uint32_t n_frames;
     uint32_t t0;                // stream time (frames since create) of the first frame, mod 2^16
@@ -127,8 +128,9 @@ struct ChorusArgs {
     float *chorus_ring;         // [n][csize][2]
     uint32_t *state;            // [CHS_N][n] (floats stored bitwise)
     const uint32_t *coef;       // [CHC_N][n]
-    const float *in;            // [2][n_frames][n]
-    float *out;                 // [2][n_frames][n]
+    const float *in;            // [2][..][n], channel planes `plane` floats apart
+    float *out;                 // [2][..][n]
+    uint64_t plane;             // floats between the channel planes of in / out (>= n_frames * n)
     uint32_t n, n_frames;
     uint32_t t0;                // write position of the first frame (mod ring sizes)
     uint32_t psize, csize;      // ring sizes (powers of two)
