@@ -17,38 +17,49 @@ namespace {
 
 enum { SEG_IDLE = 0, SEG_ATTACK = 1, SEG_DECAY = 2, SEG_RELEASE = 3 };
 
-// daisysp::Adsr::Process(gate)
+// daisysp::Adsr::Process(gate), branch-free: every lane evaluates the segment step and selects
+// (same operations and order as the branchy form, so the same bits).
 __device__ __forceinline__ float adsr(bool gate, uint32_t &mode, bool &gprev, float &x, float atk_d0,
                                       float atk_tgt, float dec_d0, float rel_d0, float sus) {
-    if (gate && !gprev) mode = SEG_ATTACK;
-    else if (!gate && gprev) mode = SEG_RELEASE;
+    mode = (gate && !gprev) ? (uint32_t)SEG_ATTACK : ((!gate && gprev) ? (uint32_t)SEG_RELEASE : mode);
     gprev = gate;
-    float d0 = atk_d0;
-    if (mode == SEG_DECAY) d0 = dec_d0;
-    else if (mode == SEG_RELEASE) d0 = rel_d0;
-    const float target = mode == SEG_DECAY ? sus : -0.01f;
-    float out = 0.0f;
-    if (mode == SEG_ATTACK) {
-        x += d0 * (atk_tgt - x);
-        out = x;
-        if (out > 1.f) { x = out = 1.f; mode = SEG_DECAY; }
-    } else if (mode == SEG_DECAY || mode == SEG_RELEASE) {
-        x += d0 * (target - x);
-        out = x;
-        if (out < 0.0f) { x = out = 0.f; mode = SEG_IDLE; }
-    }
+    const bool atk = mode == SEG_ATTACK, dec = mode == SEG_DECAY, idle = mode == SEG_IDLE;
+    const float d0 = atk ? atk_d0 : (dec ? dec_d0 : rel_d0);
+    const float target = atk ? atk_tgt : (dec ? sus : -0.01f);
+    const float xn = x + d0 * (target - x);
+    const bool top = atk && xn > 1.f, bottom = !atk && xn < 0.0f;
+    const float out = idle ? 0.0f : (top ? 1.0f : (bottom ? 0.0f : xn));
+    x = idle ? x : out;
+    mode = top ? (uint32_t)SEG_DECAY : (bottom && !idle ? (uint32_t)SEG_IDLE : mode);
     return out;
 }
 
+// polyBLEP residual with one division: t/dt near the wrap start, (t-1)/dt near its end -- the
+// same quotients as the two-branch form
 __device__ __forceinline__ float polyblep(float dt, float t) {
-    if (t < dt) { t /= dt; return t + t - t * t - 1.0f; }
-    else if (t > 1.0f - dt) { t = (t - 1.0f) / dt; return t * t + t + t + 1.0f; }
-    return 0.0f;
+    const bool lo = t < dt, hi = !lo && t > 1.0f - dt;
+    const float q = (lo ? t : t - 1.0f) * __builtin_amdgcn_rcpf(dt);   // v_rcp: ~1 ulp
+    const float rlo = q + q - q * q - 1.0f;
+    const float rhi = q * q + q + q + 1.0f;
+    return lo ? rlo : (hi ? rhi : 0.0f);
+}
+
+// sin(x) for x in [0, pi/4] (Svf::SetFreq's argument pi * min(0.25, fc / 2sr)): odd Taylor
+// polynomial to x^9, truncation < 2e-9, i.e. within an ulp of sinf; branch-free.  The voice's
+// parity tolerance (1e-5 of max(|ref|, rms), tests/test_gpu_parity.py) covers ulp-level
+// differences from the host's sinf.
+__device__ __forceinline__ float sin_quarter(float x) {
+    const float x2 = x * x;
+    float p = 2.7557319e-6f;                 // 1/9!
+    p = p * x2 + -1.9841270e-4f;             // -1/7!
+    p = p * x2 + 8.3333333e-3f;              // 1/5!
+    p = p * x2 + -1.6666667e-1f;             // -1/3!
+    return x + (x * x2) * p;
 }
 
 }  // namespace
 
-__global__ __launch_bounds__(256) void voice_block_v1(VoiceArgs a) {
+__global__ __launch_bounds__(64) void voice_block_v2(VoiceArgs a) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
     const uint32_t n = a.n;
@@ -61,6 +72,7 @@ __global__ __launch_bounds__(256) void voice_block_v1(VoiceArgs a) {
     const float damp_res = c[VCC_DAMP_RES * n + i], drive = c[VCC_DRIVE * n + i];
     const float port_c = c[VCC_PORT_COEF * n + i], fc_max = c[VCC_FC_MAX * n + i];
     const float sr = c[VCC_SR * n + i], inv_sr = c[VCC_INV_SR * n + i];
+    const float inv_2sr = 1.0f / (sr * 2.0f);
 
     float *s = a.state;
     float phase = s[VCS_PHASE * n + i];
@@ -75,6 +87,7 @@ __global__ __launch_bounds__(256) void voice_block_v1(VoiceArgs a) {
     bool gprev_a = (flags >> 6) & 1u, gprev_f = (flags >> 7) & 1u;
     const bool gate = (flags >> 8) & 1u;
 
+#pragma unroll 2
     for (uint32_t f = 0; f < a.n_frames; ++f) {
         float amp = adsr(gate, mode_a, gprev_a, xa, atk_d0a, atk_tga, dec_d0a, rel_d0a, sus_a);
         amp *= amp_amt;
@@ -92,9 +105,13 @@ __global__ __launch_bounds__(256) void voice_block_v1(VoiceArgs a) {
         const float fe = adsr(gate, mode_f, gprev_f, xf, atk_d0f, atk_tgf, dec_d0f, rel_d0f, sus_f);
         const float fc_in = cutoff + ((fe * 20000.0f) * fenv_amt);
         const float fc = fminf(fmaxf(fc_in, 1.0e-6f), fc_max);
-        const float arg = 0.25f < fc / (sr * 2.0f) ? 0.25f : fc / (sr * 2.0f);
-        const float fq = 2.0f * sinf(3.1415927410125732f * arg);
-        const float dlim = 2.0f < 2.0f / fq - fq * 0.5f ? 2.0f : 2.0f / fq - fq * 0.5f;
+        // the three per-sample divisions of Svf::SetFreq / polyBLEP use the hardware reciprocal
+        // (~1 ulp; within the voice tolerance, like sin_quarter)
+        const float fcn = fc * inv_2sr;
+        const float arg = 0.25f < fcn ? 0.25f : fcn;
+        const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
+        const float lim = 2.0f * __builtin_amdgcn_rcpf(fq) - fq * 0.5f;
+        const float dlim = 2.0f < lim ? 2.0f : lim;
         const float damp = damp_res < dlim ? damp_res : dlim;
         // Svf::Process: two passes, Low() = average of the two low outputs
         float notch = src - damp * band;
@@ -122,8 +139,8 @@ __global__ __launch_bounds__(256) void voice_block_v1(VoiceArgs a) {
 
 hipError_t launch_voice(const VoiceArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
-    const uint32_t threads = 256;
-    hipLaunchKernelGGL(voice_block_v1, dim3((a.n + threads - 1) / threads), dim3(threads), 0, s, a);
+    const uint32_t threads = 64;       // one wave per workgroup: 32,768 voices spread over every CU
+    hipLaunchKernelGGL(voice_block_v2, dim3((a.n + threads - 1) / threads), dim3(threads), 0, s, a);
     return hipGetLastError();
 }
 
