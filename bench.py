@@ -27,6 +27,12 @@ sys.path.insert(0, ROOT)
 
 METRIC = "stereo samples/s across N effect instances @48kHz; % HBM roofline; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+FP32_VALU_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md)
+# The voice is VALU-bound (~5 B of HBM per sample): its roofline is FP32 operations, counted
+# from the reference arithmetic per sample: 2 ADSR steps 6, amp 1, Port 3,
+# SetFreq 1, polyBLEP saw 11, 0.5 gain 1, filter-env cutoff 3, Svf::SetFreq 8 + sin, two Svf
+# passes 22, Low() average 3, output 1, sin and the three divisions 4 -> 64.
+VOICE_FLOPS_PER_SAMPLE = 64.0
 WORKLOADS = {
     # name: (kind, default instances per GPU, BASELINE config it restates)
     "chorus": ("chorus", 65536, "configs[1]: 65,536 ChorusEffect instances, 48 kHz, 256-sample blocks, 1xMI355X"),
@@ -172,7 +178,12 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
     # the single collective of the run (RCCL over xGMI when world > 1): outside the timed region
-    checksum = float(out.abs().sum().item())
+    # sum |y| over the finite outputs (a voice whose Svf diverges -- possible in the reference
+    # DaisySP arithmetic at high cutoff, low resonance and high drive -- yields inf/NaN there too;
+    # DESIGN.md section 5); the count of non-finite samples is reported beside it
+    finite = torch.isfinite(out)
+    nonfinite = int((~finite).sum().item())
+    checksum = float(torch.where(finite, out.abs(), torch.zeros_like(out)).sum().item())
     stats = reduce_stats(RunStats(elapsed, kern_ms, float(n) * B * args.steps, checksum), device=dev)
     elapsed, kern_ms, frames = stats.elapsed_s, stats.kernel_ms, stats.frames
 
@@ -191,6 +202,18 @@ def main():
                     traffic = tr.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        if kind == "voice":
+            tflops = VOICE_FLOPS_PER_SAMPLE * n * B / (kern_ms * 1e-3) / 1e12
+            roofline = {"bound": "valu", "achieved": tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,
+                        "kernel": eng.kernel_name, "kernel_ms": kern_ms,
+                        "algorithmic_flops_per_frame": VOICE_FLOPS_PER_SAMPLE,
+                        "algorithmic_bytes_per_frame": bpf, "hbm_gbs": achieved, "frames_per_launch": n * B}
+        else:
+            roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                        "kernel": eng.kernel_name, "kernel_ms": kern_ms,
+                        "algorithmic_bytes_per_frame": bpf, "frames_per_launch": n * B}
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
@@ -211,12 +234,10 @@ def main():
             "config": {"workload": args.workload, "restates": desc, "instances_per_gpu": n,
                        "instances_total": n * world, "block": B, "sample_rate": args.sample_rate,
                        "input_pool_blocks": pool_n, "parallelism": f"instance-shard x{world} (no data-path collective)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": eng.kernel_name, "kernel_ms": kern_ms,
-                         "algorithmic_bytes_per_frame": bpf, "frames_per_launch": n * B},
+            "roofline": roofline,
             "cpu_baseline": cpu,
             "output_checksum": stats.checksum,
+            "output_nonfinite_rank0": nonfinite,
         }
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -34,5 +34,9 @@ if [ "$mode" = prof ]; then
         python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0
     step prof_dattorro 600 rocprofv3 --kernel-trace --stats -d "$out/prof_dattorro" -o run --output-format csv -- \
         python3 bench.py --workload dattorro --steps 20 --warmup 3 --cpu-seconds 0
+    step prof_voice 600 rocprofv3 --kernel-trace --stats -d "$out/prof_voice" -o run --output-format csv -- \
+        python3 bench.py --workload voice --steps 50 --warmup 3 --cpu-seconds 0
+    step prof_chain 600 rocprofv3 --kernel-trace --stats -d "$out/prof_chain" -o run --output-format csv -- \
+        python3 bench.py --workload chain --steps 20 --warmup 3 --cpu-seconds 0
 fi
 echo "== done $(date +%T)"
