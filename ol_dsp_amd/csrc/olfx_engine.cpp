@@ -840,11 +840,11 @@ double olfx_algorithmic_bytes_per_frame(const olfx_engine *e) {
 const char *olfx_kernel_name(const olfx_engine *e) {
     if (!e) return "";
     switch (e->kind) {
-    case OLFX_KIND_DATTORRO: return "dattorro_block_v3";
+    case OLFX_KIND_DATTORRO: return "dattorro_block_v4";
     case OLFX_KIND_CHORUS:
     case OLFX_KIND_PITCHSHIFT: return "chorus_block_v10";
     case OLFX_KIND_VOICE: return "voice_block_v2";
-    case OLFX_KIND_CHAIN: return "dattorro_block_v3";
+    case OLFX_KIND_CHAIN: return "dattorro_block_v4";
     default: return "";
     }
 }
