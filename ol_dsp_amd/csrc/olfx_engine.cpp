@@ -285,6 +285,7 @@ struct olfx_engine {
     size_t d_bytes = 0;
 
     // dattorro (also the chain's reverb stage)
+    uint32_t n_dt = 0;           // reverb-stage instances: n, or n rounded up to 64 for the chain
     float *dt_rings = nullptr;
     float *dt_state = nullptr;
     float *dt_coef = nullptr;
@@ -295,8 +296,6 @@ struct olfx_engine {
     uint32_t *ch_state = nullptr, *ch_coef = nullptr;
     float *ps_pring = nullptr, *ps_cring = nullptr;      // chain stage 2
     uint32_t *ps_state = nullptr, *ps_coef = nullptr;
-    float *chain_tmp = nullptr;                          // chain intermediates [2][2][block][n]
-    uint32_t chain_tmp_frames = 0;
 
     // voice
     float *vc_state = nullptr, *vc_coef = nullptr;
@@ -373,12 +372,13 @@ int upload_params(olfx_engine *e, hipStream_t s) {
     };
     if (e->kind == OLFX_KIND_DATTORRO || e->kind == OLFX_KIND_CHAIN) {
         const uint32_t base = e->kind == OLFX_KIND_CHAIN ? OLFX_CN_VERB0 : 0;
-        std::vector<float> c((size_t)DTC_N * n);
+        const uint32_t nd = e->n_dt;                   // padding instances get zero coefficients
+        std::vector<float> c((size_t)DTC_N * nd, 0.f);
         float cc[DTC_N];
         for (uint32_t i = 0; i < n; ++i) {
             gather(i);
             derive_dattorro(p.data() + base, cc);
-            for (int k = 0; k < DTC_N; ++k) c[(size_t)k * n + i] = cc[k];
+            for (int k = 0; k < DTC_N; ++k) c[(size_t)k * nd + i] = cc[k];
         }
         HIPCHK(e, hipMemcpyAsync(e->dt_coef, c.data(), c.size() * 4, hipMemcpyHostToDevice, s));
         HIPCHK(e, hipStreamSynchronize(s));
@@ -490,14 +490,6 @@ int ensure_staging(olfx_engine *e, size_t fin, size_t fout) {
     return OLFX_OK;
 }
 
-int ensure_chain_tmp(olfx_engine *e, uint32_t n_frames) {
-    if (n_frames <= e->chain_tmp_frames) return OLFX_OK;
-    if (e->chain_tmp) (void)hipFree(e->chain_tmp);
-    e->chain_tmp = nullptr;
-    HIPCHK(e, hipMalloc((void **)&e->chain_tmp, (size_t)4 * n_frames * e->n * 4));
-    e->chain_tmp_frames = n_frames;
-    return OLFX_OK;
-}
 
 int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hipStream_t s) {
     hipError_t r = hipSuccess;
@@ -507,14 +499,14 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hip
         size_t off = 0;
         for (int l = 0; l < DT_NLINES; ++l) {
             a.ring[l] = e->dt_rings + off;
-            off += (size_t)kDtSize[l] * e->n;
+            off += (size_t)kDtSize[l] * e->n_dt;
         }
         a.state = e->dt_state;
         a.coef = e->dt_coef;
         a.in = in;
         a.out = out;
         a.plane = (uint64_t)n_frames * e->n;
-        a.n = e->n;
+        a.n = e->n_dt;
         a.n_frames = n_frames;
         a.t0 = t0 & 0xFFFFu;
         a.in_ch = 2;
@@ -557,14 +549,17 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hip
         break;
     }
     case OLFX_KIND_CHAIN: {
-        int rc = ensure_chain_tmp(e, n_frames);
-        if (rc) return rc;
-        float *t1 = e->chain_tmp;
-        float *t2 = e->chain_tmp + (size_t)2 * n_frames * e->n;
-        r = launch_chorus(ch_args(e->ch_pring, e->ch_cring, e->ch_state, e->ch_coef, din, t1, 0), s);
-        if (r == hipSuccess)
-            r = launch_chorus(ch_args(e->ps_pring, e->ps_cring, e->ps_state, e->ps_coef, t1, t2, 1), s);
-        if (r == hipSuccess) r = launch_dattorro(dt_args(t2, dout), s);
+        // one fused launch: chorus and pitch-shift waves feed the reverb wave through LDS
+        ChainArgs a{};
+        a.c1 = ch_args(e->ch_pring, e->ch_cring, e->ch_state, e->ch_coef, nullptr, nullptr, 0);
+        a.c2 = ch_args(e->ps_pring, e->ps_cring, e->ps_state, e->ps_coef, nullptr, nullptr, 1);
+        a.d = dt_args(nullptr, nullptr);
+        a.in = din;
+        a.out = dout;
+        a.plane = (uint64_t)n_frames * e->n;
+        a.n = e->n;
+        a.n_frames = n_frames;
+        r = launch_chain(a, s);
         break;
     }
     default: return e->fail(OLFX_E_KIND, "unknown kind");
@@ -627,6 +622,7 @@ int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32
     e->sr = sample_rate;
     e->n_params = n_params_of(kind);
     chorus_sizes(sample_rate, &e->psize, &e->csize);
+    e->n_dt = kind == OLFX_KIND_CHAIN ? (n_inst + 63u) & ~63u : n_inst;
 
     hipError_t r = hipSetDevice(device);
     if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
@@ -646,9 +642,9 @@ int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32
     const bool has_ps = kind == OLFX_KIND_CHAIN;
     const bool has_vc = kind == OLFX_KIND_VOICE;
     if (has_dt) {
-        o_dt_r = cv.take((size_t)dt_total_floats() * n * 4);
-        o_dt_s = cv.take((size_t)DTS_N * n * 4);
-        o_dt_c = cv.take((size_t)DTC_N * n * 4);
+        o_dt_r = cv.take((size_t)dt_total_floats() * e->n_dt * 4);
+        o_dt_s = cv.take((size_t)DTS_N * e->n_dt * 4);
+        o_dt_c = cv.take((size_t)DTC_N * e->n_dt * 4);
     }
     if (has_ch) {
         o_ch_p = cv.take((size_t)2 * e->psize * n * 4);
@@ -710,7 +706,6 @@ int olfx_destroy(olfx_engine *e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->d_mem) (void)hipFree(e->d_mem);
-    if (e->chain_tmp) (void)hipFree(e->chain_tmp);
     if (e->h_in) (void)hipHostFree(e->h_in);
     if (e->h_out) (void)hipHostFree(e->h_out);
     if (e->d_in) (void)hipFree(e->d_in);
@@ -844,7 +839,7 @@ const char *olfx_kernel_name(const olfx_engine *e) {
     case OLFX_KIND_CHORUS:
     case OLFX_KIND_PITCHSHIFT: return "chorus_block_v10";
     case OLFX_KIND_VOICE: return "voice_block_v2";
-    case OLFX_KIND_CHAIN: return "dattorro_block_v4";
+    case OLFX_KIND_CHAIN: return "chain_block_v1";
     default: return "";
     }
 }

@@ -166,7 +166,20 @@ struct VoiceArgs {
 };
 
 // Launchers (defined in the .hip files).
+// The fused chain (chain.hip): chorus -> pitch-shift -> dattorro in one launch.  c1 / c2 / d
+// carry each stage's rings, state and coefficients (their in / out fields are unused); the
+// reverb stage's instance count d.n is n rounded up to 64 (padding instances compute harmlessly).
+struct ChainArgs {
+    ChorusArgs c1, c2;
+    DattorroArgs d;
+    const float *in;            // [2][..][n]
+    float *out;                 // [2][..][n]
+    uint64_t plane;             // floats between channel planes of in / out
+    uint32_t n, n_frames;       // real instances; frames (multiple of 4)
+};
+
 hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s);
+hipError_t launch_chain(const ChainArgs &a, hipStream_t s);
 hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s);
 hipError_t launch_voice(const VoiceArgs &a, hipStream_t s);
 
