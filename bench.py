@@ -40,6 +40,7 @@ WORKLOADS = {
     "voice": ("voice", 32768, "configs[3]: 262,144 synthlib voices = 32,768 per GPU x 8"),
     "chain": ("chain", 16384, "configs[4]: 131,072 chorus->pitch-shift->dattorro chains = 16,384 per GPU x 8"),
     "pitchshift": ("pitchshift", 65536, "pitch-shift stage alone"),
+    "fxrack": ("fxrack", 65536, "SURVEY 8f row 1: fxlib FxRack<2> (delay -> reverb -> filter -> master), 65,536 instances"),
 }
 
 
@@ -69,8 +70,10 @@ def draw_params(kind: str, n: int, seed: int) -> np.ndarray:
             np.full(n, .70, np.float32), u(.25, .95), u(.05, .95)]
     voice = [u(100, 8000), u(0, .9), u(0, 1), u(0, 1), u(.001, .5), u(0, 1), u(.001, .5), u(0, 1), u(.001, .5),
              u(.2, 1), u(.001, .5), u(0, 1), u(.001, .5), u(0, 1), u(.001, .5), u(0, .05)]
+    rack = [u(0.05, 1), u(0, .9), u(0, 1), u(100, 12000), u(0, .8), u(0, 1), u(100, 12000), u(0, .8),
+            u(0, 1), rng.integers(0, 5, n).astype(np.float32), u(0, 1)]
     table = {"chorus": chorus, "pitchshift": pitch, "dattorro": verb, "voice": voice,
-             "chain": chorus + pitch + verb}
+             "chain": chorus + pitch + verb, "fxrack": rack}
     return np.stack(table[kind])
 
 
@@ -97,6 +100,12 @@ def cpu_baseline(kind: str, block: int, sr: float, budget_s: float, threads: int
         for i in range(n):
             for f in range(p.shape[0]):
                 bank.set(i, f if kind == "chorus" else (0, 7)[f], float(p[f, i]))
+        step = lambda: bank.process(x, threads)  # noqa: E731
+    elif kind == "fxrack":
+        bank = O.FxRack(n, sr)
+        for i in range(n):
+            for f in range(p.shape[0]):
+                bank.set(i, f, float(p[f, i]))
         step = lambda: bank.process(x, threads)  # noqa: E731
     elif kind == "voice":
         bank = O.Voice(n, sr)

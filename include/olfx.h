@@ -59,7 +59,8 @@ enum {
     OLFX_KIND_CHORUS     = 2,  /* RNBO stereo-chorus (mono-chorus x2, shared params) */
     OLFX_KIND_PITCHSHIFT = 3,  /* gen~ pitchshift, stereo */
     OLFX_KIND_VOICE      = 4,  /* synthlib SynthVoice: polyBLEP saw -> SVF LP (env cutoff) -> amp env; mono out */
-    OLFX_KIND_CHAIN      = 5   /* fused chorus -> pitch-shift -> dattorro, stereo */
+    OLFX_KIND_CHAIN      = 5,  /* fused chorus -> pitch-shift -> dattorro, stereo */
+    OLFX_KIND_FXRACK     = 6   /* fxlib ol::fx::FxRack<2>: delay -> reverb -> filter -> master (Fx.h:398-492) */
 };
 
 /* ---- parameters (field index, value is what the reference setter takes) ---- */
@@ -99,6 +100,21 @@ enum {
     OLFX_VC_FILTER_RELEASE, OLFX_VC_AMP_ENV_AMOUNT, OLFX_VC_AMP_ATTACK, OLFX_VC_AMP_ATTACK_SHAPE,
     OLFX_VC_AMP_DECAY, OLFX_VC_AMP_SUSTAIN, OLFX_VC_AMP_RELEASE, OLFX_VC_PORTAMENTO,
     OLFX_VC_NPARAMS
+};
+/* Effect rack: ol::fx::FxRack<2> members (modules/fxlib/Fx.h; defaults in brackets) */
+enum {
+    OLFX_FR_DELAY_TIME = 0,      /* DelayFx time [0,1] -> 0..48000 samples            [0.5]   Fx.h:172,214 */
+    OLFX_FR_DELAY_FEEDBACK,      /* DelayFx feedback                                   [0.5]   Fx.h:173 */
+    OLFX_FR_DELAY_BALANCE,       /* DelayFx wet/dry                                    [0.33]  Fx.h:174 */
+    OLFX_FR_DELAY_CUTOFF,        /* DelayFx filter_ cutoff, Hz              [scale(64,0,127,0,20000)] :188 */
+    OLFX_FR_DELAY_RESONANCE,     /* DelayFx filter_ resonance [0,1]            [scale(24,0,127,0,1)] :189 */
+    OLFX_FR_REVERB_BALANCE,      /* ReverbFx balance (over the ReverbSc stub)   [0.1]   Fx.h:282 */
+    OLFX_FR_FILTER_CUTOFF,       /* FxRack filter1 cutoff, Hz                  [20000]  Fx.h:75 */
+    OLFX_FR_FILTER_RESONANCE,    /* [0] */
+    OLFX_FR_FILTER_DRIVE,        /* [0] */
+    OLFX_FR_FILTER_TYPE,         /* 0 low, 1 band, 2 high, 3 notch, 4 peak      [0]     Fx.h:67-73 */
+    OLFX_FR_MASTER_VOLUME,       /* [0.8] Fx.h:405 */
+    OLFX_FR_NPARAMS
 };
 /* Chain: chorus params, then pitch-shift params, then dattorro params */
 #define OLFX_CN_CHORUS0   0

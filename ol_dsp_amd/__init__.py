@@ -4,12 +4,12 @@ The product is ``libolfx.so`` (ol_dsp_amd/csrc -> ol_dsp_amd/libolfx.so, C-ABI i
 include/olfx.h).  This package is the thin Python mirror of that boundary used by tests and
 bench.py; it never computes audio on the CPU.
 """
-from ._lib import (IO_DEVICE, IO_HOST, KIND_CHAIN, KIND_CHORUS, KIND_DATTORRO, KIND_PITCHSHIFT,
+from ._lib import (IO_DEVICE, IO_HOST, KIND_CHAIN, KIND_CHORUS, KIND_DATTORRO, KIND_FXRACK, KIND_PITCHSHIFT,
                    KIND_VOICE, LIB_PATH, OlfxError, load)
 from .engine import KIND_NAMES, PARAMS, Engine, kind_info
 
 __all__ = [
     "Engine", "OlfxError", "PARAMS", "KIND_NAMES", "kind_info", "load", "LIB_PATH",
-    "KIND_DATTORRO", "KIND_CHORUS", "KIND_PITCHSHIFT", "KIND_VOICE", "KIND_CHAIN",
+    "KIND_DATTORRO", "KIND_CHORUS", "KIND_PITCHSHIFT", "KIND_VOICE", "KIND_CHAIN", "KIND_FXRACK",
     "IO_DEVICE", "IO_HOST",
 ]

@@ -28,6 +28,7 @@ KIND_CHORUS = 2
 KIND_PITCHSHIFT = 3
 KIND_VOICE = 4
 KIND_CHAIN = 5
+KIND_FXRACK = 6
 
 IO_DEVICE = 0
 IO_HOST = 1

@@ -1,0 +1,228 @@
+// ol_dsp_amd/csrc/fxrack.hip -- the fxlib effect rack ol::fx::FxRack<2> on gfx950.
+//
+// Reference (modules/fxlib/Fx.h:398-492; oracle/fxrack_ref.c restates it):
+//   DelayFx<2>   per channel: r = DelayLine.Read(); DelayLine.Write(in + feedback r);
+//                filter_ (Svf LowPass) on channel 0 in place; a = r bal + in (1 - bal)   Fx.h:193-206
+//   ReverbFx<2>  over the in-tree ReverbSc stub (Reverb.h:26-31): b = 0.8 a rbal + a (1 - rbal)
+//   FilterFx<2>  filter1 (Svf, selected output) on channel 0 only; channel 1 is never written
+//                and FxRack's buf_c starts at 0 (Fx.h:408), so output 1 is 0   Fx.h:88-108
+//   out = buf_c * master_volume
+// DelayLine<float, 48000> (DaisySP, restated): read at delay D and D + 1, linear interpolation,
+// read before write.  Here the ring is time-forward (position = t mod 48000) and stereo-
+// interleaved [n][48000][2]: both channels share the delay, so one window load serves both.
+//
+// Mapping (as chorus_stage.h): lane = (instance j of the wave, channel), a wave = 32 instances x
+// 2 channels.  The block runs in 16-frame chunks.  A chunk's reads fall in a window of 20
+// positions starting at (t0 - D - 1) rounded down to even: 10 x 16-B stereo pieces per
+// instance, loaded cooperatively one chunk ahead and de-interleaved into LDS as [slot][lane]
+// (conflict-free per-frame reads).  The chunk's writes leave as one 128-B stereo run per
+// instance (8 lanes x 16 B) from LDS staging.  Delays shorter than a chunk read positions the
+// chunk itself writes: every written sample also goes into the window (a junk slot when it falls
+// outside), and positions the next window needs before they reach the ring are patched in from
+// registers -- so every delay 0..47999 takes the same branch-free path.
+// Bound: HBM (32 B per stereo frame: ring write 8 + ring read 8 + I/O 16).
+#include <type_traits>
+
+#include "chorus_stage.h"
+
+namespace olfx {
+
+namespace {
+
+constexpr int kFrThreads = 256;
+constexpr int kFrChunk = 16;
+constexpr int kFrWin = 20;                          // positions per window (10 stereo pieces)
+constexpr int kFrSlots = kFrWin + 1;                // + junk slot
+constexpr int kFrStride = 36;                       // staging floats per instance (32 + pad)
+constexpr int kFrRegion = kFrSlots * 64 + 32 * kFrStride;   // floats of LDS per wave
+
+// Svf::Process (DaisySP, double-sampled Chamberlin) returning the selected output
+// (0 low, 1 band, 2 high, 3 notch, 4 peak), as oracle/fxrack_ref.c
+__device__ __forceinline__ float svf_tick(float in, float freq, float damp, float drive, uint32_t type,
+                                          float &low, float &band) {
+    float notch = in - damp * band;
+    low = low + freq * band;
+    float high = notch - low;
+    band = freq * high + band - drive * band * band * band;
+    float o_low = 0.5f * low, o_high = 0.5f * high, o_band = 0.5f * band;
+    float o_peak = 0.5f * (low - high), o_notch = 0.5f * notch;
+    notch = in - damp * band;
+    low = low + freq * band;
+    high = notch - low;
+    band = freq * high + band - drive * band * band * band;
+    o_low += 0.5f * low;
+    o_high += 0.5f * high;
+    o_band += 0.5f * band;
+    o_peak += 0.5f * (low - high);
+    o_notch += 0.5f * notch;
+    return type == 1 ? o_band : (type == 2 ? o_high : (type == 3 ? o_notch : (type == 4 ? o_peak : o_low)));
+}
+
+__device__ __forceinline__ uint32_t wrap48k(int64_t p) {
+    const int64_t m = p % (int64_t)kFrMaxDelay;
+    return (uint32_t)(m < 0 ? m + kFrMaxDelay : m);
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kFrThreads) void fxrack_block_v1(FxRackArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wib = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint32_t wave = blockIdx.x * (kFrThreads / 64) + wib, lane = tid & 63u;
+    const uint32_t j = lane >> 1, ch = lane & 1u;
+    const uint32_t inst0 = wave * 32u;
+    const uint32_t n = a.n, nf = a.n_frames;
+    if (inst0 >= n) return;
+    const uint32_t i_raw = inst0 + j;
+    const bool valid = i_raw < n;
+    const uint32_t i = valid ? i_raw : n - 1;
+
+    const uint32_t D = a.coef[FRC_DELAY * n + i];
+    const float frac = __uint_as_float(a.coef[FRC_FRAC * n + i]);
+    const float feedback = __uint_as_float(a.coef[FRC_FEEDBACK * n + i]);
+    const float dbal = __uint_as_float(a.coef[FRC_DBAL * n + i]);
+    const float dfreq = __uint_as_float(a.coef[FRC_DFREQ * n + i]);
+    const float ddamp = __uint_as_float(a.coef[FRC_DDAMP * n + i]);
+    const float ddrive = __uint_as_float(a.coef[FRC_DDRIVE * n + i]);
+    const float rbal = __uint_as_float(a.coef[FRC_RBAL * n + i]);
+    const float ffreq = __uint_as_float(a.coef[FRC_FFREQ * n + i]);
+    const float fdamp = __uint_as_float(a.coef[FRC_FDAMP * n + i]);
+    const float fdrive = __uint_as_float(a.coef[FRC_FDRIVE * n + i]);
+    const uint32_t ftype = a.coef[FRC_FTYPE * n + i];
+    const float master = __uint_as_float(a.coef[FRC_MASTER * n + i]);
+    float dlow = __uint_as_float(a.state[FRS_DLOW * n + i]);
+    float dband = __uint_as_float(a.state[FRS_DBAND * n + i]);
+    float flow = __uint_as_float(a.state[FRS_FLOW * n + i]);
+    float fband = __uint_as_float(a.state[FRS_FBAND * n + i]);
+
+    // the wave's 32 rings (12.3 MB) get their own descriptor, so 32-bit offsets cover any n
+    const ch::Rsrc rR = ch::rsrc(a.ring + (size_t)inst0 * kFrMaxDelay * 2, (uint64_t)min(32u, n - inst0) * kFrMaxDelay * 8);
+    const ch::Rsrc rIn = ch::rsrc(a.in, (a.plane + (uint64_t)nf * n) * 4);
+    const ch::Rsrc rOut = ch::rsrc(a.out, (a.plane + (uint64_t)nf * n) * 4);
+    const uint32_t io_v = ch * (uint32_t)a.plane * 4u + i * 4u, frame_b = n * 4u;
+    const uint32_t out_v = valid ? io_v : 0xFFFFFFF0u;
+    constexpr uint32_t kRing = kFrMaxDelay * 8u;        // bytes per instance ring
+
+    float *win = lds + wib * kFrRegion;                 // [kFrSlots][64]
+    float *wcol = win + lane;
+    float *stage = win + kFrSlots * 64;                 // [32][kFrStride]
+
+    // window of the chunk starting at t: first position (t - D - 1) rounded down to even, as an
+    // offset from t (the ring position of t is (a.t0 + f0) mod 48000)
+    auto rel_of = [&](uint32_t t) { return (int)(((int64_t)t - (int64_t)D - 1) & ~(int64_t)1) - (int)t; };
+    // cooperative window load: piece P = r * 64 + lane of 320 -> instance jj = P / 10, piece m
+    float4 v[5];
+    auto load_window = [&](uint32_t t) {
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            const uint32_t P = (uint32_t)r * 64u + lane, jj = P / 10u, m = P % 10u;
+            const int rel = __builtin_amdgcn_ds_bpermute((int)(jj << 3), rel_of(t));   // lane 2 jj
+            const uint32_t oj = min(inst0 + jj, n - 1) - inst0;   // ring within the wave's descriptor
+            const uint32_t pos = wrap48k((int64_t)t + rel + 2 * (int)m);
+            v[r] = ch::ld4(rR, oj * kRing + pos * 8u);
+        }
+    };
+    auto stage_window = [&]() {
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            const uint32_t P = (uint32_t)r * 64u + lane, jj = P / 10u, m = P % 10u;
+            float *p = win + 2u * m * 64u + 2u * jj;
+            *(float2 *)p = make_float2(v[r].x, v[r].y);
+            *(float2 *)(p + 64) = make_float2(v[r].z, v[r].w);
+        }
+    };
+
+    float x[kFrChunk], xn[kFrChunk], y[kFrChunk];
+    const uint32_t t00 = a.t0;                          // ring position of frame 0
+    int C = (int)min((uint32_t)kFrChunk, nf);
+#pragma unroll
+    for (int k = 0; k < kFrChunk; ++k) x[k] = k < C ? ch::ld1(rIn, io_v, (uint32_t)k * frame_b) : 0.f;
+    load_window(t00);
+    for (uint32_t f0 = 0; f0 < nf; f0 += kFrChunk) {
+        C = (int)min((uint32_t)kFrChunk, nf - f0);
+        const int Cn = f0 + kFrChunk < nf ? (int)min((uint32_t)kFrChunk, nf - f0 - kFrChunk) : 0;
+        const uint32_t t = t00 + f0;                    // chunk's first position, unreduced
+        const int rel = rel_of(t);
+        // ---- 1. this chunk's window -> LDS (loaded one chunk ahead), patched with the previous
+        //         chunk's writes that had not reached the ring when it was loaded ----
+        stage_window();
+        if (f0 > 0) {
+#pragma unroll
+            for (int k = 0; k < kFrChunk; ++k) {
+                const int s = k - kFrChunk - rel;       // slot of position t - 16 + k
+                if (s >= 0 && s < kFrWin) wcol[s * 64] = y[k];
+            }
+        }
+        // ---- 2. the next chunk's inputs and window in flight (unconditional) ----
+#pragma unroll
+        for (int k = 0; k < kFrChunk; ++k) {
+            const float vv = ch::ld1(rIn, io_v, min(f0 + kFrChunk + (uint32_t)k, nf - 1u) * frame_b);
+            xn[k] = k < Cn ? vv : 0.f;
+        }
+        load_window(t + kFrChunk);
+        // ---- 3. the frames ----
+        auto frame = [&](auto generic_tag, int k) {
+            constexpr bool GENERIC = decltype(generic_tag)::value;
+            if (GENERIC && k >= C) return;
+            // DelayLine::Read: a at delay D, b at D + 1 (slots k - D - rel, one below)
+            const int sa = k - (int)D - rel;
+            const float av = wcol[sa * 64], bv = wcol[(sa - 1) * 64];
+            const float r = av + (bv - av) * frac;
+            const float w = x[k] + (feedback * r);      // DelayLine::Write
+            y[k] = w;
+            wcol[min(k - rel, kFrWin) * 64] = w;        // visible to later frames of this chunk
+            // DelayFx: filter_ (LowPass) on channel 0, in place
+            const float fr = svf_tick(r, dfreq, ddamp, ddrive, 0u, dlow, dband);
+            const float buf = ch == 0 ? fr : r;
+            const float a0 = (buf * dbal) + (x[k] * (1 - dbal));
+            // ReverbFx over the ReverbSc stub
+            const float vb = a0 * 0.8f;
+            const float b0 = (vb * rbal) + (a0 * (1 - rbal));
+            // FilterFx filter1 on channel 0; channel 1 of buf_c stays 0
+            const float c = svf_tick(b0, ffreq, fdamp, fdrive, ftype, flow, fband);
+            const float o = (ch == 0 ? c : 0.0f) * master;
+            ch::st1(rOut, out_v, (f0 + (uint32_t)k) * frame_b, o);
+        };
+        if (C == kFrChunk) {
+#pragma unroll
+            for (int k = 0; k < kFrChunk; ++k) frame(std::false_type{}, k);
+        } else {
+#pragma unroll
+            for (int k = 0; k < kFrChunk; ++k) frame(std::true_type{}, k);
+        }
+        // ---- 4. the chunk's writes -> ring (staged [instance][frame][ch], 8 lanes per 128 B) ----
+        {
+            float *st = stage + j * kFrStride + ch;
+#pragma unroll
+            for (int k = 0; k < kFrChunk; ++k) st[2 * k] = y[k];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t q = (uint32_t)r * 64u + lane, o = q >> 3, f2 = 2u * (q & 7u);
+                const float4 vv = *(const float4 *)(stage + o * kFrStride + 2u * f2);
+                const uint32_t oi = inst0 + o;
+                if (oi < n && (int)f2 < C) ch::st4(rR, o * kRing + wrap48k((int64_t)t + f2) * 8u, vv);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kFrChunk; ++k) x[k] = xn[k];
+    }
+    if (!valid || ch != 0) return;
+    a.state[FRS_DLOW * n + i] = __float_as_uint(dlow);
+    a.state[FRS_DBAND * n + i] = __float_as_uint(dband);
+    a.state[FRS_FLOW * n + i] = __float_as_uint(flow);
+    a.state[FRS_FBAND * n + i] = __float_as_uint(fband);
+}
+
+hipError_t launch_fxrack(const FxRackArgs &a, hipStream_t s) {
+    if (a.n == 0 || a.n_frames == 0) return hipSuccess;
+    if ((a.n_frames & 3u) || (a.t0 & 1u) || a.t0 >= kFrMaxDelay) return hipErrorInvalidValue;
+    if ((a.plane + (uint64_t)a.n_frames * a.n) * 4 >= (1ull << 32)) return hipErrorInvalidValue;
+    const uint32_t waves = (a.n + 31) / 32;
+    const uint32_t blocks = (waves + kFrThreads / 64 - 1) / (kFrThreads / 64);
+    const size_t lds = (size_t)(kFrThreads / 64) * kFrRegion * sizeof(float);
+    hipLaunchKernelGGL(fxrack_block_v1, dim3(blocks), dim3(kFrThreads), lds, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace olfx

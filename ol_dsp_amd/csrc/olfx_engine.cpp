@@ -67,8 +67,20 @@ uint32_t n_params_of(int kind) {
     case OLFX_KIND_PITCHSHIFT: return OLFX_PS_NPARAMS;
     case OLFX_KIND_VOICE: return OLFX_VC_NPARAMS;
     case OLFX_KIND_CHAIN: return OLFX_CN_NPARAMS;
+    case OLFX_KIND_FXRACK: return OLFX_FR_NPARAMS;
     default: return 0;
     }
+}
+
+// ol::core::scale (modules/corelib/ol_corelib.h:27-44), t_sample = float
+float core_scale(float in, float inlow, float inhigh, float outlow, float outhigh, float power) {
+    const float denom = inhigh - inlow;
+    const float inscale = denom == 0.f ? 0.f : (float)(1.f / denom);
+    const float outdiff = outhigh - outlow;
+    float value = (in - inlow) * inscale;
+    if (value > 0.0f) value = powf(value, power);
+    else if (value < 0.0f) value = -powf(-value, power);
+    return (value * outdiff) + outlow;
 }
 
 // Reference defaults of the user-facing parameters.
@@ -122,6 +134,20 @@ void default_params(int kind, float *p) {
         default_params(OLFX_KIND_CHORUS, p + OLFX_CN_CHORUS0);
         default_params(OLFX_KIND_PITCHSHIFT, p + OLFX_CN_PITCH0);
         default_params(OLFX_KIND_DATTORRO, p + OLFX_CN_VERB0);
+        break;
+    case OLFX_KIND_FXRACK:
+        // Fx.h member defaults; DelayFx::Init sets its filter through UpdateMidiControl(CC, 64 / 24)
+        p[OLFX_FR_DELAY_TIME] = 0.5f;
+        p[OLFX_FR_DELAY_FEEDBACK] = 0.5f;
+        p[OLFX_FR_DELAY_BALANCE] = 0.33f;
+        p[OLFX_FR_DELAY_CUTOFF] = core_scale(64.f, 0.f, 127.f, 0.f, 20000.f, 1.f);
+        p[OLFX_FR_DELAY_RESONANCE] = core_scale(24.f, 0.f, 127.f, 0.f, 1.f, 1.f);
+        p[OLFX_FR_REVERB_BALANCE] = 0.1f;
+        p[OLFX_FR_FILTER_CUTOFF] = 20000.f;
+        p[OLFX_FR_FILTER_RESONANCE] = 0.f;
+        p[OLFX_FR_FILTER_DRIVE] = 0.f;
+        p[OLFX_FR_FILTER_TYPE] = 0.f;
+        p[OLFX_FR_MASTER_VOLUME] = 0.8f;
         break;
     default: break;
     }
@@ -215,6 +241,35 @@ float adsr_sustain(float s) { return (s <= 0.f) ? -0.01f : (s > 1.f ? 1.f : s); 
 
 // Voice: `configured` = false reproduces SynthVoice::Init without any Update()
 // (SynthVoice.h:31-39): DaisySP Init defaults in the envelopes and the Svf.
+// FxRack<2> (modules/fxlib/Fx.h:398-492): DelayLine::SetDelay(scale(time, 0,1, 0,48000, 1)),
+// and FilterFx::Update = Svf SetFreq, SetRes, SetDrive (DaisySP restated, as oracle/fxrack_ref.c)
+void svf_coef(float cutoff, float res_in, float drive_in, float sr, float *freq, float *damp, float *drive) {
+    const float fc = clampf(cutoff, 1.0e-6f, sr / 3.f);
+    const float f = 2.0f * sinf(3.1415927410125732f * std::min(0.25f, fc / (sr * 2.0f)));
+    const float res = clampf(res_in, 0.f, 1.f);
+    *freq = f;
+    *damp = std::min(2.0f * (1.0f - powf(res, 0.25f)), std::min(2.0f, 2.0f / f - f * 0.5f));
+    *drive = clampf(drive_in * 0.1f, 0.f, 1.f) * res;
+}
+
+void derive_fxrack(const float *p, float sr, uint32_t *c) {
+    auto put = [&](int k, float v) { std::memcpy(&c[k], &v, 4); };
+    const float dly = core_scale(p[OLFX_FR_DELAY_TIME], 0.f, 1.f, 0.f, (float)kFrMaxDelay, 1.f);
+    const int32_t id = (int32_t)dly;
+    c[FRC_DELAY] = (uint32_t)id < kFrMaxDelay ? (uint32_t)id : kFrMaxDelay - 1;
+    put(FRC_FRAC, dly - (float)id);
+    put(FRC_FEEDBACK, p[OLFX_FR_DELAY_FEEDBACK]);
+    put(FRC_DBAL, p[OLFX_FR_DELAY_BALANCE]);
+    float f, d, dr;
+    svf_coef(p[OLFX_FR_DELAY_CUTOFF], p[OLFX_FR_DELAY_RESONANCE], 0.f, sr, &f, &d, &dr);
+    put(FRC_DFREQ, f); put(FRC_DDAMP, d); put(FRC_DDRIVE, dr);
+    put(FRC_RBAL, p[OLFX_FR_REVERB_BALANCE]);
+    svf_coef(p[OLFX_FR_FILTER_CUTOFF], p[OLFX_FR_FILTER_RESONANCE], p[OLFX_FR_FILTER_DRIVE], sr, &f, &d, &dr);
+    put(FRC_FFREQ, f); put(FRC_FDAMP, d); put(FRC_FDRIVE, dr);
+    c[FRC_FTYPE] = (uint32_t)(int32_t)p[OLFX_FR_FILTER_TYPE];
+    put(FRC_MASTER, p[OLFX_FR_MASTER_VOLUME]);
+}
+
 void derive_voice(const float *p, bool configured, float sr, float *c) {
     float tgt;
     if (!configured) {
@@ -285,6 +340,9 @@ struct olfx_engine {
     size_t d_bytes = 0;
 
     // dattorro (also the chain's reverb stage)
+    // fx rack
+    float *fr_ring = nullptr;
+    uint32_t *fr_state = nullptr, *fr_coef = nullptr;
     uint32_t n_dt = 0;           // reverb-stage instances: n, or n rounded up to 64 for the chain
     float *dt_rings = nullptr;
     float *dt_state = nullptr;
@@ -359,6 +417,7 @@ uint64_t state_bytes(int kind, uint32_t n, float sr) {
     case OLFX_KIND_PITCHSHIFT: return ch * n;
     case OLFX_KIND_VOICE: return vc * n;
     case OLFX_KIND_CHAIN: return (dt + 2 * ch) * n;
+    case OLFX_KIND_FXRACK: return ((uint64_t)kFrMaxDelay * 2 * 4 + FRS_N * 4 + FRC_N * 4) * n;
     default: return 0;
     }
 }
@@ -400,6 +459,17 @@ int upload_params(olfx_engine *e, hipStream_t s) {
         HIPCHK(e, hipMemcpyAsync(e->ch_coef, c.data(), c.size() * 4, hipMemcpyHostToDevice, s));
         if (e->kind == OLFX_KIND_CHAIN)
             HIPCHK(e, hipMemcpyAsync(e->ps_coef, c2.data(), c2.size() * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(e, hipStreamSynchronize(s));
+    }
+    if (e->kind == OLFX_KIND_FXRACK) {
+        std::vector<uint32_t> c((size_t)FRC_N * n);
+        uint32_t cc[FRC_N];
+        for (uint32_t i = 0; i < n; ++i) {
+            gather(i);
+            derive_fxrack(p.data(), e->sr, cc);
+            for (int k = 0; k < FRC_N; ++k) c[(size_t)k * n + i] = cc[k];
+        }
+        HIPCHK(e, hipMemcpyAsync(e->fr_coef, c.data(), c.size() * 4, hipMemcpyHostToDevice, s));
         HIPCHK(e, hipStreamSynchronize(s));
     }
     if (e->kind == OLFX_KIND_VOICE) {
@@ -548,6 +618,20 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hip
         r = launch_voice(a, s);
         break;
     }
+    case OLFX_KIND_FXRACK: {
+        FxRackArgs a{};
+        a.ring = e->fr_ring;
+        a.state = e->fr_state;
+        a.coef = e->fr_coef;
+        a.in = din;
+        a.out = dout;
+        a.plane = (uint64_t)n_frames * e->n;
+        a.n = e->n;
+        a.n_frames = n_frames;
+        a.t0 = (uint32_t)(e->frames % kFrMaxDelay);
+        r = launch_fxrack(a, s);
+        break;
+    }
     case OLFX_KIND_CHAIN: {
         // one fused launch: chorus and pitch-shift waves feed the reverb wave through LDS
         ChainArgs a{};
@@ -641,6 +725,13 @@ int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32
     const bool has_ch = kind == OLFX_KIND_CHORUS || kind == OLFX_KIND_PITCHSHIFT || kind == OLFX_KIND_CHAIN;
     const bool has_ps = kind == OLFX_KIND_CHAIN;
     const bool has_vc = kind == OLFX_KIND_VOICE;
+    const bool has_fr = kind == OLFX_KIND_FXRACK;
+    size_t o_fr_r = 0, o_fr_s = 0, o_fr_c = 0;
+    if (has_fr) {
+        o_fr_r = cv.take((size_t)kFrMaxDelay * 2 * n * 4);
+        o_fr_s = cv.take((size_t)FRS_N * n * 4);
+        o_fr_c = cv.take((size_t)FRC_N * n * 4);
+    }
     if (has_dt) {
         o_dt_r = cv.take((size_t)dt_total_floats() * e->n_dt * 4);
         o_dt_s = cv.take((size_t)DTS_N * e->n_dt * 4);
@@ -687,6 +778,11 @@ int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32
         e->ps_cring = (float *)(base + o_ps_c);
         e->ps_state = (uint32_t *)(base + o_ps_s);
         e->ps_coef = (uint32_t *)(base + o_ps_k);
+    }
+    if (has_fr) {
+        e->fr_ring = (float *)(base + o_fr_r);
+        e->fr_state = (uint32_t *)(base + o_fr_s);
+        e->fr_coef = (uint32_t *)(base + o_fr_c);
     }
     if (has_vc) {
         e->vc_state = (float *)(base + o_vc_s);
@@ -828,6 +924,7 @@ double olfx_algorithmic_bytes_per_frame(const olfx_engine *e) {
     case OLFX_KIND_PITCHSHIFT: return 40.0;    // 2 x (w + 2 taps) x 4 + 16 I/O
     case OLFX_KIND_VOICE: return 5.4;          // 4 B out + per-block state
     case OLFX_KIND_CHAIN: return 228.6;
+    case OLFX_KIND_FXRACK: return 32.0;       // ring write 8 + ring read 8 + I/O 16 per stereo frame
     default: return 0.0;
     }
 }
@@ -840,6 +937,7 @@ const char *olfx_kernel_name(const olfx_engine *e) {
     case OLFX_KIND_PITCHSHIFT: return "chorus_block_v10";
     case OLFX_KIND_VOICE: return "voice_block_v2";
     case OLFX_KIND_CHAIN: return "chain_block_v1";
+    case OLFX_KIND_FXRACK: return "fxrack_block_v1";
     default: return "";
     }
 }

@@ -165,7 +165,35 @@ struct VoiceArgs {
     uint32_t n, n_frames;
 };
 
+// ----------------------------------------------------------------------------------------------
+// Effect rack ol::fx::FxRack<2> (fxrack.hip): delay lines + two Svf (channel 0) + ReverbSc stub.
+// ----------------------------------------------------------------------------------------------
+constexpr uint32_t kFrMaxDelay = 48000;     // MAX_DELAY (modules/fxlib/Fx.h:23): ring positions
+enum {
+    FRC_DELAY = 0,      // uint: DelayLine delay_ (integer part, clamped to 47999)
+    FRC_FRAC,           // DelayLine frac_
+    FRC_FEEDBACK, FRC_DBAL,
+    FRC_DFREQ, FRC_DDAMP, FRC_DDRIVE,       // DelayFx filter_ Svf (LowPass)
+    FRC_RBAL,                               // ReverbFx balance
+    FRC_FFREQ, FRC_FDAMP, FRC_FDRIVE,       // FxRack filter1 Svf
+    FRC_FTYPE,          // uint: 0 low, 1 band, 2 high, 3 notch, 4 peak
+    FRC_MASTER,
+    FRC_N
+};
+enum { FRS_DLOW = 0, FRS_DBAND, FRS_FLOW, FRS_FBAND, FRS_N };
+struct FxRackArgs {
+    float *ring;                // [n][kFrMaxDelay][2] stereo-interleaved delay lines
+    uint32_t *state;            // [FRS_N][n] (floats stored bitwise)
+    const uint32_t *coef;       // [FRC_N][n]
+    const float *in;            // [2][..][n]
+    float *out;                 // [2][..][n]
+    uint64_t plane;
+    uint32_t n, n_frames;
+    uint32_t t0;                // ring position of the first frame: frames since create mod 48000
+};
+
 // Launchers (defined in the .hip files).
+hipError_t launch_fxrack(const FxRackArgs &a, hipStream_t s);
 // The fused chain (chain.hip): chorus -> pitch-shift -> dattorro in one launch.  c1 / c2 / d
 // carry each stage's rings, state and coefficients (their in / out fields are unused); the
 // reverb stage's instance count d.n is n rounded up to 64 (padding instances compute harmlessly).

@@ -26,6 +26,7 @@ KIND_NAMES = {
     "pitchshift": _lib.KIND_PITCHSHIFT,
     "voice": _lib.KIND_VOICE,
     "chain": _lib.KIND_CHAIN,
+    "fxrack": _lib.KIND_FXRACK,
 }
 
 # parameter field names, in C-ABI order
@@ -38,6 +39,9 @@ PARAMS = {
                       "filter_attack", "filter_attack_shape", "filter_decay", "filter_sustain",
                       "filter_release", "amp_env_amount", "amp_attack", "amp_attack_shape",
                       "amp_decay", "amp_sustain", "amp_release", "portamento"],
+    _lib.KIND_FXRACK: ["delay_time", "delay_feedback", "delay_balance", "delay_cutoff", "delay_resonance",
+                       "reverb_balance", "filter_cutoff", "filter_resonance", "filter_drive", "filter_type",
+                       "master_volume"],
 }
 PARAMS[_lib.KIND_CHAIN] = (["chorus_" + p for p in PARAMS[_lib.KIND_CHORUS]]
                            + ["pitch_" + p for p in PARAMS[_lib.KIND_PITCHSHIFT]]

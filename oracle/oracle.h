@@ -66,6 +66,29 @@ int oracle_voice_config(oracle_voice *o, int inst, const float *values);
 int oracle_voice_note(oracle_voice *o, int inst, int on, int note);
 int oracle_voice_process(oracle_voice *o, float *out, int n_frames, int n_threads);
 
+/* ---- fxlib effect rack ol::fx::FxRack<2> (spec oracle for the DaisySP parts, parity unpinned) ---- */
+enum {
+    OFR_DELAY_TIME = 0,        /* DelayFx time [0,1] -> SetDelay(time * 48000)          Fx.h:172,214 */
+    OFR_DELAY_FEEDBACK,        /* DelayFx feedback                                      Fx.h:173 */
+    OFR_DELAY_BALANCE,         /* DelayFx wet/dry balance                               Fx.h:174 */
+    OFR_DELAY_CUTOFF,          /* DelayFx filter_ cutoff, Hz                            Fx.h:188 */
+    OFR_DELAY_RESONANCE,       /* DelayFx filter_ resonance [0,1]                       Fx.h:189 */
+    OFR_REVERB_BALANCE,        /* ReverbFx balance                                      Fx.h:282 */
+    OFR_FILTER_CUTOFF,         /* FxRack filter1 cutoff, Hz                             Fx.h:75 */
+    OFR_FILTER_RESONANCE,      /* FxRack filter1 resonance [0,1] */
+    OFR_FILTER_DRIVE,          /* FxRack filter1 drive [0,1] */
+    OFR_FILTER_TYPE,           /* 0 low, 1 band, 2 high, 3 notch, 4 peak                Fx.h:67-73 */
+    OFR_MASTER_VOLUME,         /* FxRack master_volume                                  Fx.h:405 */
+    OFR_NPARAMS
+};
+typedef struct oracle_fxrack oracle_fxrack;
+void oracle_fxrack_defaults(float *p);
+oracle_fxrack *oracle_fxrack_create(int n_inst, float sample_rate);
+void oracle_fxrack_destroy(oracle_fxrack *o);
+int oracle_fxrack_set(oracle_fxrack *o, int inst, int field, float value);
+/* in / out: [2][n_frames][n_inst] */
+int oracle_fxrack_process(oracle_fxrack *o, const float *in, float *out, int n_frames, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,6 +22,9 @@ REF_LIB_O0 = os.path.join(HERE, "_ref", "libverb_ref_O0.so")
 DT_FIELDS = ["pre_delay", "pre_filter", "input_diffusion1", "input_diffusion2",
              "decay_diffusion", "decay", "damping"]
 CH_FIELDS = ["pitch", "mix", "q", "cutoff", "phase", "depth", "rate", "window"]
+FR_FIELDS = ["delay_time", "delay_feedback", "delay_balance", "delay_cutoff", "delay_resonance",
+             "reverb_balance", "filter_cutoff", "filter_resonance", "filter_drive", "filter_type",
+             "master_volume"]
 VC_FIELDS = ["filter_cutoff", "filter_resonance", "filter_drive", "filter_env_amount",
              "filter_attack", "filter_attack_shape", "filter_decay", "filter_sustain",
              "filter_release", "amp_env_amount", "amp_attack", "amp_attack_shape",
@@ -67,6 +70,12 @@ def lib() -> ctypes.CDLL:
         L.oracle_voice_config.argtypes = [ctypes.c_void_p, ctypes.c_int, _PF]
         L.oracle_voice_note.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.oracle_voice_process.argtypes = [ctypes.c_void_p, _PF, ctypes.c_int, ctypes.c_int]
+        L.oracle_fxrack_defaults.argtypes = [_PF]
+        L.oracle_fxrack_create.restype = ctypes.c_void_p
+        L.oracle_fxrack_create.argtypes = [ctypes.c_int, _F]
+        L.oracle_fxrack_destroy.argtypes = [ctypes.c_void_p]
+        L.oracle_fxrack_set.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _F]
+        L.oracle_fxrack_process.argtypes = [ctypes.c_void_p, _PF, _PF, ctypes.c_int, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -206,4 +215,37 @@ class Voice(_Bank):
     def process(self, frames: int, threads: int = 1) -> np.ndarray:
         out = np.empty((1, frames, self.n), dtype=np.float32)
         assert self.L.oracle_voice_process(self.h, _pf(out), frames, threads) == 0
+        return out
+
+
+def fxrack_defaults() -> np.ndarray:
+    p = np.zeros(len(FR_FIELDS), np.float32)
+    lib().oracle_fxrack_defaults(_pf(p))
+    return p
+
+
+class FxRack(_Bank):
+    """ol::fx::FxRack<2>: stereo in -> delay -> reverb (ReverbSc stub) -> filter (ch 0) -> master."""
+
+    def __init__(self, n: int, sample_rate: float = 48000.0):
+        self.n = n
+        self.L = lib()
+        self.h = self.L.oracle_fxrack_create(n, sample_rate)
+        assert self.h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.oracle_fxrack_destroy(self.h)
+            self.h = None
+
+    def set(self, inst: int, field, value: float) -> None:
+        f = FR_FIELDS.index(field) if isinstance(field, str) else int(field)
+        assert self.L.oracle_fxrack_set(self.h, inst, f, value) == 0
+
+    def process(self, x: np.ndarray, threads: int = 1) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        ch, frames, n = x.shape
+        assert ch == 2 and n == self.n
+        out = np.empty_like(x)
+        assert self.L.oracle_fxrack_process(self.h, _pf(x), _pf(out), frames, threads) == 0
         return out

@@ -95,6 +95,24 @@ def voice_configs(rng: np.random.Generator, n: int) -> np.ndarray:
     return p
 
 
+def fxrack_params(rng: np.random.Generator, n: int) -> np.ndarray:
+    """Same draw as tests/helpers.py: fxrack_params."""
+    p = np.empty((11, n), dtype=np.float32)
+    p[0] = rng.uniform(0, 1, n)
+    p[0, ::4] = rng.uniform(0, 17, len(p[0, ::4])) / 48000
+    p[1] = rng.uniform(0, 0.9, n)
+    p[2] = rng.uniform(0, 1, n)
+    p[3] = rng.uniform(100, 12000, n)
+    p[4] = rng.uniform(0, 0.8, n)
+    p[5] = rng.uniform(0, 1, n)
+    p[6] = rng.uniform(100, 12000, n)
+    p[7] = rng.uniform(0, 0.8, n)
+    p[8] = rng.uniform(0, 1, n)
+    p[9] = rng.integers(0, 5, n).astype(np.float32)
+    p[10] = rng.uniform(0, 1, n)
+    return p
+
+
 def main() -> None:
     if not O.ref_available() or not O.ref_available(o0=True):
         O.build()
@@ -167,6 +185,18 @@ def main() -> None:
     yv = np.concatenate([ya, yb], axis=1)
     gold["voice"] = {"n": nv, "frames": fv, "note_off_at": fv // 2, "notes": notes, "params": pv.tolist(),
                      "fnv1a64": [f"{O.fnv1a64_lr(yv[0, :, i], yv[0, :, i]):016x}" for i in range(nv)]}
+
+    # ---- fx rack (FxRack<2>): frozen spec-oracle vectors, past the echo and the 48000 wrap ----
+    nr, fr = 6, 60000
+    pr = fxrack_params(np.random.default_rng(91), nr)
+    xr = noise_block(nr, fr, 900)
+    rk = O.FxRack(nr)
+    for i in range(nr):
+        for f in range(pr.shape[0]):
+            rk.set(i, f, float(pr[f, i]))
+    yr = rk.process(xr)
+    gold["fxrack"] = {"n": nr, "frames": fr, "input_base": 900, "params": pr.tolist(),
+                      "fnv1a64": [f"{O.fnv1a64_lr(yr[0, :, i], yr[1, :, i]):016x}" for i in range(nr)]}
 
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(gold, f, indent=1)

@@ -83,3 +83,21 @@ def voice_configs(rng: np.random.Generator, n: int) -> np.ndarray:
     p[14] = rng.uniform(0.001, 0.5, n)
     p[15] = rng.uniform(0, 0.05, n)
     return p
+
+def fxrack_params(rng: np.random.Generator, n: int) -> np.ndarray:
+    """FxRack<2> member values (FR_FIELDS order), seeded; every 4th instance gets a delay shorter
+    than a 16-frame chunk (time * 48000 in [0, 17)), the path that reads its own chunk's writes."""
+    p = np.empty((11, n), dtype=np.float32)
+    p[0] = rng.uniform(0, 1, n)
+    p[0, ::4] = rng.uniform(0, 17, len(p[0, ::4])) / 48000
+    p[1] = rng.uniform(0, 0.9, n)
+    p[2] = rng.uniform(0, 1, n)
+    p[3] = rng.uniform(100, 12000, n)
+    p[4] = rng.uniform(0, 0.8, n)
+    p[5] = rng.uniform(0, 1, n)
+    p[6] = rng.uniform(100, 12000, n)
+    p[7] = rng.uniform(0, 0.8, n)
+    p[8] = rng.uniform(0, 1, n)
+    p[9] = rng.integers(0, 5, n).astype(np.float32)
+    p[10] = rng.uniform(0, 1, n)
+    return p

@@ -66,6 +66,9 @@ def test_abi_version_and_kind_info():
     vc = ofx.kind_info(ofx.KIND_VOICE)
     assert (vc.n_params, vc.in_channels, vc.out_channels) == (16, 0, 1)
     assert ofx.kind_info(ofx.KIND_CHAIN).n_params == 8 + 2 + 7
+    fr = ofx.kind_info(ofx.KIND_FXRACK)
+    assert fr.n_params == 11 and fr.in_channels == 2 and fr.out_channels == 2
+    assert fr.state_bytes_per_instance == (48000 * 2 + 4 + 13) * 4
     with pytest.raises(ofx.OlfxError):
         ofx.kind_info(99)
 

@@ -8,8 +8,8 @@ import numpy as np
 import pytest
 
 import oracle as O
-from helpers import (bits_equal, chorus_params, dt_params, fast_noise, first_mismatch, noise_block,
-                     rel_err, voice_configs)
+from helpers import (bits_equal, chorus_params, dt_params, fast_noise, first_mismatch, fxrack_params,
+                     noise_block, rel_err, voice_configs)
 
 pytestmark = pytest.mark.gpu
 
@@ -362,3 +362,61 @@ def test_chain_vs_composed_oracle(cuda):
             d.set(i, f, float(pd[f, i]))
     yr = d.process(c2.process(c1.process(x)))
     assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
+# ------------------------------------------------------------------------------- fx rack
+def _fxrack_pair(n, p):
+    e = engine("fxrack", n)
+    e.set_params(0, p)
+    ref = O.FxRack(n)
+    for i in range(n):
+        for f in range(p.shape[0]):
+            ref.set(i, f, float(p[f, i]))
+    return e, ref
+
+
+@pytest.mark.parametrize("n", [37, 96])
+def test_fxrack_vs_oracle(cuda, n):
+    """FxRack<2> bit-exact against the oracle: ragged instance counts, partial chunks, and
+    delays from 0 to 47999 samples (every 4th instance shorter than a chunk)."""
+    rng = np.random.default_rng(n)
+    p = fxrack_params(rng, n)
+    p[0, 1] = 1.0                     # the clamp to 47,999
+    p[0, 2] = 0.0                     # delay 0: reads the sample written 48,000 frames ago
+    x = fast_noise(n, 3000, seed=n)
+    e, ref = _fxrack_pair(n, p)
+    y = run_gpu(e, x, [256] * 5 + [4, 12, 240, 1460], cuda)
+    yr = ref.process(x, threads=8)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
+def test_fxrack_long_run_wraps_and_param_change(cuda):
+    """110,000 frames: the 48,000-position rings wrap twice; the delay time changes between
+    blocks (DelayFx::Update, Fx.h:209-216)."""
+    n = 64
+    rng = np.random.default_rng(5)
+    p = fxrack_params(rng, n)
+    x = fast_noise(n, 110000, seed=5)
+    e, ref = _fxrack_pair(n, p)
+    y1 = run_gpu(e, x[:, :60000], [4096] * 14 + [2656], cuda)
+    yr1 = ref.process(x[:, :60000], threads=8)
+    p2 = fxrack_params(rng, n)
+    e.set_params(0, p2[:1])
+    for i in range(n):
+        ref.set(i, 0, float(p2[0, i]))
+    y2 = run_gpu(e, x[:, 60000:], [4096] * 12 + [1848], cuda)
+    yr2 = ref.process(x[:, 60000:], threads=8)
+    y, yr = np.concatenate([y1, y2], 1), np.concatenate([yr1, yr2], 1)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
+def test_fxrack_golden_and_channel1_silent(cuda, golden):
+    g = golden["fxrack"]
+    p = np.asarray(g["params"], np.float32)
+    x = noise_block(g["n"], g["frames"], g["input_base"])
+    e = engine("fxrack", g["n"])
+    e.set_params(0, p)
+    y = run_gpu(e, x, [2048] * 29 + [608], cuda)
+    assert [f"{O.fnv1a64_lr(y[0, :, i], y[1, :, i]):016x}" for i in range(g["n"])] == g["fnv1a64"]
+    assert np.all(y[1] == 0)
+

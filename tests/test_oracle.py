@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from helpers import bits_equal, first_mismatch, noise_block
+from helpers import bits_equal, first_mismatch, fxrack_params, noise_block
 
 
 # ---------------------------------------------------------------- dattorro, vs golden fixtures
@@ -211,3 +211,53 @@ def test_voice_reference_pins_synth_test():
 def test_voice_silent_until_note():
     vo = O.Voice(2)
     assert np.all(vo.process(512) == 0)
+
+
+# ------------------------------------------------------------------------------- fx rack
+def test_fxrack_defaults_and_echo():
+    """FxRack<2> at its reference defaults (Fx.h): the delay echo arrives exactly
+    scale(0.5, 0,1, 0,48000) = 24000 samples later, and channel 1 of the output stays 0 because
+    FilterFx writes only channel 0 (Fx.h:88-108) into the zero-initialised buf_c (Fx.h:408)."""
+    p = O.fxrack_defaults()
+    assert p[0] == 0.5 and p[2] == np.float32(0.33) and p[10] == np.float32(0.8)
+    assert p[3] == np.float32(64 * np.float32(1 / 127)) * 20000
+    r = O.FxRack(1)
+    x = np.zeros((2, 30000, 1), np.float32)
+    x[:, 0, 0] = 1.0
+    y = r.process(x)
+    assert np.all(y[1] == 0)
+    assert abs(y[0, 0, 0]) > 0.1
+    quiet = np.abs(y[0, 2000:23990, 0]).max()
+    echo = np.abs(y[0, 24000:24200, 0]).max()
+    assert echo > 100 * quiet
+
+
+def test_fxrack_sine_never_nan():
+    """test/fx_test.cpp:25-55: the delay fed a 20 kHz sine at 48 kHz for one second never
+    outputs NaN (here through the whole rack, every filter type, a few delay settings)."""
+    n = 10
+    r = O.FxRack(n)
+    for i in range(n):
+        r.set(i, "filter_type", float(i % 5))
+        r.set(i, "delay_time", [0.5, 0.0, 1.0, 1e-5, 0.25][i % 5])
+    t = np.arange(48000, dtype=np.float64)
+    s = (0.5 * np.sin(2 * np.pi * 20000 * t / 48000)).astype(np.float32)
+    x = np.broadcast_to(s[None, :, None], (2, 48000, n)).copy()
+    y = r.process(x, threads=4)
+    assert np.all(np.isfinite(y))
+
+
+def test_fxrack_blocked_equals_unblocked_and_golden(golden):
+    g = golden["fxrack"]
+    p = np.asarray(g["params"], np.float32)
+    x = noise_block(g["n"], g["frames"], g["input_base"])
+    a, b = O.FxRack(g["n"]), O.FxRack(g["n"])
+    for i in range(g["n"]):
+        for f in range(p.shape[0]):
+            a.set(i, f, float(p[f, i]))
+            b.set(i, f, float(p[f, i]))
+    ya = a.process(x)
+    yb = np.concatenate([b.process(x[:, s:s + 1000]) for s in range(0, g["frames"], 1000)], 1)
+    assert bits_equal(ya, yb), first_mismatch(ya, yb)
+    assert [f"{O.fnv1a64_lr(ya[0, :, i], ya[1, :, i]):016x}" for i in range(g["n"])] == g["fnv1a64"]
+
