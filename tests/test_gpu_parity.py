@@ -385,7 +385,7 @@ def test_fxrack_vs_oracle(cuda, n):
     p[0, 2] = 0.0                     # delay 0: reads the sample written 48,000 frames ago
     x = fast_noise(n, 3000, seed=n)
     e, ref = _fxrack_pair(n, p)
-    y = run_gpu(e, x, [256] * 5 + [4, 12, 240, 1460], cuda)
+    y = run_gpu(e, x, [256] * 5 + [4, 12, 240, 1464], cuda)
     yr = ref.process(x, threads=8)
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
@@ -404,7 +404,7 @@ def test_fxrack_long_run_wraps_and_param_change(cuda):
     e.set_params(0, p2[:1])
     for i in range(n):
         ref.set(i, 0, float(p2[0, i]))
-    y2 = run_gpu(e, x[:, 60000:], [4096] * 12 + [1848], cuda)
+    y2 = run_gpu(e, x[:, 60000:], [4096] * 12 + [848], cuda)
     yr2 = ref.process(x[:, 60000:], threads=8)
     y, yr = np.concatenate([y1, y2], 1), np.concatenate([yr1, yr2], 1)
     assert bits_equal(y, yr), first_mismatch(y, yr)
