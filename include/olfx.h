@@ -132,6 +132,24 @@ typedef struct olfx_event {
     uint8_t  pad;
 } olfx_event;
 
+/* ---- control changes (MIDI CC / hardware controls; corelib/cc_map.h numbers) ----
+   The reference's UpdateMidiControl(control, 0..127) / UpdateHardwareControl(control, float)
+   mapped to one parameter field, per kind:
+     OLFX_KIND_VOICE : SynthVoice::UpdateMidiControl / UpdateHardwareControl (SynthVoice.h:100-229)
+     OLFX_KIND_FXRACK: FxRack::UpdateMidiControl / UpdateHardwareControl (Fx.h:451-489) and the
+                       DelayFx / ReverbFx / FilterFx handlers it forwards to (Fx.h:116-163, 218-267, 313-391)
+   Controls the reference ignores for a kind (its `default: update = false`) are skipped. */
+enum { OLFX_CTL_MIDI = 0, OLFX_CTL_HARDWARE = 1 };
+#define OLFX_IGNORED 1                 /* olfx_control_map: the reference ignores this control */
+#define OLFX_FIELD_UPDATE_ONLY 0xFFFFFFFFu   /* handled control that sets no modelled field (Update() only) */
+typedef struct olfx_control_event {
+    uint32_t inst;
+    uint8_t  control;   /* CC number, corelib/cc_map.h */
+    uint8_t  source;    /* OLFX_CTL_MIDI (value 0..127) or OLFX_CTL_HARDWARE (value as given) */
+    uint16_t pad;
+    float    value;
+} olfx_control_event;
+
 /* ---- I/O flags ---- */
 enum {
     OLFX_IO_DEVICE = 0,  /* in/out are device pointers (no copies; the fast path) */
@@ -170,6 +188,14 @@ int olfx_set_params(olfx_engine *e, uint32_t first, uint32_t count, uint32_t fie
 int olfx_set_param(olfx_engine *e, uint32_t inst, uint32_t field, float value);
 /* Read back the current (host shadow) value of one parameter. */
 int olfx_get_param(olfx_engine *e, uint32_t inst, uint32_t field, float *value);
+
+/* Map one control change to (field, value) exactly as the reference handler scales it
+   (ol::core::scale, corelib/ol_corelib.h:31-44).  Returns OLFX_OK, OLFX_IGNORED, or an error.
+   Pure host function: no engine, no device. */
+int olfx_control_map(int kind, uint8_t control, int source, float value, uint32_t *field, float *param_value);
+/* Apply control changes in order (each: the mapped olfx_set_param; ignored controls skipped).
+   Replaces UpdateMidiControl / UpdateHardwareControl per instance. */
+int olfx_control(olfx_engine *e, const olfx_control_event *ev, uint32_t n);
 
 /* Queue note events (voices); applied in order at the start of the next olfx_process. */
 int olfx_note_events(olfx_engine *e, const olfx_event *ev, uint32_t n);

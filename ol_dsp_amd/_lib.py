@@ -63,6 +63,21 @@ class Event(ctypes.Structure):
     ]
 
 
+class ControlEvent(ctypes.Structure):
+    _fields_ = [
+        ("inst", ctypes.c_uint32),
+        ("control", ctypes.c_uint8),
+        ("source", ctypes.c_uint8),
+        ("pad", ctypes.c_uint16),
+        ("value", ctypes.c_float),
+    ]
+
+
+CTL_MIDI = 0
+CTL_HARDWARE = 1
+IGNORED = 1
+FIELD_UPDATE_ONLY = 0xFFFFFFFF
+
 # every symbol include/olfx.h declares, with (restype, argtypes)
 _P = ctypes.c_void_p
 _U32 = ctypes.c_uint32
@@ -77,6 +92,9 @@ SIGNATURES = {
     "olfx_set_param": (ctypes.c_int, [_P, _U32, _U32, _F]),
     "olfx_get_param": (ctypes.c_int, [_P, _U32, _U32, ctypes.POINTER(_F)]),
     "olfx_note_events": (ctypes.c_int, [_P, ctypes.POINTER(Event), _U32]),
+    "olfx_control_map": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint8, ctypes.c_int, _F, ctypes.POINTER(_U32),
+                                        ctypes.POINTER(_F)]),
+    "olfx_control": (ctypes.c_int, [_P, ctypes.POINTER(ControlEvent), _U32]),
     "olfx_process": (ctypes.c_int, [_P, _P, _P, _U32, ctypes.c_int, _P]),
     "olfx_sync": (ctypes.c_int, [_P]),
     "olfx_stream": (_P, [_P]),

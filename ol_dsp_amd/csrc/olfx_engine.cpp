@@ -842,6 +842,91 @@ int olfx_set_params(olfx_engine *e, uint32_t first, uint32_t count, uint32_t fie
     return OLFX_OK;
 }
 
+// ---- control changes (corelib/cc_map.h) ----
+namespace {
+enum : uint8_t {
+    CC_CTL_PORTAMENTO = 5, CC_CTL_VOLUME = 7,
+    CC_REVERB_BALANCE = 34,
+    CC_DELAY_TIME = 35, CC_DELAY_FEEDBACK = 36, CC_DELAY_CUTOFF = 37, CC_DELAY_RESONANCE = 38,
+    CC_DELAY_BALANCE = 39,
+    CC_FILTER_CUTOFF = 41, CC_FILTER_RESONANCE = 42, CC_FILTER_DRIVE = 44,
+    CC_FX_FILTER_CUTOFF = 45, CC_FX_FILTER_RESONANCE = 46, CC_FX_FILTER_TYPE = 47, CC_FX_FILTER_DRIVE = 48,
+    CC_ENV_FILT_AMT = 73, CC_ENV_FILT_A = 74, CC_ENV_FILT_D = 75, CC_ENV_FILT_S = 76, CC_ENV_FILT_R = 77,
+    CC_ENV_AMP_A = 108, CC_ENV_AMP_D = 109, CC_ENV_AMP_S = 110, CC_ENV_AMP_R = 111,
+    CC_OSC_1_VOLUME = 114,
+};
+}  // namespace
+
+int olfx_control_map(int kind, uint8_t control, int source, float value, uint32_t *field, float *param_value) {
+    if (!field || !param_value || (source != OLFX_CTL_MIDI && source != OLFX_CTL_HARDWARE)) return OLFX_E_ARG;
+    const bool midi = source == OLFX_CTL_MIDI;
+    // MIDI: ol::core::scale(val, 0, 127, lo, hi, power); hardware: scale(value, 0, 1, ...) or raw
+    auto sc = [&](float hi, float power) {
+        return midi ? core_scale(value, 0.f, 127.f, 0.f, hi, power) : core_scale(value, 0.f, 1.f, 0.f, hi, power);
+    };
+    const float unit = midi ? core_scale(value, 0.f, 127.f, 0.f, 1.f, 1.f) : value;   // `scaled` / raw value
+    auto put = [&](uint32_t f, float v) { *field = f; *param_value = v; return OLFX_OK; };
+    if (kind == OLFX_KIND_VOICE) {                 // SynthVoice.h:100-229
+        switch (control) {
+        case CC_CTL_VOLUME: return put(OLFX_VC_AMP_ENV_AMOUNT, unit);
+        case CC_CTL_PORTAMENTO: return put(OLFX_VC_PORTAMENTO, sc(1.f, 4.f));
+        case CC_FILTER_CUTOFF: return put(OLFX_VC_FILTER_CUTOFF, sc(20000.f, 2.5f));
+        case CC_FILTER_RESONANCE: return put(OLFX_VC_FILTER_RESONANCE, unit);
+        case CC_FILTER_DRIVE: return put(OLFX_VC_FILTER_DRIVE, unit);
+        case CC_ENV_FILT_AMT: return put(OLFX_VC_FILTER_ENV_AMOUNT, unit);
+        case CC_ENV_FILT_A: return put(OLFX_VC_FILTER_ATTACK, unit);
+        case CC_ENV_FILT_D: return put(OLFX_VC_FILTER_DECAY, sc(1.f, 3.f));
+        case CC_ENV_FILT_S: return put(OLFX_VC_FILTER_SUSTAIN, unit);
+        case CC_ENV_FILT_R: return put(OLFX_VC_FILTER_RELEASE, unit);
+        case CC_ENV_AMP_A: return put(OLFX_VC_AMP_ATTACK, unit);
+        case CC_ENV_AMP_D: return put(OLFX_VC_AMP_DECAY, unit);
+        case CC_ENV_AMP_S: return put(OLFX_VC_AMP_SUSTAIN, unit);
+        case CC_ENV_AMP_R: return put(OLFX_VC_AMP_RELEASE, unit);
+        case CC_OSC_1_VOLUME: return put(OLFX_FIELD_UPDATE_ONLY, unit);   // osc_1_mix: unused by Process
+        default: return OLFX_IGNORED;
+        }
+    }
+    if (kind == OLFX_KIND_FXRACK) {                // FxRack -> FilterFx / DelayFx / ReverbFx
+        switch (control) {
+        case CC_FX_FILTER_CUTOFF: return put(OLFX_FR_FILTER_CUTOFF, midi ? sc(20000.f, 1.f) : sc(20000.f, 1.02f));
+        case CC_FX_FILTER_RESONANCE: return put(OLFX_FR_FILTER_RESONANCE, unit);
+        case CC_FX_FILTER_DRIVE: return put(OLFX_FR_FILTER_DRIVE, unit);
+        case CC_FX_FILTER_TYPE: return put(OLFX_FR_FILTER_TYPE, (float)(int32_t)sc(5.f, 1.f));   // FilterType(float)
+        case CC_DELAY_TIME: return put(OLFX_FR_DELAY_TIME, unit);
+        case CC_DELAY_FEEDBACK: return put(OLFX_FR_DELAY_FEEDBACK, unit);
+        case CC_DELAY_BALANCE: return put(OLFX_FR_DELAY_BALANCE, unit);
+        case CC_DELAY_CUTOFF:                      // DelayFx handles these in MIDI only (Fx.h:253-260)
+            return midi ? put(OLFX_FR_DELAY_CUTOFF, sc(20000.f, 1.f)) : OLFX_IGNORED;
+        case CC_DELAY_RESONANCE: return midi ? put(OLFX_FR_DELAY_RESONANCE, unit) : OLFX_IGNORED;
+        case CC_REVERB_BALANCE: return put(OLFX_FR_REVERB_BALANCE, unit);
+        case CC_CTL_VOLUME: return put(OLFX_FR_MASTER_VOLUME, unit);
+        default: return OLFX_IGNORED;              // incl. the reverb CCs that reach only the ReverbSc stub
+        }
+    }
+    return n_params_of(kind) ? OLFX_IGNORED : OLFX_E_KIND;
+}
+
+int olfx_control(olfx_engine *e, const olfx_control_event *ev, uint32_t n) {
+    if (!e) return OLFX_E_ARG;
+    if (n && !ev) return e->fail(OLFX_E_ARG, "olfx_control: null events");
+    for (uint32_t k = 0; k < n; ++k) {
+        if (ev[k].inst >= e->n) return e->fail(OLFX_E_ARG, "olfx_control: event %u: instance out of range", k);
+        uint32_t field;
+        float v;
+        const int rc = olfx_control_map(e->kind, ev[k].control, ev[k].source, ev[k].value, &field, &v);
+        if (rc == OLFX_IGNORED) continue;
+        if (rc != OLFX_OK) return e->fail(rc, "olfx_control: event %u", k);
+        if (field == OLFX_FIELD_UPDATE_ONLY) {    // Update() with unchanged members
+            if (e->kind == OLFX_KIND_VOICE) e->configured[ev[k].inst] = 1;
+            e->dirty = true;
+            continue;
+        }
+        const int r2 = olfx_set_params(e, ev[k].inst, 1, field, 1, &v);
+        if (r2 != OLFX_OK) return r2;
+    }
+    return OLFX_OK;
+}
+
 int olfx_set_param(olfx_engine *e, uint32_t inst, uint32_t field, float value) {
     return olfx_set_params(e, inst, 1, field, 1, &value);
 }

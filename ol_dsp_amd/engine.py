@@ -136,6 +136,20 @@ class Engine:
             arr[k].velocity = int(e[3]) if len(e) > 3 else 100
         check(self.lib.olfx_note_events(self._h, arr, len(evs)), self._h)
 
+    def control(self, events: Iterable[Sequence]) -> None:
+        """Control changes, applied in order: iterable of (inst, cc, value[, source]); source
+        "midi" (value 0..127, the default) or "hw" (UpdateHardwareControl value)."""
+        evs = list(events)
+        if not evs:
+            return
+        arr = (_lib.ControlEvent * len(evs))()
+        for k, e in enumerate(evs):
+            arr[k].inst = int(e[0])
+            arr[k].control = int(e[1])
+            arr[k].value = float(e[2])
+            arr[k].source = _lib.CTL_HARDWARE if len(e) > 3 and e[3] in ("hw", _lib.CTL_HARDWARE) else _lib.CTL_MIDI
+        check(self.lib.olfx_control(self._h, arr, len(evs)), self._h)
+
     # ---- processing ----
     def process(self, x, out=None, n_frames: Optional[int] = None, stream=None):
         """Process one block for all instances.
@@ -197,3 +211,22 @@ class Engine:
     @property
     def kernel_name(self) -> str:
         return self.lib.olfx_kernel_name(self._h).decode()
+
+
+def control_map(kind, control: int, value: float, source: str = "midi"):
+    """The reference's UpdateMidiControl / UpdateHardwareControl mapping for one control change
+    (host-only, no device): (field name or "update_only", mapped value), or None if the
+    reference ignores the control for this kind."""
+    k = KIND_NAMES[kind] if isinstance(kind, str) else int(kind)
+    lib = load()
+    field = ctypes.c_uint32()
+    val = ctypes.c_float()
+    src = _lib.CTL_HARDWARE if source in ("hw", _lib.CTL_HARDWARE) else _lib.CTL_MIDI
+    rc = lib.olfx_control_map(k, int(control), src, float(value), ctypes.byref(field), ctypes.byref(val))
+    if rc == _lib.IGNORED:
+        return None
+    check(rc, None)
+    if field.value == _lib.FIELD_UPDATE_ONLY:
+        return "update_only", val.value
+    return PARAMS[k][field.value], val.value
+

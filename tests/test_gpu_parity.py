@@ -420,3 +420,44 @@ def test_fxrack_golden_and_channel1_silent(cuda, golden):
     assert [f"{O.fnv1a64_lr(y[0, :, i], y[1, :, i]):016x}" for i in range(g["n"])] == g["fnv1a64"]
     assert np.all(y[1] == 0)
 
+
+
+# ------------------------------------------------------------------- control changes (8f row 4)
+def test_control_changes_equal_mapped_params(cuda):
+    """olfx_control applies the reference's CC handlers: an engine driven by MIDI / hardware
+    control changes matches one given the mapped values by set_param (bit-exact), and the fx
+    rack also matches the oracle configured with those values."""
+    import ol_dsp_amd as ofx
+    n = 8
+    evs = [(i, cc, v) for i in range(n) for cc, v in ((35, 3 + 9 * i), (36, 50), (39, 80), (37, 70),
+                                                      (45, 90), (47, 20 * i % 128), (34, 64), (7, 100))]
+    evs += [(0, 45, 0.3, "hw"), (1, 35, 0.25, "hw"), (2, 32, 99)]       # cc 32: reverb stub, ignored
+    e1, e2 = engine("fxrack", n), engine("fxrack", n)
+    e1.control(evs)
+    ref = O.FxRack(n)
+    for ev in evs:
+        m = ofx.control_map("fxrack", ev[1], ev[2], ev[3] if len(ev) > 3 else "midi")
+        if m is not None:
+            e2.set_param(ev[0], m[0], m[1])
+            ref.set(ev[0], m[0], m[1])
+    x = fast_noise(n, 2048, seed=8)
+    y1, y2 = run_gpu(e1, x, [256] * 8, cuda), run_gpu(e2, x, [256] * 8, cuda)
+    yr = ref.process(x)
+    assert bits_equal(y1, y2) and bits_equal(y1, yr), first_mismatch(y1, yr)
+
+    # voice: cutoff / envelope CCs, and osc_1_mix (cc 114), which only re-runs Update() --
+    # an unconfigured voice then leaves the DaisySP defaults for the SynthVoice member values
+    nv = 4
+    vevs = [(0, 41, 90), (0, 75, 40), (1, 5, 30), (2, 114, 64), (3, 41, 0.5, "hw")]
+    v1, v2 = engine("voice", nv), engine("voice", nv)
+    v1.control(vevs)
+    for ev in vevs:
+        m = ofx.control_map("voice", ev[1], ev[2], ev[3] if len(ev) > 3 else "midi")
+        if m[0] == "update_only":
+            v2.set_param(ev[0], 0, v2.get_param(ev[0], 0))    # configure with unchanged members
+        else:
+            v2.set_param(ev[0], m[0], m[1])
+    for v in (v1, v2):
+        v.note_events([(i, 1, 48 + 5 * i) for i in range(nv)])
+    a, b = _voice_run(v1, 1024, cuda), _voice_run(v2, 1024, cuda)
+    assert bits_equal(a, b), first_mismatch(a, b)
