@@ -95,9 +95,18 @@ public:
         check(olfx_process(e_, in, out, n_frames, io, stream), e_, "olfx_process");
     }
     void sync() { check(olfx_sync(e_), e_, "olfx_sync"); }
+    /* UpdateMidiControl / UpdateHardwareControl of the reference operator (SynthVoice.h:100-229,
+       Fx.h:451-489): applied at the next process; controls the reference ignores are skipped. */
+    void UpdateMidiControl(uint32_t i, uint8_t control, uint8_t value) { ctl(i, control, OLFX_CTL_MIDI, value); }
+    void UpdateHardwareControl(uint32_t i, uint8_t control, float value) { ctl(i, control, OLFX_CTL_HARDWARE, value); }
     void reset() { check(olfx_reset(e_), e_, "olfx_reset"); }
 
 protected:
+    void ctl(uint32_t i, uint8_t control, int source, float value) {
+        olfx_control_event ev{};
+        ev.inst = i; ev.control = control; ev.source = (uint8_t)source; ev.value = value;
+        check(olfx_control(e_, &ev, 1), e_, "olfx_control");
+    }
     olfx_engine *e_ = nullptr;
 };
 
@@ -150,6 +159,19 @@ public:
         : Engine(OLFX_KIND_PITCHSHIFT, n_inst, sample_rate, block, device) {}
     void SetShift(uint32_t i, float hz) { set(i, OLFX_PS_SHIFT, hz); }
     void SetWindow(uint32_t i, float ms) { set(i, OLFX_PS_WINDOW, ms); }
+};
+
+/* ol::fx::FxRack<2> over N racks (modules/fxlib/Fx.h:398-492): DelayFx -> ReverbFx (over the
+   in-tree ReverbSc stub) -> FilterFx -> master volume; stereo in, [2][F][N] out (channel 1 is 0,
+   as in the reference: FilterFx writes only channel 0 of the rack's zeroed output buffer). */
+class FxRackBank : public Engine {
+public:
+    FxRackBank(uint32_t n_inst, float sample_rate, uint32_t block = 256, int device = 0)
+        : Engine(OLFX_KIND_FXRACK, n_inst, sample_rate, block, device) {}
+    void Process(const float *frame_in, float *frame_out, uint32_t n_frames,
+                 int io = OLFX_IO_HOST, void *stream = nullptr) {
+        process(frame_in, frame_out, n_frames, io, stream);
+    }
 };
 
 /* ol::synth::SynthVoice over N voices (SynthVoice.h). The config array is in Voice::Config field

@@ -196,6 +196,31 @@ TEST(Synth, VoiceNoteOnOffPins) {
     EXPECT_TRUE(y[1] != 0.f && y[1] != 1.f);
 }
 
+/* FxRack<2> driven by MIDI control changes (FxRack::UpdateMidiControl) vs the oracle given the
+   same reference scaling (ol::core::scale with power 1 is exact: v * (1/127) * range). */
+TEST(FxRack, MidiControlledRackMatchesOracle) {
+    const uint32_t n = 40, frames = 1024;
+    olfx::FxRackBank rack(n, 48000.f);
+    oracle_fxrack *ref = oracle_fxrack_create((int)n, 48000.f);
+    const float inv127 = 1.f / 127.f;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t t = (uint8_t)(2 + 3 * i), fb = 64, cut = (uint8_t)(40 + i);
+        rack.UpdateMidiControl(i, 35, t);        // CC_DELAY_TIME
+        rack.UpdateMidiControl(i, 36, fb);       // CC_DELAY_FEEDBACK
+        rack.UpdateMidiControl(i, 45, cut);      // CC_FX_FILTER_CUTOFF
+        oracle_fxrack_set(ref, (int)i, OFR_DELAY_TIME, (float)t * inv127 * 1.f + 0.f);
+        oracle_fxrack_set(ref, (int)i, OFR_DELAY_FEEDBACK, (float)fb * inv127 * 1.f + 0.f);
+        oracle_fxrack_set(ref, (int)i, OFR_FILTER_CUTOFF, (float)cut * inv127 * 20000.f + 0.f);
+    }
+    std::vector<float> x = noise(2, frames, n, 10);
+    std::vector<float> y = run_blocks([&](const float *a, float *b, uint32_t f) { rack.Process(a, b, f); },
+                                      x, 2, 2, frames, n, 256);
+    std::vector<float> yr(y.size());
+    oracle_fxrack_process(ref, x.data(), yr.data(), (int)frames, 8);
+    EXPECT_TRUE(first_bit_mismatch(y, yr) == (size_t)-1);
+    oracle_fxrack_destroy(ref);
+}
+
 /* Error behaviour: failures throw olfx::Error carrying the C-ABI code; nothing is silent. */
 TEST(Boundary, ErrorsThrowWithCode) {
     int code = 0;

@@ -35,4 +35,4 @@ def test_cpp_operators_on_gpu():
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=600)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "6 tests, 0 failures" in r.stdout
+    assert "7 tests, 0 failures" in r.stdout
