@@ -33,11 +33,18 @@ FP32_VALU_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md)
 # SetFreq 1, polyBLEP saw 11, 0.5 gain 1, filter-env cutoff 3, Svf::SetFreq 8 + sin, two Svf
 # passes 22, Low() average 3, output 1, sin and the three divisions 4 -> 64.
 VOICE_FLOPS_PER_SAMPLE = 64.0
+# MoogFilter voice: the same voice minus the Svf (27) plus daisysp::LadderFilter: SetAlpha/Qadjust
+# 20, input drive 1, and per 4x-oversampled step: feedback sum 9, Pade tanh 6, four stages 24,
+# accumulate 3 (x4 = 168) -> 216.
+VOICE_MOOG_FLOPS_PER_SAMPLE = 216.0
+VOICE_KINDS = ("voice", "voice_moog")
 WORKLOADS = {
     # name: (kind, default instances per GPU, BASELINE config it restates)
     "chorus": ("chorus", 65536, "configs[1]: 65,536 ChorusEffect instances, 48 kHz, 256-sample blocks, 1xMI355X"),
     "dattorro": ("dattorro", 65536, "configs[2]: 65,536 dattorro-verb instances (full network), 48 kHz"),
     "voice": ("voice", 32768, "configs[3]: 262,144 synthlib voices = 32,768 per GPU x 8"),
+    "voice_moog": ("voice_moog", 32768, "SURVEY 8f row 3: configs[3] with the Daisy firmware's MoogFilter "
+                   "(daisysp::LadderFilter) voices, 32,768 per GPU"),
     "chain": ("chain", 16384, "configs[4]: 131,072 chorus->pitch-shift->dattorro chains = 16,384 per GPU x 8"),
     "pitchshift": ("pitchshift", 65536, "pitch-shift stage alone"),
     "fxrack": ("fxrack", 65536, "SURVEY 8f row 1: fxlib FxRack<2> (delay -> reverb -> filter -> master), 65,536 instances"),
@@ -72,7 +79,7 @@ def draw_params(kind: str, n: int, seed: int) -> np.ndarray:
              u(.2, 1), u(.001, .5), u(0, 1), u(.001, .5), u(0, 1), u(.001, .5), u(0, .05)]
     rack = [u(0.05, 1), u(0, .9), u(0, 1), u(100, 12000), u(0, .8), u(0, 1), u(100, 12000), u(0, .8),
             u(0, 1), rng.integers(0, 5, n).astype(np.float32), u(0, 1)]
-    table = {"chorus": chorus, "pitchshift": pitch, "dattorro": verb, "voice": voice,
+    table = {"chorus": chorus, "pitchshift": pitch, "dattorro": verb, "voice": voice, "voice_moog": voice,
              "chain": chorus + pitch + verb, "fxrack": rack}
     return np.stack(table[kind])
 
@@ -82,7 +89,7 @@ def cpu_baseline(kind: str, block: int, sr: float, budget_s: float, threads: int
     same workload: a bank of instances, 256-frame blocks, until the wall budget is spent."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    n = 8192 if kind != "voice" else 32768
+    n = 8192 if kind not in VOICE_KINDS else 32768
     rng = np.random.default_rng(7)
     p = draw_params(kind, n, 7)
     x = (rng.random((2, block, n), dtype=np.float32) - 0.5)
@@ -107,8 +114,8 @@ def cpu_baseline(kind: str, block: int, sr: float, budget_s: float, threads: int
             for f in range(p.shape[0]):
                 bank.set(i, f, float(p[f, i]))
         step = lambda: bank.process(x, threads)  # noqa: E731
-    elif kind == "voice":
-        bank = O.Voice(n, sr)
+    elif kind in VOICE_KINDS:
+        bank = O.Voice(n, sr, moog=kind == "voice_moog")
         for i in range(n):
             bank.config(i, p[:, i])
             bank.note(i, True, 36 + i % 60)
@@ -126,7 +133,7 @@ def cpu_baseline(kind: str, block: int, sr: float, budget_s: float, threads: int
         if el >= budget_s:
             break
     frames = blocks * block * n
-    return {"value": frames / el, "unit": "stereo samples/s" if kind != "voice" else "voice samples/s",
+    return {"value": frames / el, "unit": "stereo samples/s" if kind not in VOICE_KINDS else "voice samples/s",
             "cores": threads, "kind": kind_used,
             "sample": f"{n} instances x {blocks} blocks x {block} frames ({el:.1f} s wall, {threads} OpenMP threads"
                       f"{', oracle/_ref = libs/dattorro-verb/verb.cpp -O2' if kind_used == 'reference' else ', oracle C restatement -O2'})"}
@@ -159,7 +166,7 @@ def main():
     pool_n = max(2, int(args.pool_bytes // blk_bytes)) if ich else 1
     pool = [torch.rand((ich, B, n), generator=gen, device=dev) - 0.5 for _ in range(pool_n)] if ich else [None]
     out = torch.empty((och, B, n), device=dev)
-    if kind == "voice":   # NoteOn for every voice at block 0
+    if kind in VOICE_KINDS:   # NoteOn for every voice at block 0
         eng.note_events([(i, 1, 36 + (i * 7) % 61) for i in range(n)])
     stream = torch.cuda.Stream(dev)        # dedicated non-default stream: events see the kernels
     torch.cuda.synchronize(dev)
@@ -211,12 +218,13 @@ def main():
                     traffic = tr.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        if kind == "voice":
-            tflops = VOICE_FLOPS_PER_SAMPLE * n * B / (kern_ms * 1e-3) / 1e12
+        if kind in VOICE_KINDS:
+            fps = VOICE_MOOG_FLOPS_PER_SAMPLE if kind == "voice_moog" else VOICE_FLOPS_PER_SAMPLE
+            tflops = fps * n * B / (kern_ms * 1e-3) / 1e12
             roofline = {"bound": "valu", "achieved": tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,
                         "kernel": eng.kernel_name, "kernel_ms": kern_ms,
-                        "algorithmic_flops_per_frame": VOICE_FLOPS_PER_SAMPLE,
+                        "algorithmic_flops_per_frame": fps,
                         "algorithmic_bytes_per_frame": bpf, "hbm_gbs": achieved, "frames_per_launch": n * B}
         else:
             roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -230,7 +238,7 @@ def main():
         res = {
             "metric": METRIC,
             "value": value,
-            "unit": "voice samples/s" if kind == "voice" else "stereo samples/s",
+            "unit": "voice samples/s" if kind in VOICE_KINDS else "stereo samples/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,

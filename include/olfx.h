@@ -60,7 +60,11 @@ enum {
     OLFX_KIND_PITCHSHIFT = 3,  /* gen~ pitchshift, stereo */
     OLFX_KIND_VOICE      = 4,  /* synthlib SynthVoice: polyBLEP saw -> SVF LP (env cutoff) -> amp env; mono out */
     OLFX_KIND_CHAIN      = 5,  /* fused chorus -> pitch-shift -> dattorro, stereo */
-    OLFX_KIND_FXRACK     = 6   /* fxlib ol::fx::FxRack<2>: delay -> reverb -> filter -> master (Fx.h:398-492) */
+    OLFX_KIND_FXRACK     = 6,  /* fxlib ol::fx::FxRack<2>: delay -> reverb -> filter -> master (Fx.h:398-492) */
+    OLFX_KIND_VOICE_MOOG = 7   /* SynthVoice(OscillatorSoundSource, MoogFilter): the Daisy synth firmware voice
+                                  (ol_daisy/app/synth/main.cpp:49-52); daisysp::LadderFilter LP24 in place of the
+                                  SVF (Filter.h:35-63).  Same OLFX_VC_* parameters (FILTER_DRIVE is ignored:
+                                  MoogFilter::SetDrive is a no-op), note events and control changes. */
 };
 
 /* ---- parameters (field index, value is what the reference setter takes) ---- */

@@ -179,8 +179,12 @@ public:
    the next Process, in call order. */
 class VoiceBank : public Engine {
 public:
-    VoiceBank(uint32_t n_inst, float sample_rate, uint32_t block = 256, int device = 0)
-        : Engine(OLFX_KIND_VOICE, n_inst, sample_rate, block, device) {}
+    /* filter: the SynthVoice's Filter (SynthVoice.h:22-29) -- SvfFilter (default, OLFX_KIND_VOICE)
+     * or MoogFilter (OLFX_KIND_VOICE_MOOG, the Daisy synth firmware's voices, main.cpp:49-52) */
+    enum class Filter { Svf, Moog };
+    VoiceBank(uint32_t n_inst, float sample_rate, uint32_t block = 256, int device = 0, Filter filter = Filter::Svf)
+        : Engine(filter == Filter::Moog ? OLFX_KIND_VOICE_MOOG : OLFX_KIND_VOICE, n_inst, sample_rate, block,
+                 device) {}
     /* SynthVoice::UpdateConfig + Update (SynthVoice.h:55-98) */
     void UpdateConfig(uint32_t i, const float config[OLFX_VC_NPARAMS]) {
         set_block(i, 1, 0, OLFX_VC_NPARAMS, config);   /* [16][1] field-major == the config array */
@@ -189,20 +193,17 @@ public:
     void NoteOff(uint32_t i, uint8_t midi_note, uint8_t velocity) { push(i, OLFX_EV_NOTE_OFF, midi_note, velocity); }
     /* frame_out [1][F][N] */
     void Process(float *frame_out, uint32_t n_frames, int io = OLFX_IO_HOST, void *stream = nullptr) {
-        if (!events_.empty()) {
-            check(olfx_note_events(e_, events_.data(), (uint32_t)events_.size()), e_, "olfx_note_events");
-            events_.clear();
-        }
         process(nullptr, frame_out, n_frames, io, stream);
     }
 
 private:
+    /* the engine queues note events itself and applies them, in call order, at the next process
+       (olfx_note_events), so Engine::process (BlockAdapter) sees them too */
     void push(uint32_t i, uint8_t type, uint8_t note, uint8_t vel) {
         olfx_event ev{};
         ev.inst = i; ev.type = type; ev.note = note; ev.velocity = vel;
-        events_.push_back(ev);
+        check(olfx_note_events(e_, &ev, 1), e_, "olfx_note_events");
     }
-    std::vector<olfx_event> events_;
 };
 
 }  // namespace olfx

@@ -29,6 +29,7 @@ KIND_PITCHSHIFT = 3
 KIND_VOICE = 4
 KIND_CHAIN = 5
 KIND_FXRACK = 6
+KIND_VOICE_MOOG = 7
 
 IO_DEVICE = 0
 IO_HOST = 1

@@ -65,7 +65,8 @@ uint32_t n_params_of(int kind) {
     case OLFX_KIND_DATTORRO: return OLFX_DT_NPARAMS;
     case OLFX_KIND_CHORUS: return OLFX_CH_NPARAMS;
     case OLFX_KIND_PITCHSHIFT: return OLFX_PS_NPARAMS;
-    case OLFX_KIND_VOICE: return OLFX_VC_NPARAMS;
+    case OLFX_KIND_VOICE:
+    case OLFX_KIND_VOICE_MOOG: return OLFX_VC_NPARAMS;
     case OLFX_KIND_CHAIN: return OLFX_CN_NPARAMS;
     case OLFX_KIND_FXRACK: return OLFX_FR_NPARAMS;
     default: return 0;
@@ -112,6 +113,7 @@ void default_params(int kind, float *p) {
         p[OLFX_PS_WINDOW] = 10.0f;
         break;
     case OLFX_KIND_VOICE:
+    case OLFX_KIND_VOICE_MOOG:
         // SynthVoice member defaults (SynthVoice.h:285-311); Config order (Voice.h:14-31)
         p[OLFX_VC_FILTER_CUTOFF] = 0.0f;
         p[OLFX_VC_FILTER_RESONANCE] = 0.0f;
@@ -270,7 +272,7 @@ void derive_fxrack(const float *p, float sr, uint32_t *c) {
     put(FRC_MASTER, p[OLFX_FR_MASTER_VOLUME]);
 }
 
-void derive_voice(const float *p, bool configured, float sr, float *c) {
+void derive_voice(const float *p, bool configured, bool moog, float sr, float *c) {
     float tgt;
     if (!configured) {
         // daisysp::Adsr::Init: attack 0.1 s shape 0, decay 0.1 s, release 0.1 s, sustain 0.7
@@ -312,6 +314,15 @@ void derive_voice(const float *p, bool configured, float sr, float *c) {
     c[VCC_FC_MAX] = sr / 3.f;
     c[VCC_SR] = sr;
     c[VCC_INV_SR] = 1.0f / sr;
+    if (moog) {
+        // daisysp::LadderFilter: Init -> SetRes(0.2), SetInputDrive(0.5) (drive <= 1: drive_scaled =
+        // drive), sr_int_recip_ = 1 / (sr * 4); Update -> MoogFilter::SetRes -> SetRes(res):
+        // K = 4 * clamp(res, 0, kMaxResonance 1.8); MoogFilter::SetDrive is a no-op
+        const float res = configured ? p[OLFX_VC_FILTER_RESONANCE] : 0.2f;
+        c[VCC_LADDER_K] = 4.0f * fminf(fmaxf(res, 0.0f), 1.8f);
+        c[VCC_LADDER_DRIVE] = 0.5f;
+        c[VCC_LADDER_WREC] = 1.0f / (sr * 4);
+    }
 }
 
 }  // namespace
@@ -416,6 +427,7 @@ uint64_t state_bytes(int kind, uint32_t n, float sr) {
     case OLFX_KIND_CHORUS:
     case OLFX_KIND_PITCHSHIFT: return ch * n;
     case OLFX_KIND_VOICE: return vc * n;
+    case OLFX_KIND_VOICE_MOOG: return vc * n + (uint64_t)(VCS_N_MOOG - VCS_N) * 4 * n;
     case OLFX_KIND_CHAIN: return (dt + 2 * ch) * n;
     case OLFX_KIND_FXRACK: return ((uint64_t)kFrMaxDelay * 2 * 4 + FRS_N * 4 + FRC_N * 4) * n;
     default: return 0;
@@ -472,12 +484,12 @@ int upload_params(olfx_engine *e, hipStream_t s) {
         HIPCHK(e, hipMemcpyAsync(e->fr_coef, c.data(), c.size() * 4, hipMemcpyHostToDevice, s));
         HIPCHK(e, hipStreamSynchronize(s));
     }
-    if (e->kind == OLFX_KIND_VOICE) {
+    if (is_voice_kind(e->kind)) {
         std::vector<float> c((size_t)VCC_N * n);
         float cc[VCC_N];
         for (uint32_t i = 0; i < n; ++i) {
             gather(i);
-            derive_voice(p.data(), e->configured[i] != 0, e->sr, cc);
+            derive_voice(p.data(), e->configured[i] != 0, e->kind == OLFX_KIND_VOICE_MOOG, e->sr, cc);
             for (int k = 0; k < VCC_N; ++k) c[(size_t)k * n + i] = cc[k];
         }
         HIPCHK(e, hipMemcpyAsync(e->vc_coef, c.data(), c.size() * 4, hipMemcpyHostToDevice, s));
@@ -520,7 +532,7 @@ int apply_events(olfx_engine *e, hipStream_t s) {
 
 int init_state(olfx_engine *e) {
     HIPCHK(e, hipMemsetAsync(e->d_mem, 0, e->d_bytes, e->stream));
-    if (e->kind == OLFX_KIND_VOICE) {
+    if (is_voice_kind(e->kind)) {
         // daisysp Oscillator::Init phase 0; Svf::Init states 0 and freq 0.25; Adsr idle;
         // freq_ = 0 (SynthVoice.h:276); Port z1 = 0.
         std::vector<float> st((size_t)VCS_N * e->n, 0.f);
@@ -608,13 +620,15 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hip
     case OLFX_KIND_PITCHSHIFT:
         r = launch_chorus(ch_args(e->ch_pring, e->ch_cring, e->ch_state, e->ch_coef, din, dout, 1), s);
         break;
-    case OLFX_KIND_VOICE: {
+    case OLFX_KIND_VOICE:
+    case OLFX_KIND_VOICE_MOOG: {
         VoiceArgs a{};
         a.state = e->vc_state;
         a.coef = e->vc_coef;
         a.out = dout;
         a.n = e->n;
         a.n_frames = n_frames;
+        a.moog = e->kind == OLFX_KIND_VOICE_MOOG;
         r = launch_voice(a, s);
         break;
     }
@@ -652,8 +666,8 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hip
     return OLFX_OK;
 }
 
-uint32_t in_channels(int kind) { return kind == OLFX_KIND_VOICE ? 0u : 2u; }
-uint32_t out_channels(int kind) { return kind == OLFX_KIND_VOICE ? 1u : 2u; }
+uint32_t in_channels(int kind) { return is_voice_kind(kind) ? 0u : 2u; }
+uint32_t out_channels(int kind) { return is_voice_kind(kind) ? 1u : 2u; }
 
 }  // namespace
 
@@ -724,7 +738,7 @@ int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32
     const bool has_dt = kind == OLFX_KIND_DATTORRO || kind == OLFX_KIND_CHAIN;
     const bool has_ch = kind == OLFX_KIND_CHORUS || kind == OLFX_KIND_PITCHSHIFT || kind == OLFX_KIND_CHAIN;
     const bool has_ps = kind == OLFX_KIND_CHAIN;
-    const bool has_vc = kind == OLFX_KIND_VOICE;
+    const bool has_vc = is_voice_kind(kind);
     const bool has_fr = kind == OLFX_KIND_FXRACK;
     size_t o_fr_r = 0, o_fr_s = 0, o_fr_c = 0;
     if (has_fr) {
@@ -750,7 +764,7 @@ int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32
         o_ps_k = cv.take((size_t)CHC_N * n * 4);
     }
     if (has_vc) {
-        o_vc_s = cv.take((size_t)VCS_N * n * 4);
+        o_vc_s = cv.take((size_t)voice_state_slots(kind) * n * 4);
         o_vc_c = cv.take((size_t)VCC_N * n * 4);
     }
     e->d_bytes = cv.off;
@@ -836,7 +850,7 @@ int olfx_set_params(olfx_engine *e, uint32_t first, uint32_t count, uint32_t fie
             e->params[(size_t)field * e->n + first + k] = v;
         }
     }
-    if (e->kind == OLFX_KIND_VOICE)
+    if (is_voice_kind(e->kind))
         for (uint32_t k = 0; k < count; ++k) e->configured[first + k] = 1;
     e->dirty = true;
     return OLFX_OK;
@@ -866,7 +880,7 @@ int olfx_control_map(int kind, uint8_t control, int source, float value, uint32_
     };
     const float unit = midi ? core_scale(value, 0.f, 127.f, 0.f, 1.f, 1.f) : value;   // `scaled` / raw value
     auto put = [&](uint32_t f, float v) { *field = f; *param_value = v; return OLFX_OK; };
-    if (kind == OLFX_KIND_VOICE) {                 // SynthVoice.h:100-229
+    if (is_voice_kind(kind)) {                     // SynthVoice.h:100-229
         switch (control) {
         case CC_CTL_VOLUME: return put(OLFX_VC_AMP_ENV_AMOUNT, unit);
         case CC_CTL_PORTAMENTO: return put(OLFX_VC_PORTAMENTO, sc(1.f, 4.f));
@@ -917,7 +931,7 @@ int olfx_control(olfx_engine *e, const olfx_control_event *ev, uint32_t n) {
         if (rc == OLFX_IGNORED) continue;
         if (rc != OLFX_OK) return e->fail(rc, "olfx_control: event %u", k);
         if (field == OLFX_FIELD_UPDATE_ONLY) {    // Update() with unchanged members
-            if (e->kind == OLFX_KIND_VOICE) e->configured[ev[k].inst] = 1;
+            if (is_voice_kind(e->kind)) e->configured[ev[k].inst] = 1;
             e->dirty = true;
             continue;
         }
@@ -939,7 +953,7 @@ int olfx_get_param(olfx_engine *e, uint32_t inst, uint32_t field, float *value) 
 
 int olfx_note_events(olfx_engine *e, const olfx_event *ev, uint32_t n) {
     if (!e) return OLFX_E_ARG;
-    if (e->kind != OLFX_KIND_VOICE) return e->fail(OLFX_E_STATE, "olfx_note_events: not a voice engine");
+    if (!is_voice_kind(e->kind)) return e->fail(OLFX_E_STATE, "olfx_note_events: not a voice engine");
     if (n && !ev) return e->fail(OLFX_E_ARG, "olfx_note_events: null events");
     for (uint32_t k = 0; k < n; ++k) {
         if (ev[k].inst >= e->n || ev[k].note > 127 || ev[k].type > 1)
@@ -960,7 +974,7 @@ int olfx_process(olfx_engine *e, const float *in, float *out, uint32_t n_frames,
     hipStream_t s = (hipStream_t)stream;   // NULL = the HIP default (null) stream
     int rc = upload_params(e, s);
     if (rc) return rc;
-    if (e->kind == OLFX_KIND_VOICE) {
+    if (is_voice_kind(e->kind)) {
         rc = apply_events(e, s);
         if (rc) return rc;
     }
@@ -1008,6 +1022,7 @@ double olfx_algorithmic_bytes_per_frame(const olfx_engine *e) {
     case OLFX_KIND_CHORUS: return 56.0;        // 2 x (pitch w + 2 taps + chorus w + tap) x 4 + 16 I/O
     case OLFX_KIND_PITCHSHIFT: return 40.0;    // 2 x (w + 2 taps) x 4 + 16 I/O
     case OLFX_KIND_VOICE: return 5.4;          // 4 B out + per-block state
+    case OLFX_KIND_VOICE_MOOG: return 5.7;     // 4 B out + per-block state (9 more state words)
     case OLFX_KIND_CHAIN: return 228.6;
     case OLFX_KIND_FXRACK: return 32.0;       // ring write 8 + ring read 8 + I/O 16 per stereo frame
     default: return 0.0;
@@ -1021,6 +1036,7 @@ const char *olfx_kernel_name(const olfx_engine *e) {
     case OLFX_KIND_CHORUS:
     case OLFX_KIND_PITCHSHIFT: return "chorus_block_v10";
     case OLFX_KIND_VOICE: return "voice_block_v2";
+    case OLFX_KIND_VOICE_MOOG: return "voice_block_v2<true>";
     case OLFX_KIND_CHAIN: return "chain_block_v1";
     case OLFX_KIND_FXRACK: return "fxrack_block_v1";
     default: return "";

@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/olfx.h"
+
 #define OLFX_HD __host__ __device__ __forceinline__
 
 namespace olfx {
@@ -150,19 +152,29 @@ enum {
     VCC_FC_MAX,         // sr / 3
     VCC_SR,             // sample rate
     VCC_INV_SR,         // Oscillator sr_recip_ = 1/sr
-    VCC_N
+    VCC_N,
+    // MoogFilter voices reuse the Svf-only slots for the daisysp::LadderFilter coefficients
+    VCC_LADDER_K = VCC_DAMP_RES,      // 4 * clamp(res, 0, 1.8)        (LadderFilter::SetRes)
+    VCC_LADDER_DRIVE = VCC_DRIVE,     // input drive_scaled_ (0.5: Init; MoogFilter::SetDrive is a no-op)
+    VCC_LADDER_WREC = VCC_FC_MAX      // sr_int_recip_ = 1 / (4 sr)     (4x oversampling)
 };
 enum {
     VCS_PHASE = 0, VCS_PORT_Z, VCS_ENVA_X, VCS_ENVF_X, VCS_LOW, VCS_BAND, VCS_FREQ,
     VCS_FLAGS,          // bits 0-2 amp mode, 3-5 filt mode, 6 gate(amp prev), 7 gate(filt prev), 8 gate
-    VCS_N
+    VCS_N,
+    // MoogFilter voices append the LadderFilter state: z0_[4], z1_[4], oldinput_ (VCS_LOW/BAND unused)
+    VCS_LZ0 = VCS_N, VCS_LZ1 = VCS_LZ0 + 4, VCS_LOLD = VCS_LZ1 + 4,
+    VCS_N_MOOG
 };
+inline bool is_voice_kind(int k) { return k == OLFX_KIND_VOICE || k == OLFX_KIND_VOICE_MOOG; }
+inline uint32_t voice_state_slots(int k) { return k == OLFX_KIND_VOICE_MOOG ? (uint32_t)VCS_N_MOOG : (uint32_t)VCS_N; }
 
 struct VoiceArgs {
-    float *state;               // [VCS_N][n]
+    float *state;               // [VCS_N][n], MoogFilter voices [VCS_N_MOOG][n]
     const float *coef;          // [VCC_N][n]
     float *out;                 // [1][n_frames][n]
     uint32_t n, n_frames;
+    uint32_t moog;              // 1: daisysp::LadderFilter (MoogFilter) in place of the Svf
 };
 
 // ----------------------------------------------------------------------------------------------

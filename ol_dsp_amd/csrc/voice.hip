@@ -9,6 +9,13 @@
 // published algorithm ("parity unpinned").  Setter-side transcendentals
 // (expf/logf/powf in Adsr/Svf/Port setters, mtof) run on the host; the per-sample sinf of
 // Svf::SetFreq runs here.  VALU-bound: ~5 B of HBM traffic per sample.
+//
+// MOOG = true is the Daisy synth firmware's voice, SynthVoice(OscillatorSoundSource, MoogFilter)
+// (ol_daisy/app/synth/main.cpp:49-52, Filter.h:35-63): MoogFilter::Process is a no-op and
+// Low(frame) = daisysp::LadderFilter::Process(frame) with SetFreq(fc) (-> SetAlpha) every sample,
+// unclamped.  LadderFilter: 4x linear-interpolated oversampling, Pade tanh of the feedback sum,
+// four one-zero/one-pole stages, LP24 output (restated, [unverified] like the rest of DaisySP;
+// oracle/voice_ref.c ladder_process).  ~4x the Svf voice's VALU work per sample.
 #include "olfx_internal.h"
 
 namespace olfx {
@@ -57,8 +64,54 @@ __device__ __forceinline__ float sin_quarter(float x) {
     return x + (x * x2) * p;
 }
 
+// daisysp::LadderFilter's tanh: Pade approximant, saturating beyond |x| > 3 (the exact division
+// keeps it bit-identical with the oracle)
+__device__ __forceinline__ float ladder_tanh(float x) {
+    const float x2 = x * x;
+    const float r = x * (27.0f + x2) / (27.0f + 9.0f * x2);
+    return x > 3.0f ? 1.0f : (x < -3.0f ? -1.0f : r);
+}
+
+// LadderFilter::LPF stage i: one zero at -0.3 (0.3/1.3 feed-forward of the previous input), one pole
+__device__ __forceinline__ float ladder_lpf(float s, float alpha, float &z0, float &z1) {
+    float ft = s * (1.0f / 1.3f) + (0.3f / 1.3f) * z0 - z1;
+    ft = ft * alpha + z1;
+    z1 = ft;
+    z0 = s;
+    return ft;
+}
+
+struct Ladder {
+    float z0[4], z1[4], old;
+};
+
+// LadderFilter::SetFreq(fc) (SetAlpha) then Process(in), LP24
+__device__ __forceinline__ float ladder_process(Ladder &L, float fc, float in, float k, float drive_scaled,
+                                                float wrec) {
+    const float wc = fc * 2.0f * 3.1415927410125732f * wrec;
+    const float wc2 = wc * wc;
+    const float alpha = 0.9892f * wc - 0.4324f * wc2 + 0.1381f * wc * wc2 - 0.0202f * wc2 * wc2;
+    const float qadj = 1.006f + 0.0536f * wc - 0.095f * wc2 - 0.05f * wc2 * wc2;
+    const float input = in * drive_scaled;
+    float total = 0.0f, interp = 0.0f;
+#pragma unroll
+    for (int os = 0; os < 4; ++os) {
+        float u = (interp * L.old + (1.0f - interp) * input) - (L.z1[3] - 0.5f * input) * k * qadj;
+        u = ladder_tanh(u);
+        const float s1 = ladder_lpf(u, alpha, L.z0[0], L.z1[0]);
+        const float s2 = ladder_lpf(s1, alpha, L.z0[1], L.z1[1]);
+        const float s3 = ladder_lpf(s2, alpha, L.z0[2], L.z1[2]);
+        const float s4 = ladder_lpf(s3, alpha, L.z0[3], L.z1[3]);
+        total += s4 * (1.0f / 4);
+        interp += 1.0f / 4;
+    }
+    L.old = input;
+    return total;
+}
+
 }  // namespace
 
+template <bool MOOG>
 __global__ __launch_bounds__(64) void voice_block_v2(VoiceArgs a) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
@@ -86,6 +139,15 @@ __global__ __launch_bounds__(64) void voice_block_v2(VoiceArgs a) {
     uint32_t mode_a = flags & 7u, mode_f = (flags >> 3) & 7u;
     bool gprev_a = (flags >> 6) & 1u, gprev_f = (flags >> 7) & 1u;
     const bool gate = (flags >> 8) & 1u;
+    Ladder L;
+    if (MOOG) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            L.z0[k] = s[(VCS_LZ0 + k) * n + i];
+            L.z1[k] = s[(VCS_LZ1 + k) * n + i];
+        }
+        L.old = s[VCS_LOLD * n + i];
+    }
 
 #pragma unroll 2
     for (uint32_t f = 0; f < a.n_frames; ++f) {
@@ -104,6 +166,12 @@ __global__ __launch_bounds__(64) void voice_block_v2(VoiceArgs a) {
         // filter envelope -> Svf::SetFreq
         const float fe = adsr(gate, mode_f, gprev_f, xf, atk_d0f, atk_tgf, dec_d0f, rel_d0f, sus_f);
         const float fc_in = cutoff + ((fe * 20000.0f) * fenv_amt);
+        if (MOOG) {
+            // LadderFilter slots: VCC_LADDER_K = damp_res, VCC_LADDER_DRIVE = drive,
+            // VCC_LADDER_WREC = fc_max
+            a.out[(size_t)f * n + i] = ladder_process(L, fc_in, src, damp_res, drive, fc_max) * amp;
+            continue;
+        }
         const float fc = fminf(fmaxf(fc_in, 1.0e-6f), fc_max);
         // the three per-sample divisions of Svf::SetFreq / polyBLEP use the hardware reciprocal
         // (~1 ulp; within the voice tolerance, like sin_quarter)
@@ -135,12 +203,22 @@ __global__ __launch_bounds__(64) void voice_block_v2(VoiceArgs a) {
     s[VCS_LOW * n + i] = low;
     s[VCS_BAND * n + i] = band;
     s[VCS_FLAGS * n + i] = __uint_as_float(flags);
+    if (MOOG) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            s[(VCS_LZ0 + k) * n + i] = L.z0[k];
+            s[(VCS_LZ1 + k) * n + i] = L.z1[k];
+        }
+        s[VCS_LOLD * n + i] = L.old;
+    }
 }
 
 hipError_t launch_voice(const VoiceArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
     const uint32_t threads = 64;       // one wave per workgroup: 32,768 voices spread over every CU
-    hipLaunchKernelGGL(voice_block_v2, dim3((a.n + threads - 1) / threads), dim3(threads), 0, s, a);
+    const dim3 grid((a.n + threads - 1) / threads);
+    if (a.moog) hipLaunchKernelGGL(voice_block_v2<true>, grid, dim3(threads), 0, s, a);
+    else hipLaunchKernelGGL(voice_block_v2<false>, grid, dim3(threads), 0, s, a);
     return hipGetLastError();
 }
 

@@ -27,6 +27,7 @@ KIND_NAMES = {
     "voice": _lib.KIND_VOICE,
     "chain": _lib.KIND_CHAIN,
     "fxrack": _lib.KIND_FXRACK,
+    "voice_moog": _lib.KIND_VOICE_MOOG,
 }
 
 # parameter field names, in C-ABI order
@@ -43,6 +44,7 @@ PARAMS = {
                        "reverb_balance", "filter_cutoff", "filter_resonance", "filter_drive", "filter_type",
                        "master_volume"],
 }
+PARAMS[_lib.KIND_VOICE_MOOG] = PARAMS[_lib.KIND_VOICE]
 PARAMS[_lib.KIND_CHAIN] = (["chorus_" + p for p in PARAMS[_lib.KIND_CHORUS]]
                            + ["pitch_" + p for p in PARAMS[_lib.KIND_PITCHSHIFT]]
                            + ["verb_" + p for p in PARAMS[_lib.KIND_DATTORRO]])

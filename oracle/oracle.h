@@ -61,6 +61,8 @@ enum {  /* Voice::Config order, modules/synthlib/Voice.h:14-31 */
 };
 typedef struct oracle_voice oracle_voice;
 oracle_voice *oracle_voice_create(int n_inst, float sample_rate);
+/* model 0: SvfFilter voice (SynthVoice default), 1: MoogFilter voice (daisysp::LadderFilter) */
+oracle_voice *oracle_voice_create_model(int n_inst, float sample_rate, int model);
 void oracle_voice_destroy(oracle_voice *o);
 int oracle_voice_config(oracle_voice *o, int inst, const float *values);
 int oracle_voice_note(oracle_voice *o, int inst, int on, int note);

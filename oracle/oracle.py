@@ -66,6 +66,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_chorus_process.argtypes = [ctypes.c_void_p, _PF, _PF, ctypes.c_int, ctypes.c_int]
         L.oracle_voice_create.restype = ctypes.c_void_p
         L.oracle_voice_create.argtypes = [ctypes.c_int, _F]
+        L.oracle_voice_create_model.restype = ctypes.c_void_p
+        L.oracle_voice_create_model.argtypes = [ctypes.c_int, _F, ctypes.c_int]
         L.oracle_voice_destroy.argtypes = [ctypes.c_void_p]
         L.oracle_voice_config.argtypes = [ctypes.c_void_p, ctypes.c_int, _PF]
         L.oracle_voice_note.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -193,10 +195,13 @@ class Chorus(_Bank):
 
 
 class Voice(_Bank):
-    def __init__(self, n: int, sample_rate: float = 48000.0):
+    """SynthVoice bank.  moog=False: SvfFilter voice (SynthVoice default); moog=True: MoogFilter
+    voice (daisysp::LadderFilter, the Daisy synth firmware's voice, main.cpp:49-52)."""
+
+    def __init__(self, n: int, sample_rate: float = 48000.0, moog: bool = False):
         self.n = n
         self.L = lib()
-        self.h = self.L.oracle_voice_create(n, sample_rate)
+        self.h = self.L.oracle_voice_create_model(n, sample_rate, int(bool(moog)))
         assert self.h
 
     def close(self):

@@ -12,7 +12,12 @@
  *   daisysp::Oscillator (WAVE_POLYBLEP_SAW, normalised phase, amp 0.5),
  *   daisysp::Adsr (Init(sr, 1), SetAttackTime(t, shape), SetTimeConstant, Process(gate), Retrigger),
  *   daisysp::Svf (double-sampled Chamberlin, SetFreq/SetRes/SetDrive, Low()),
- *   daisysp::mtof.
+ *   daisysp::mtof,
+ *   daisysp::LadderFilter (the MoogFilter voice of the Daisy synth firmware, Filter.h:35-63,
+ *   ol_daisy/app/synth/main.cpp:49-52): Huovilainen-style 4-pole ladder, 4x linear-interpolated
+ *   oversampling, Pade tanh on the feedback sum, one-zero/one-pole stages (0.3/1.3 zero), the
+ *   polynomial alpha/Qadjust fit of the normalised cutoff, LP24 output.  [unverified] against the
+ *   DaisySP source, like the rest of this file.
  * The only reference pins at this boundary are qualitative (synth_test.cpp:102-148: first sample
  * after NoteOn/NoteOff/NoteOn is exactly 0, later != 0 and != 1; amp_env_amount 0 -> 0) and are
  * reproduced by tests/test_oracle.py.
@@ -35,6 +40,9 @@ typedef struct {
     float phase, sr_recip;
     /* svf */
     float sr, fc_max, res, pre_drive, drive, low, band;
+    /* ladder (daisysp::LadderFilter, MoogFilter voices only) */
+    float lz0[4], lz1[4], l_old, alpha_scratch, l_k, l_pbg, l_drive_scaled, l_sr_int_recip;
+    int model;                      /* 0: SvfFilter (SynthVoice default), 1: MoogFilter */
     /* port */
     float port_coef, port_z;
     adsr_t amp_env, filt_env;
@@ -119,9 +127,70 @@ static float polyblep(float dt, float t)
 static float fclampf(float in, float mn, float mx) { return fminf(fmaxf(in, mn), mx); }
 #define MINF(a, b) ((a) < (b) ? (a) : (b))
 
-static void voice_init(voice_t *v, float sr)
+/* daisysp::LadderFilter::Init(sr): SetPassbandGain(0.5), SetInputDrive(0.5), SetFreq(5000),
+ * SetRes(0.2).  SetFreq is re-issued every sample by SynthVoice::Process, so only K, pbg and the
+ * input drive persist. */
+#define LADDER_OS 4
+static void ladder_init(voice_t *v, float sr)
+{
+    memset(v->lz0, 0, sizeof(v->lz0));
+    memset(v->lz1, 0, sizeof(v->lz1));
+    v->l_old = 0.f;
+    v->l_sr_int_recip = 1.0f / (sr * LADDER_OS);
+    v->l_pbg = 0.5f;
+    v->l_drive_scaled = 0.5f;           /* SetInputDrive(0.5): drive <= 1 -> drive_scaled = drive */
+    v->l_k = 4.0f * 0.2f;               /* SetRes(0.2) */
+}
+
+/* LadderFilter::SetRes: K = 4 * clamp(res, 0, kMaxResonance = 1.8) */
+static float ladder_k(float res) { return 4.0f * fminf(fmaxf(res, 0.0f), 1.8f); }
+
+/* Pade tanh, saturating at |x| > 3 */
+static float ladder_tanh(float x)
+{
+    if (x > 3.0f) return 1.0f;
+    if (x < -3.0f) return -1.0f;
+    const float x2 = x * x;
+    return x * (27.0f + x2) / (27.0f + 9.0f * x2);
+}
+
+static float ladder_lpf(voice_t *v, float s, int i)
+{
+    float ft = s * (1.0f / 1.3f) + (0.3f / 1.3f) * v->lz0[i] - v->lz1[i];
+    ft = ft * v->alpha_scratch + v->lz1[i];
+    v->lz1[i] = ft;
+    v->lz0[i] = s;
+    return ft;
+}
+
+/* LadderFilter::SetFreq(fc) -> SetAlpha, then LadderFilter::Process(in), LP24 */
+static float ladder_process(voice_t *v, float fc, float in)
+{
+    const float wc = fc * 2.0f * 3.1415927410125732f * v->l_sr_int_recip;
+    const float wc2 = wc * wc;
+    v->alpha_scratch = 0.9892f * wc - 0.4324f * wc2 + 0.1381f * wc * wc2 - 0.0202f * wc2 * wc2;
+    const float qadj = 1.006f + 0.0536f * wc - 0.095f * wc2 - 0.05f * wc2 * wc2;
+    const float input = in * v->l_drive_scaled;
+    float total = 0.0f, interp = 0.0f;
+    for (int os = 0; os < LADDER_OS; os++) {
+        float u = (interp * v->l_old + (1.0f - interp) * input) - (v->lz1[3] - v->l_pbg * input) * v->l_k * qadj;
+        u = ladder_tanh(u);
+        const float s1 = ladder_lpf(v, u, 0);
+        const float s2 = ladder_lpf(v, s1, 1);
+        const float s3 = ladder_lpf(v, s2, 2);
+        const float s4 = ladder_lpf(v, s3, 3);
+        total += s4 * (1.0f / LADDER_OS);
+        interp += 1.0f / LADDER_OS;
+    }
+    v->l_old = input;
+    return total;
+}
+
+static void voice_init(voice_t *v, float sr, int model)
 {
     memset(v, 0, sizeof(*v));
+    v->model = model;
+    ladder_init(v, sr);
     v->sr_recip = 1.0f / sr;                        /* Oscillator::Init */
     v->sr = sr; v->fc_max = sr / 3.f;               /* Svf::Init */
     v->res = 0.5f; v->pre_drive = 0.5f; v->drive = 0.5f;
@@ -139,6 +208,8 @@ static void voice_update(voice_t *v, const float *p, float sr)
     v->filter_cutoff = p[OVC_FILTER_CUTOFF];
     v->filter_env_amount = p[OVC_FILTER_ENV_AMOUNT];
     v->amp_env_amount = p[OVC_AMP_ENV_AMOUNT];
+    /* MoogFilter::SetRes -> LadderFilter::SetRes; MoogFilter::SetDrive is a no-op */
+    v->l_k = ladder_k(p[OVC_FILTER_RESONANCE]);
     /* Svf::SetRes, Svf::SetDrive */
     v->res = fclampf(p[OVC_FILTER_RESONANCE], 0.f, 1.f);
     v->drive = v->pre_drive * v->res;
@@ -169,8 +240,11 @@ static float voice_tick(voice_t *v)
     v->phase += inc;
     if (v->phase > 1.0f) v->phase -= 1.0f;
     const float src = o * 0.5f;
-    /* filter envelope -> Svf::SetFreq */
+    /* filter envelope -> Filter::SetFreq */
     const float fc_in = v->filter_cutoff + ((adsr_process(&v->filt_env, v->gate) * 20000) * v->filter_env_amount);
+    /* MoogFilter: Process() is a no-op, Low(frame) = LadderFilter::Process(frame); the frequency
+     * reaches SetAlpha unclamped */
+    if (v->model == 1) return ladder_process(v, fc_in, src) * amp;
     const float fc = fclampf(fc_in, 1.0e-6f, v->fc_max);
     const float fq = 2.0f * sinf(3.1415927410125732f * MINF(0.25f, fc / (v->sr * 2.0f)));
     const float damp = MINF(2.0f * (1.0f - powf(v->res, 0.25f)), MINF(2.0f, 2.0f / fq - fq * 0.5f));
@@ -190,7 +264,12 @@ static float voice_tick(voice_t *v)
 
 oracle_voice *oracle_voice_create(int n_inst, float sample_rate)
 {
-    if (n_inst <= 0) return NULL;
+    return oracle_voice_create_model(n_inst, sample_rate, 0);
+}
+
+oracle_voice *oracle_voice_create_model(int n_inst, float sample_rate, int model)
+{
+    if (n_inst <= 0 || model < 0 || model > 1) return NULL;
     oracle_voice *o = (oracle_voice *)calloc(1, sizeof(*o));
     if (!o) return NULL;
     o->n = n_inst;
@@ -198,7 +277,7 @@ oracle_voice *oracle_voice_create(int n_inst, float sample_rate)
     o->v = (voice_t *)calloc((size_t)n_inst, sizeof(voice_t));
     o->params = (float *)calloc((size_t)n_inst * OVC_NPARAMS, sizeof(float));
     if (!o->v || !o->params) { oracle_voice_destroy(o); return NULL; }
-    for (int i = 0; i < n_inst; i++) voice_init(&o->v[i], sample_rate);
+    for (int i = 0; i < n_inst; i++) voice_init(&o->v[i], sample_rate, model);
     return o;
 }
 

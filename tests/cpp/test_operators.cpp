@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "olfx_adapter.hpp"
 #include "olfx_fx.hpp"
 #include "../../oracle/oracle.h"
 
@@ -142,11 +143,12 @@ TEST(PitchShift, BankMatchesOracleBitExact) {
     oracle_chorus_destroy(ref);
 }
 
-/* SynthVoice Init / UpdateConfig / NoteOn / NoteOff / Process vs the DaisySP restatement. */
-TEST(Synth, VoiceBankMatchesOracle) {
+/* SynthVoice Init / UpdateConfig / NoteOn / NoteOff / Process vs the DaisySP restatement, for the
+   SvfFilter voice and the MoogFilter (daisysp::LadderFilter) voice. */
+static void voice_bank_matches_oracle(olfx::VoiceBank::Filter filter) {
     const uint32_t n = 96, half = 1024;
-    olfx::VoiceBank voices(n, 48000.f);
-    oracle_voice *ref = oracle_voice_create((int)n, 48000.f);
+    olfx::VoiceBank voices(n, 48000.f, 256, 0, filter);
+    oracle_voice *ref = oracle_voice_create_model((int)n, 48000.f, filter == olfx::VoiceBank::Filter::Moog);
     Lcg r(14);
     std::vector<uint8_t> notes(n);
     for (uint32_t i = 0; i < n; ++i) {
@@ -181,6 +183,10 @@ TEST(Synth, VoiceBankMatchesOracle) {
     }
     oracle_voice_destroy(ref);
 }
+
+TEST(Synth, VoiceBankMatchesOracle) { voice_bank_matches_oracle(olfx::VoiceBank::Filter::Svf); }
+
+TEST(Synth, MoogVoiceBankMatchesOracle) { voice_bank_matches_oracle(olfx::VoiceBank::Filter::Moog); }
 
 /* test/synth_test.cpp:102-148 pins: the first sample after NoteOn is exactly 0, and later
    samples are neither 0 nor 1. */
@@ -222,6 +228,46 @@ TEST(FxRack, MidiControlledRackMatchesOracle) {
 }
 
 /* Error behaviour: failures throw olfx::Error carrying the C-ABI code; nothing is silent. */
+/* The per-frame -> block adapter over the GPU rack, driven one frame at a time like the
+   workout_buddy AudioCallback, with a MIDI CC queued mid-block: equals the oracle run in blocks
+   with the CC applied at the block boundary, delayed by one block. */
+TEST(Adapter, PerFrameRackMatchesOracleDelayed) {
+    const uint32_t n = 24, B = 128, F = 1000;
+    olfx::FxRackBank rack(n, 48000.f, B);
+    olfx::BlockAdapter<olfx::FxRackBank> ad(rack, 2, 2, B);
+    oracle_fxrack *ref = oracle_fxrack_create((int)n, 48000.f);
+    std::vector<float> x = noise(2, F, n, 4242), ya(2 * (size_t)F * n), yd(ya.size());
+    std::vector<float> fi(2 * n), fo(2 * n);
+    for (uint32_t t = 0; t < F; ++t) {
+        if (t == 300) ad.QueueMidiControl(5, 45, 3);          // delay time -> short echo
+        for (uint32_t c = 0; c < 2; ++c) std::memcpy(&fi[c * n], &x[((size_t)c * F + t) * n], n * 4);
+        ad.ProcessFrame(fi.data(), fo.data());
+        for (uint32_t c = 0; c < 2; ++c) std::memcpy(&ya[((size_t)c * F + t) * n], &fo[c * n], n * 4);
+    }
+    // oracle: blocks of B, the CC mapped by the product's host map at the boundary of block 2
+    uint32_t done = 0;
+    yd = run_blocks([&](const float *xi, float *yo, uint32_t b) {
+        if (done == 2 * B) {
+            uint32_t field;
+            float v;
+            olfx_control_map(OLFX_KIND_FXRACK, 45, OLFX_CTL_MIDI, 3.f, &field, &v);
+            oracle_fxrack_set(ref, 5, (int)field, v);
+        }
+        oracle_fxrack_process(ref, xi, yo, (int)b, 4);
+        done += b;
+    }, x, 2, 2, F, n, B);
+    bool ok = true;
+    for (uint32_t c = 0; c < 2 && ok; ++c)
+        for (uint32_t t = 0; t < F && ok; ++t)
+            for (uint32_t i = 0; i < n && ok; ++i) {
+                const float a = ya[((size_t)c * F + t) * n + i];
+                const float d = t < B ? 0.f : yd[((size_t)c * F + t - B) * n + i];
+                ok = std::memcmp(&a, &d, 4) == 0;
+            }
+    EXPECT_TRUE(ok);
+    oracle_fxrack_destroy(ref);
+}
+
 TEST(Boundary, ErrorsThrowWithCode) {
     int code = 0;
     try { olfx::Engine bad(99, 4, 48000.f); } catch (const olfx::Error &e) { code = e.code(); }

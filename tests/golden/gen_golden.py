@@ -186,6 +186,22 @@ def main() -> None:
     gold["voice"] = {"n": nv, "frames": fv, "note_off_at": fv // 2, "notes": notes, "params": pv.tolist(),
                      "fnv1a64": [f"{O.fnv1a64_lr(yv[0, :, i], yv[0, :, i]):016x}" for i in range(nv)]}
 
+    # ---- MoogFilter voice (daisysp::LadderFilter restated): frozen spec-oracle vectors ----
+    rm = np.random.default_rng(97)
+    nm, fm = 5, 4800
+    pm = voice_configs(rm, nm)
+    notes_m = [int(v) for v in rm.integers(36, 97, nm)]
+    vm = O.Voice(nm, moog=True)
+    for i in range(nm):
+        vm.config(i, pm[:, i])
+        vm.note(i, True, notes_m[i])
+    ya = vm.process(fm // 2)
+    for i in range(nm):
+        vm.note(i, False, notes_m[i])
+    ym = np.concatenate([ya, vm.process(fm // 2)], axis=1)
+    gold["voice_moog"] = {"n": nm, "frames": fm, "note_off_at": fm // 2, "notes": notes_m, "params": pm.tolist(),
+                          "fnv1a64": [f"{O.fnv1a64_lr(ym[0, :, i], ym[0, :, i]):016x}" for i in range(nm)]}
+
     # ---- fx rack (FxRack<2>): frozen spec-oracle vectors, past the echo and the 48000 wrap ----
     nr, fr = 6, 60000
     pr = fxrack_params(np.random.default_rng(91), nr)

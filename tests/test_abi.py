@@ -65,6 +65,10 @@ def test_abi_version_and_kind_info():
     assert ch.state_bytes_per_instance == (2 * (512 + 2048) + 6 + 12) * 4
     vc = ofx.kind_info(ofx.KIND_VOICE)
     assert (vc.n_params, vc.in_channels, vc.out_channels) == (16, 0, 1)
+    assert vc.state_bytes_per_instance == (8 + 19) * 4
+    vm = ofx.kind_info(ofx.KIND_VOICE_MOOG)
+    assert (vm.n_params, vm.in_channels, vm.out_channels) == (16, 0, 1)
+    assert vm.state_bytes_per_instance == (8 + 9 + 19) * 4      # + LadderFilter z0_[4], z1_[4], oldinput_
     assert ofx.kind_info(ofx.KIND_CHAIN).n_params == 8 + 2 + 7
     fr = ofx.kind_info(ofx.KIND_FXRACK)
     assert fr.n_params == 11 and fr.in_channels == 2 and fr.out_channels == 2

@@ -10,6 +10,7 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 CPP = os.path.join(HERE, "cpp")
 BIN = os.path.join(CPP, "test_operators")
+ADAPTER_BIN = os.path.join(CPP, "test_adapter")
 
 
 def _build():
@@ -29,10 +30,21 @@ def test_cpp_operator_test_builds_and_fails_loudly_without_gpu():
     assert "no HIP device" in r.stdout and "(code -4)" in r.stdout
 
 
+def test_cpp_block_adapter_host_logic():
+    """include/olfx_adapter.hpp over CPU oracle banks: per-frame, ragged and
+    interleaved callers get the bank's output delayed by exactly one block, bit for bit; queued
+    CCs / notes land at the next block boundary in queue order; Queue() from a second thread."""
+    _build()
+    r = subprocess.run([ADAPTER_BIN], capture_output=True, text=True, timeout=120)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "4 tests, 0 failures" in r.stdout
+
+
 @pytest.mark.gpu
 def test_cpp_operators_on_gpu():
     _build()
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=600)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "7 tests, 0 failures" in r.stdout
+    assert "9 tests, 0 failures" in r.stdout

@@ -264,9 +264,9 @@ def test_chorus_full_size_properties(cuda):
 
 
 # ------------------------------------------------------------------------------------- voice
-def _voice_pair(n, cfg, notes, on=True):
-    e = engine("voice", n)
-    ref = O.Voice(n)
+def _voice_pair(n, cfg, notes, on=True, kind="voice"):
+    e = engine(kind, n)
+    ref = O.Voice(n, moog=kind == "voice_moog")
     if cfg is not None:
         e.set_params(0, cfg)
         for i in range(n):
@@ -286,12 +286,15 @@ def _voice_run(e, frames, cuda):
     return out.cpu().numpy()
 
 
-def test_voice_vs_oracle(cuda):
+@pytest.mark.parametrize("kind", ["voice", "voice_moog"])
+def test_voice_vs_oracle(cuda, kind):
+    """SvfFilter voice and MoogFilter (daisysp::LadderFilter) voice against the oracle, through a
+    NoteOn and a NoteOff."""
     n = 256
     rng = np.random.default_rng(21)
     cfg = voice_configs(rng, n)
     notes = [int(v) for v in rng.integers(36, 97, n)]
-    e, ref = _voice_pair(n, cfg, notes)
+    e, ref = _voice_pair(n, cfg, notes, kind=kind)
     ya = np.concatenate([_voice_run(e, 256, cuda) for _ in range(8)], 1)
     yra = ref.process(2048)
     e.note_events([(i, 0, notes[i]) for i in range(n)])
@@ -330,14 +333,46 @@ def test_voice_golden_and_pins(cuda, golden):
     assert v[1] != 0 and v[1] != 1
 
 
-def test_voice_unconfigured_defaults(cuda):
-    """Init without Update: DaisySP defaults in envelopes and Svf (SynthVoice.h:31-39)."""
+@pytest.mark.parametrize("kind", ["voice", "voice_moog"])
+def test_voice_unconfigured_defaults(cuda, kind):
+    """Init without Update: DaisySP defaults in envelopes and Svf / LadderFilter (SynthVoice.h:31-39)."""
     n = 4
     notes = [40, 60, 72, 90]
-    e, ref = _voice_pair(n, None, notes)
+    e, ref = _voice_pair(n, None, notes, kind=kind)
     y = np.concatenate([_voice_run(e, 512, cuda) for _ in range(4)], 1)
     yr = ref.process(2048)
     assert rel_err(y[0].T, yr[0].T) <= VOICE_TOL
+
+
+def test_voice_moog_golden_and_state_carry(cuda, golden):
+    """MoogFilter voices against the frozen fixture, in ragged blocks (the LadderFilter state and
+    oldinput_ carry across launches), plus the synth_test.cpp:102-148 first-sample pin."""
+    g = golden["voice_moog"]
+    p = np.asarray(g["params"], np.float32)
+    e, _ = _voice_pair(g["n"], p, g["notes"], kind="voice_moog")
+    parts, done = [], 0
+    for b in (4, 12, 60, 700, g["note_off_at"] - 776):     # olfx_process: multiples of 4
+        parts.append(_voice_run(e, b, cuda))
+        done += b
+    assert done == g["note_off_at"]
+    e.note_events([(i, 0, g["notes"][i]) for i in range(g["n"])])
+    parts.append(_voice_run(e, g["frames"] - g["note_off_at"], cuda))
+    y = np.concatenate(parts, 1)
+    vo = O.Voice(g["n"], moog=True)
+    for i in range(g["n"]):
+        vo.config(i, p[:, i])
+        vo.note(i, True, g["notes"][i])
+    yr = vo.process(g["note_off_at"])
+    for i in range(g["n"]):
+        vo.note(i, False, g["notes"][i])
+    yr = np.concatenate([yr, vo.process(g["frames"] - g["note_off_at"])], 1)
+    assert [f"{O.fnv1a64_lr(yr[0, :, i], yr[0, :, i]):016x}" for i in range(g["n"])] == g["fnv1a64"]
+    assert np.all(np.isfinite(y))
+    assert rel_err(y[0].T, yr[0].T) <= VOICE_TOL
+    e2 = engine("voice_moog", 1)
+    e2.note_events([(0, 1, 60)])
+    v = _voice_run(e2, 4, cuda)[0, :, 0]
+    assert v[0] == 0 and v[1] != 0 and v[1] != 1
 
 
 # ------------------------------------------------------------------------------------- chain

@@ -213,6 +213,56 @@ def test_voice_silent_until_note():
     assert np.all(vo.process(512) == 0)
 
 
+# ------------------------------------------- MoogFilter voice (daisysp::LadderFilter, unpinned)
+def _moog_run(cfg_edit=None, frames=4800, note=48):
+    vo = O.Voice(1, moog=True)
+    cfg = np.asarray(O.VOICE_DEFAULTS, np.float32)
+    cfg[O.VC_FIELDS.index("filter_env_amount")] = 0.0
+    for k, v in (cfg_edit or {}).items():
+        cfg[O.VC_FIELDS.index(k)] = v
+    vo.config(0, cfg)
+    vo.note(0, True, note)
+    return vo.process(frames)[0, :, 0]
+
+
+def test_voice_moog_frozen_golden(golden):
+    g = golden["voice_moog"]
+    p = np.asarray(g["params"], np.float32)
+    vo = O.Voice(g["n"], moog=True)
+    for i in range(g["n"]):
+        vo.config(i, p[:, i])
+        vo.note(i, True, g["notes"][i])
+    ya = vo.process(g["note_off_at"])
+    for i in range(g["n"]):
+        vo.note(i, False, g["notes"][i])
+    y = np.concatenate([ya, vo.process(g["frames"] - g["note_off_at"])], axis=1)
+    assert [f"{O.fnv1a64_lr(y[0, :, i], y[0, :, i]):016x}" for i in range(g["n"])] == g["fnv1a64"]
+
+
+def test_voice_moog_reference_pins_and_filter_semantics():
+    """synth_test.cpp:102-148 pins hold for the firmware's MoogFilter voice too; MoogFilter::SetDrive
+    is a no-op (Filter.h:47); the LP24 ladder attenuates a 1 kHz saw far more at 200 Hz than at 8 kHz; a
+    resonance past the clamp (K = 4 * 1.8) stays bounded through the tanh."""
+    vo = O.Voice(1, moog=True)
+    vo.note(0, True, 60)
+    vo.note(0, False, 60)
+    assert vo.process(1)[0, 0, 0] == 0
+    vo.note(0, True, 60)
+    v = vo.process(2)[0, :, 0]
+    assert v[-1] != 0 and v[-1] != 1
+    a = _moog_run({"filter_cutoff": 3000.0, "filter_drive": 0.0})
+    b = _moog_run({"filter_cutoff": 3000.0, "filter_drive": 9.0})
+    assert bits_equal(a, b)
+    lo = _moog_run({"filter_cutoff": 200.0, "filter_resonance": 0.0}, note=84)
+    hi = _moog_run({"filter_cutoff": 8000.0, "filter_resonance": 0.0}, note=84)
+    rms = lambda y: float(np.sqrt(np.mean(y[2400:].astype(np.float64) ** 2)))
+    assert rms(lo) < 0.25 * rms(hi)
+    r = _moog_run({"filter_cutoff": 1000.0, "filter_resonance": 5.0}, frames=48000)
+    assert np.all(np.isfinite(r)) and np.abs(r).max() < 4.0
+    assert not bits_equal(r, _moog_run({"filter_cutoff": 1000.0, "filter_resonance": 1.0}, frames=48000))
+    assert bits_equal(r, _moog_run({"filter_cutoff": 1000.0, "filter_resonance": 1.8}, frames=48000))
+
+
 # ------------------------------------------------------------------------------- fx rack
 def test_fxrack_defaults_and_echo():
     """FxRack<2> at its reference defaults (Fx.h): the delay echo arrives exactly
