@@ -24,30 +24,14 @@ namespace {
 
 enum { SEG_IDLE = 0, SEG_ATTACK = 1, SEG_DECAY = 2, SEG_RELEASE = 3 };
 
-// daisysp::Adsr::Process(gate), branch-free: every lane evaluates the segment step and selects
-// (same operations and order as the branchy form, so the same bits).
-__device__ __forceinline__ float adsr(bool gate, uint32_t &mode, bool &gprev, float &x, float atk_d0,
-                                      float atk_tgt, float dec_d0, float rel_d0, float sus) {
-    mode = (gate && !gprev) ? (uint32_t)SEG_ATTACK : ((!gate && gprev) ? (uint32_t)SEG_RELEASE : mode);
-    gprev = gate;
-    const bool atk = mode == SEG_ATTACK, dec = mode == SEG_DECAY, idle = mode == SEG_IDLE;
-    const float d0 = atk ? atk_d0 : (dec ? dec_d0 : rel_d0);
-    const float target = atk ? atk_tgt : (dec ? sus : -0.01f);
-    const float xn = x + d0 * (target - x);
-    const bool top = atk && xn > 1.f, bottom = !atk && xn < 0.0f;
-    const float out = idle ? 0.0f : (top ? 1.0f : (bottom ? 0.0f : xn));
-    x = idle ? x : out;
-    mode = top ? (uint32_t)SEG_DECAY : (bottom && !idle ? (uint32_t)SEG_IDLE : mode);
-    return out;
-}
-
 // polyBLEP residual with one division: t/dt near the wrap start, (t-1)/dt near its end -- the
 // same quotients as the two-branch form
 __device__ __forceinline__ float polyblep(float dt, float t) {
     const bool lo = t < dt, hi = !lo && t > 1.0f - dt;
     const float q = (lo ? t : t - 1.0f) * __builtin_amdgcn_rcpf(dt);   // v_rcp: ~1 ulp
-    const float rlo = q + q - q * q - 1.0f;
-    const float rhi = q * q + q + q + 1.0f;
+    float rlo = q + q - q * q - 1.0f;
+    float rhi = q * q + q + q + 1.0f;
+    asm volatile("" : "+v"(rlo), "+v"(rhi));      // both computed: selects, not an exec-mask diamond
     return lo ? rlo : (hi ? rhi : 0.0f);
 }
 
@@ -85,140 +69,251 @@ struct Ladder {
     float z0[4], z1[4], old;
 };
 
-// LadderFilter::SetFreq(fc) (SetAlpha) then Process(in), LP24
-__device__ __forceinline__ float ladder_process(Ladder &L, float fc, float in, float k, float drive_scaled,
-                                                float wrec) {
-    const float wc = fc * 2.0f * 3.1415927410125732f * wrec;
-    const float wc2 = wc * wc;
-    const float alpha = 0.9892f * wc - 0.4324f * wc2 + 0.1381f * wc * wc2 - 0.0202f * wc2 * wc2;
-    const float qadj = 1.006f + 0.0536f * wc - 0.095f * wc2 - 0.05f * wc2 * wc2;
-    const float input = in * drive_scaled;
-    float total = 0.0f, interp = 0.0f;
-#pragma unroll
-    for (int os = 0; os < 4; ++os) {
-        float u = (interp * L.old + (1.0f - interp) * input) - (L.z1[3] - 0.5f * input) * k * qadj;
-        u = ladder_tanh(u);
-        const float s1 = ladder_lpf(u, alpha, L.z0[0], L.z1[0]);
-        const float s2 = ladder_lpf(s1, alpha, L.z0[1], L.z1[1]);
-        const float s3 = ladder_lpf(s2, alpha, L.z0[2], L.z1[2]);
-        const float s4 = ladder_lpf(s3, alpha, L.z0[3], L.z1[3]);
-        total += s4 * (1.0f / 4);
-        interp += 1.0f / 4;
-    }
-    L.old = input;
-    return total;
-}
-
 }  // namespace
 
+// daisysp::Adsr as a segment machine.  The gate is constant inside a block (note events apply
+// between blocks), so the gate-edge test of Adsr::Process only fires on the block's first sample:
+// it is applied once in begin(), and each sample is the segment update x += d0 (target - x)
+// followed by the segment's clamp -- ATTACK ends above 1 (-> DECAY at x = 1), DECAY / RELEASE end
+// below 0 (-> IDLE at x = 0) -- which is v_med3(xn, lo, hi) with the segment's (lo, hi).  The
+// segment ends in a lane only a few times per note, so the parameter switch runs behind a
+// wave-uniform test.  IDLE is d0 = 0, target 0 and no bounds: x stays 0, Adsr's IDLE output (x is 0
+// whenever the envelope is idle: it enters IDLE at 0 and leaves only through Retrigger).
+struct Env {
+    float x, d0, tgt, hi, lo;
+    uint32_t mode;
+    float dec_d0, sus;
+
+    __device__ __forceinline__ void set_segment(uint32_t m, float atk_d0, float atk_tgt, float rel_d0) {
+        const float inf = __builtin_inff();
+        const bool atk = m == SEG_ATTACK, dcy = m == SEG_DECAY, rel = m == SEG_RELEASE;
+        mode = m;
+        d0 = atk ? atk_d0 : (dcy ? dec_d0 : (rel ? rel_d0 : 0.0f));
+        tgt = atk ? atk_tgt : (dcy ? sus : (rel ? -0.01f : 0.0f));
+        hi = atk ? 1.0f : inf;
+        lo = (dcy || rel) ? 0.0f : -inf;
+    }
+    __device__ __forceinline__ void begin(bool gate, bool &gprev, uint32_t m, float x0, float atk_d0, float atk_tgt,
+                                          float dec, float rel_d0, float s) {
+        m = (gate && !gprev) ? (uint32_t)SEG_ATTACK : ((!gate && gprev) ? (uint32_t)SEG_RELEASE : m);
+        gprev = gate;
+        x = x0;
+        dec_d0 = dec;
+        sus = s;
+        set_segment(m, atk_d0, atk_tgt, rel_d0);
+    }
+    __device__ __forceinline__ float step() {
+        const float xn = x + d0 * (tgt - x);
+        const bool ends = xn > hi || xn < lo;
+        x = __builtin_amdgcn_fmed3f(xn, lo, hi);
+        if (__builtin_amdgcn_ballot_w64(ends)) {       // rare, wave-uniform: a segment ended
+            // every lane evaluates the switch and keeps it only where its segment ended (selects,
+            // no exec-masked block)
+            const float inf = __builtin_inff();
+            const bool to_dcy = mode == SEG_ATTACK;
+            d0 = ends ? (to_dcy ? dec_d0 : 0.0f) : d0;
+            tgt = ends ? (to_dcy ? sus : 0.0f) : tgt;
+            hi = ends ? inf : hi;
+            lo = ends ? (to_dcy ? 0.0f : -inf) : lo;
+            mode = ends ? (to_dcy ? (uint32_t)SEG_DECAY : (uint32_t)SEG_IDLE) : mode;
+        }
+        return x;
+    }
+};
+
+constexpr int kVcChunk = 16;        // samples per producer -> filter hand-off
+
+// One workgroup = 64 voices, two waves: the producer wave runs the amp envelope, portamento,
+// oscillator and filter envelope (and, for the ladder, SetAlpha) and hands each sample's
+// filter inputs to the filter wave through an LDS double buffer; the filter wave runs the
+// filter recurrence and stores.  32,768 voices become 1,024 waves (one per SIMD) instead of 512.
 template <bool MOOG>
-__global__ __launch_bounds__(64) void voice_block_v2(VoiceArgs a) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
+__global__ __launch_bounds__(128) void voice_block_v3(VoiceArgs a) {
+    __shared__ float4 q[2][kVcChunk][64];
     const uint32_t n = a.n;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t i0 = blockIdx.x * 64 + lane;
+    const bool live = i0 < n;
+    const uint32_t i = live ? i0 : n - 1;          // clamped: dead lanes compute, never store
+    const uint32_t nf = a.n_frames;
+    const uint32_t nchunks = (nf + kVcChunk - 1) / kVcChunk;
     const float *c = a.coef;
-    const float atk_d0a = c[VCC_ATK_D0A * n + i], atk_tga = c[VCC_ATK_TGT_A * n + i];
-    const float dec_d0a = c[VCC_DEC_D0A * n + i], rel_d0a = c[VCC_REL_D0A * n + i], sus_a = c[VCC_SUS_A * n + i];
-    const float atk_d0f = c[VCC_ATK_D0F * n + i], atk_tgf = c[VCC_ATK_TGT_F * n + i];
-    const float dec_d0f = c[VCC_DEC_D0F * n + i], rel_d0f = c[VCC_REL_D0F * n + i], sus_f = c[VCC_SUS_F * n + i];
-    const float amp_amt = c[VCC_AMP_AMT * n + i], cutoff = c[VCC_CUTOFF * n + i], fenv_amt = c[VCC_FENV_AMT * n + i];
-    const float damp_res = c[VCC_DAMP_RES * n + i], drive = c[VCC_DRIVE * n + i];
-    const float port_c = c[VCC_PORT_COEF * n + i], fc_max = c[VCC_FC_MAX * n + i];
-    const float sr = c[VCC_SR * n + i], inv_sr = c[VCC_INV_SR * n + i];
-    const float inv_2sr = 1.0f / (sr * 2.0f);
-
     float *s = a.state;
-    float phase = s[VCS_PHASE * n + i];
-    float port_z = s[VCS_PORT_Z * n + i];
-    float xa = s[VCS_ENVA_X * n + i];
-    float xf = s[VCS_ENVF_X * n + i];
-    float low = s[VCS_LOW * n + i];
-    float band = s[VCS_BAND * n + i];
-    const float freq = s[VCS_FREQ * n + i];
-    uint32_t flags = __float_as_uint(s[VCS_FLAGS * n + i]);
-    uint32_t mode_a = flags & 7u, mode_f = (flags >> 3) & 7u;
-    bool gprev_a = (flags >> 6) & 1u, gprev_f = (flags >> 7) & 1u;
-    const bool gate = (flags >> 8) & 1u;
-    Ladder L;
-    if (MOOG) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            L.z0[k] = s[(VCS_LZ0 + k) * n + i];
-            L.z1[k] = s[(VCS_LZ1 + k) * n + i];
-        }
-        L.old = s[VCS_LOLD * n + i];
-    }
 
-#pragma unroll 2
-    for (uint32_t f = 0; f < a.n_frames; ++f) {
-        float amp = adsr(gate, mode_a, gprev_a, xa, atk_d0a, atk_tga, dec_d0a, rel_d0a, sus_a);
-        amp *= amp_amt;
-        // Port::Process (Portamento.h:218-221), Oscillator::SetFreq: phase_inc = f * sr_recip
-        port_z = freq + port_c * (port_z - freq);
-        const float inc = port_z * inv_sr;
-        // Oscillator::Process, WAVE_POLYBLEP_SAW
-        float o = (2.0f * phase) - 1.0f;
-        o -= polyblep(inc, phase);
-        o *= -1.0f;
-        phase += inc;
-        if (phase > 1.0f) phase -= 1.0f;
-        const float src = o * 0.5f;
-        // filter envelope -> Svf::SetFreq
-        const float fe = adsr(gate, mode_f, gprev_f, xf, atk_d0f, atk_tgf, dec_d0f, rel_d0f, sus_f);
-        const float fc_in = cutoff + ((fe * 20000.0f) * fenv_amt);
+    if (role == 0) {
+        // ---------------- producer: envelopes, portamento, oscillator ----------------
+        const float amp_amt = c[VCC_AMP_AMT * n + i], cutoff = c[VCC_CUTOFF * n + i];
+        const float fenv_amt = c[VCC_FENV_AMT * n + i], port_c = c[VCC_PORT_COEF * n + i];
+        const float inv_sr = c[VCC_INV_SR * n + i];
+        const float drive = c[VCC_DRIVE * n + i], wrec = c[VCC_FC_MAX * n + i];   // ladder: drive_scaled, 1/(4 sr)
+        float phase = s[VCS_PHASE * n + i];
+        float port_z = s[VCS_PORT_Z * n + i];
+        const float freq = s[VCS_FREQ * n + i];
+        uint32_t flags = __float_as_uint(s[VCS_FLAGS * n + i]);
+        bool gprev_a = (flags >> 6) & 1u, gprev_f = (flags >> 7) & 1u;
+        const bool gate = (flags >> 8) & 1u;
+        Env ea, ef;
+        ea.begin(gate, gprev_a, flags & 7u, s[VCS_ENVA_X * n + i], c[VCC_ATK_D0A * n + i], c[VCC_ATK_TGT_A * n + i],
+                 c[VCC_DEC_D0A * n + i], c[VCC_REL_D0A * n + i], c[VCC_SUS_A * n + i]);
+        ef.begin(gate, gprev_f, (flags >> 3) & 7u, s[VCS_ENVF_X * n + i], c[VCC_ATK_D0F * n + i],
+                 c[VCC_ATK_TGT_F * n + i], c[VCC_DEC_D0F * n + i], c[VCC_REL_D0F * n + i], c[VCC_SUS_F * n + i]);
+
+        for (uint32_t k = 0; k <= nchunks; ++k) {
+            if (k < nchunks) {
+                const uint32_t f0 = k * kVcChunk;
+                const uint32_t m = nf - f0 < (uint32_t)kVcChunk ? nf - f0 : (uint32_t)kVcChunk;
+                float4 *qb = &q[k & 1][0][lane];
+                auto sample = [&](uint32_t j) {
+                    const float amp = ea.step() * amp_amt;
+                    // Port::Process (Portamento.h:218-221), Oscillator::SetFreq: phase_inc = f * sr_recip
+                    port_z = freq + port_c * (port_z - freq);
+                    const float inc = port_z * inv_sr;
+                    // Oscillator::Process, WAVE_POLYBLEP_SAW
+                    float o = (2.0f * phase) - 1.0f;
+                    o -= polyblep(inc, phase);
+                    o *= -1.0f;
+                    phase += inc;
+                    phase = phase > 1.0f ? phase - 1.0f : phase;
+                    const float src = o * 0.5f;
+                    const float fe = ef.step();
+                    const float fc_in = cutoff + ((fe * 20000.0f) * fenv_amt);
+                    float4 v;
+                    if (MOOG) {
+                        // LadderFilter::SetFreq -> SetAlpha, and Process's input scaling
+                        const float wc = fc_in * 2.0f * 3.1415927410125732f * wrec;
+                        const float wc2 = wc * wc;
+                        v.x = src * drive;
+                        v.y = amp;
+                        v.z = 0.9892f * wc - 0.4324f * wc2 + 0.1381f * wc * wc2 - 0.0202f * wc2 * wc2;
+                        v.w = 1.006f + 0.0536f * wc - 0.095f * wc2 - 0.05f * wc2 * wc2;
+                    } else {
+                        v.x = src;
+                        v.y = amp;
+                        v.z = fc_in;
+                        v.w = 0.0f;
+                    }
+                    qb[j * 64] = v;
+                };
+                if (m == (uint32_t)kVcChunk) {   // full chunk: unrolled, so the off-recurrence work of
+                #pragma unroll                   // neighbouring samples interleaves (ILP for a lone wave)
+                    for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) sample(j);
+                } else {
+                    for (uint32_t j = 0; j < m; ++j) sample(j);
+                }
+            }
+            __syncthreads();
+        }
+        if (live) {
+            flags = ea.mode | (ef.mode << 3) | ((uint32_t)gprev_a << 6) | ((uint32_t)gprev_f << 7) |
+                    ((uint32_t)gate << 8);
+            s[VCS_PHASE * n + i] = phase;
+            s[VCS_PORT_Z * n + i] = port_z;
+            s[VCS_ENVA_X * n + i] = ea.x;
+            s[VCS_ENVF_X * n + i] = ef.x;
+            s[VCS_FLAGS * n + i] = __uint_as_float(flags);
+        }
+    } else {
+        // ---------------- filter: Svf (SetFreq + two passes) or LadderFilter ----------------
+        const float damp_res = c[VCC_DAMP_RES * n + i], drive = c[VCC_DRIVE * n + i];
+        const float fc_max = c[VCC_FC_MAX * n + i], sr = c[VCC_SR * n + i];
+        const float inv_2sr = 1.0f / (sr * 2.0f);
+        float low = 0.f, band = 0.f;
+        Ladder L;
         if (MOOG) {
-            // LadderFilter slots: VCC_LADDER_K = damp_res, VCC_LADDER_DRIVE = drive,
-            // VCC_LADDER_WREC = fc_max
-            a.out[(size_t)f * n + i] = ladder_process(L, fc_in, src, damp_res, drive, fc_max) * amp;
-            continue;
-        }
-        const float fc = fminf(fmaxf(fc_in, 1.0e-6f), fc_max);
-        // the three per-sample divisions of Svf::SetFreq / polyBLEP use the hardware reciprocal
-        // (~1 ulp; within the voice tolerance, like sin_quarter)
-        const float fcn = fc * inv_2sr;
-        const float arg = 0.25f < fcn ? 0.25f : fcn;
-        const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
-        const float lim = 2.0f * __builtin_amdgcn_rcpf(fq) - fq * 0.5f;
-        const float dlim = 2.0f < lim ? 2.0f : lim;
-        const float damp = damp_res < dlim ? damp_res : dlim;
-        // Svf::Process: two passes, Low() = average of the two low outputs
-        float notch = src - damp * band;
-        low = low + fq * band;
-        float high = notch - low;
-        band = fq * high + band - drive * band * band * band;
-        float out_low = 0.5f * low;
-        notch = src - damp * band;
-        low = low + fq * band;
-        high = notch - low;
-        band = fq * high + band - drive * band * band * band;
-        out_low += 0.5f * low;
-        a.out[(size_t)f * n + i] = out_low * amp;
-    }
-
-    flags = mode_a | (mode_f << 3) | ((uint32_t)gprev_a << 6) | ((uint32_t)gprev_f << 7) | ((uint32_t)gate << 8);
-    s[VCS_PHASE * n + i] = phase;
-    s[VCS_PORT_Z * n + i] = port_z;
-    s[VCS_ENVA_X * n + i] = xa;
-    s[VCS_ENVF_X * n + i] = xf;
-    s[VCS_LOW * n + i] = low;
-    s[VCS_BAND * n + i] = band;
-    s[VCS_FLAGS * n + i] = __uint_as_float(flags);
-    if (MOOG) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            s[(VCS_LZ0 + k) * n + i] = L.z0[k];
-            s[(VCS_LZ1 + k) * n + i] = L.z1[k];
+            for (int k = 0; k < 4; ++k) {
+                L.z0[k] = s[(VCS_LZ0 + k) * n + i];
+                L.z1[k] = s[(VCS_LZ1 + k) * n + i];
+            }
+            L.old = s[VCS_LOLD * n + i];
+        } else {
+            low = s[VCS_LOW * n + i];
+            band = s[VCS_BAND * n + i];
         }
-        s[VCS_LOLD * n + i] = L.old;
+        float *out = a.out + i;
+        for (uint32_t k = 0; k <= nchunks; ++k) {
+            if (k > 0) {
+                const uint32_t f0 = (k - 1) * kVcChunk;
+                const uint32_t m = nf - f0 < (uint32_t)kVcChunk ? nf - f0 : (uint32_t)kVcChunk;
+                const float4 *qb = &q[(k - 1) & 1][0][lane];
+                auto sample = [&](uint32_t j) {
+                    const float4 v = qb[j * 64];
+                    float y;
+                    if (MOOG) {
+                        // LadderFilter::Process, LP24; VCC_LADDER_K = damp_res
+                        const float input = v.x, alpha = v.z, qadj = v.w;
+                        float total = 0.0f, interp = 0.0f;
+#pragma unroll
+                        for (int os = 0; os < 4; ++os) {
+                            float u = (interp * L.old + (1.0f - interp) * input) -
+                                      (L.z1[3] - 0.5f * input) * damp_res * qadj;
+                            u = ladder_tanh(u);
+                            const float s1 = ladder_lpf(u, alpha, L.z0[0], L.z1[0]);
+                            const float s2 = ladder_lpf(s1, alpha, L.z0[1], L.z1[1]);
+                            const float s3 = ladder_lpf(s2, alpha, L.z0[2], L.z1[2]);
+                            const float s4 = ladder_lpf(s3, alpha, L.z0[3], L.z1[3]);
+                            total += s4 * (1.0f / 4);
+                            interp += 1.0f / 4;
+                        }
+                        L.old = input;
+                        y = total * v.y;
+                    } else {
+                        const float src = v.x;
+                        const float fc = fminf(fmaxf(v.z, 1.0e-6f), fc_max);
+                        // Svf::SetFreq; its divisions use the hardware reciprocal (~1 ulp, within the
+                        // voice tolerance, like sin_quarter)
+                        const float fcn = fc * inv_2sr;
+                        const float arg = 0.25f < fcn ? 0.25f : fcn;
+                        const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
+                        const float lim = 2.0f * __builtin_amdgcn_rcpf(fq) - fq * 0.5f;
+                        const float dlim = 2.0f < lim ? 2.0f : lim;
+                        const float damp = damp_res < dlim ? damp_res : dlim;
+                        // Svf::Process: two passes, Low() = average of the two low outputs
+                        float notch = src - damp * band;
+                        low = low + fq * band;
+                        float high = notch - low;
+                        band = fq * high + band - drive * band * band * band;
+                        float out_low = 0.5f * low;
+                        notch = src - damp * band;
+                        low = low + fq * band;
+                        high = notch - low;
+                        band = fq * high + band - drive * band * band * band;
+                        out_low += 0.5f * low;
+                        y = out_low * v.y;
+                    }
+                    out[(size_t)(f0 + j) * n] = y;
+                };
+                if (m == (uint32_t)kVcChunk) {   // full chunk: unrolled, so the off-recurrence work of
+                #pragma unroll                   // neighbouring samples interleaves (ILP for a lone wave)
+                    for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) sample(j);
+                } else {
+                    for (uint32_t j = 0; j < m; ++j) sample(j);
+                }
+            }
+            __syncthreads();
+        }
+        if (live) {
+            if (MOOG) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    s[(VCS_LZ0 + k) * n + i] = L.z0[k];
+                    s[(VCS_LZ1 + k) * n + i] = L.z1[k];
+                }
+                s[VCS_LOLD * n + i] = L.old;
+            } else {
+                s[VCS_LOW * n + i] = low;
+                s[VCS_BAND * n + i] = band;
+            }
+        }
     }
 }
 
 hipError_t launch_voice(const VoiceArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
-    const uint32_t threads = 64;       // one wave per workgroup: 32,768 voices spread over every CU
-    const dim3 grid((a.n + threads - 1) / threads);
-    if (a.moog) hipLaunchKernelGGL(voice_block_v2<true>, grid, dim3(threads), 0, s, a);
-    else hipLaunchKernelGGL(voice_block_v2<false>, grid, dim3(threads), 0, s, a);
+    const dim3 grid((a.n + 63) / 64);     // 64 voices per workgroup, a producer and a filter wave
+    if (a.moog) hipLaunchKernelGGL(voice_block_v3<true>, grid, dim3(128), 0, s, a);
+    else hipLaunchKernelGGL(voice_block_v3<false>, grid, dim3(128), 0, s, a);
     return hipGetLastError();
 }
 
