@@ -121,103 +121,143 @@ struct Env {
     }
 };
 
-constexpr int kVcChunk = 16;        // samples per producer -> filter hand-off
+constexpr int kVcChunk = 16;        // samples per hand-off between the roles
 
-// One workgroup = 64 voices, two waves: the producer wave runs the amp envelope, portamento,
-// oscillator and filter envelope (and, for the ladder, SetAlpha) and hands each sample's
-// filter inputs to the filter wave through an LDS double buffer; the filter wave runs the
-// filter recurrence and stores.  32,768 voices become 1,024 waves (one per SIMD) instead of 512.
+// Runs f(j) for the m samples of a chunk: unrolled when the chunk is full, so the off-recurrence
+// work of neighbouring samples interleaves (ILP for a wave that is alone on its SIMD).
+template <class F>
+__device__ __forceinline__ void for_chunk(uint32_t m, F &&f) {
+    if (m == (uint32_t)kVcChunk) {
+#pragma unroll
+        for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) f(j);
+    } else {
+        for (uint32_t j = 0; j < m; ++j) f(j);
+    }
+}
+
+// One workgroup = 64 voices, the voice pipelined over waves that hand each sample's values on
+// through an LDS double buffer (one barrier per 16-sample chunk):
+//   amp role    : amp envelope, portamento, oscillator          -> (src, amp)
+//   cutoff role : filter envelope, cutoff, Svf::SetFreq         -> (fq, damp)
+//                 (ladder: LadderFilter::SetFreq -> SetAlpha     -> (alpha, Qadjust))
+//   filter role : Svf passes / LadderFilter::Process, output store
+// Svf voices run the three roles on three waves (96 of them per 32 CUs' worth of voices, so
+// 32,768 voices occupy 1,536 waves); the ladder's serial recurrence dominates its voice, so the
+// amp and cutoff roles share one wave there (two waves per workgroup).
 template <bool MOOG>
-__global__ __launch_bounds__(128) void voice_block_v3(VoiceArgs a) {
+__global__ __launch_bounds__(MOOG ? 128 : 192) void voice_block_v4(VoiceArgs a) {
+    constexpr uint32_t kRoles = MOOG ? 2u : 3u;
     __shared__ float4 q[2][kVcChunk][64];
+    __shared__ uint32_t fflags[64];
     const uint32_t n = a.n;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t i0 = blockIdx.x * 64 + lane;
-    const bool live = i0 < n;
-    const uint32_t i = live ? i0 : n - 1;          // clamped: dead lanes compute, never store
+    // dead lanes of the last workgroup mirror voice n-1 exactly (same state, same coefficients),
+    // so their stores write the values voice n-1's lane writes
+    const uint32_t i = i0 < n ? i0 : n - 1;
     const uint32_t nf = a.n_frames;
     const uint32_t nchunks = (nf + kVcChunk - 1) / kVcChunk;
     const float *c = a.coef;
     float *s = a.state;
+    const bool filt_role = wave == kRoles - 1;
+    const uint32_t flags0 = __float_as_uint(s[VCS_FLAGS * n + i]);
+    const bool gate = (flags0 >> 8) & 1u;
 
-    if (role == 0) {
-        // ---------------- producer: envelopes, portamento, oscillator ----------------
-        const float amp_amt = c[VCC_AMP_AMT * n + i], cutoff = c[VCC_CUTOFF * n + i];
-        const float fenv_amt = c[VCC_FENV_AMT * n + i], port_c = c[VCC_PORT_COEF * n + i];
-        const float inv_sr = c[VCC_INV_SR * n + i];
-        const float drive = c[VCC_DRIVE * n + i], wrec = c[VCC_FC_MAX * n + i];   // ladder: drive_scaled, 1/(4 sr)
+    // ---------------- amp and/or cutoff roles (compile-time role flags: straight-line chunks) ----------------
+    auto feed = [&](auto amp_c, auto cut_c) {
+        constexpr bool AMP = decltype(amp_c)::value, CUT = decltype(cut_c)::value;
+        const float amp_amt = c[VCC_AMP_AMT * n + i], port_c = c[VCC_PORT_COEF * n + i];
+        const float inv_sr = c[VCC_INV_SR * n + i], freq = s[VCS_FREQ * n + i];
+        const float cutoff = c[VCC_CUTOFF * n + i], fenv_amt = c[VCC_FENV_AMT * n + i];
+        // Svf: damp_res, fc_max, 1/(2 sr); ladder: drive_scaled (VCC_DRIVE), 1/(4 sr) (VCC_FC_MAX)
+        const float damp_res = c[VCC_DAMP_RES * n + i], drive = c[VCC_DRIVE * n + i];
+        const float fc_max = c[VCC_FC_MAX * n + i], inv_2sr = 1.0f / (c[VCC_SR * n + i] * 2.0f);
         float phase = s[VCS_PHASE * n + i];
         float port_z = s[VCS_PORT_Z * n + i];
-        const float freq = s[VCS_FREQ * n + i];
-        uint32_t flags = __float_as_uint(s[VCS_FLAGS * n + i]);
-        bool gprev_a = (flags >> 6) & 1u, gprev_f = (flags >> 7) & 1u;
-        const bool gate = (flags >> 8) & 1u;
+        bool gprev_a = (flags0 >> 6) & 1u, gprev_f = (flags0 >> 7) & 1u;
         Env ea, ef;
-        ea.begin(gate, gprev_a, flags & 7u, s[VCS_ENVA_X * n + i], c[VCC_ATK_D0A * n + i], c[VCC_ATK_TGT_A * n + i],
-                 c[VCC_DEC_D0A * n + i], c[VCC_REL_D0A * n + i], c[VCC_SUS_A * n + i]);
-        ef.begin(gate, gprev_f, (flags >> 3) & 7u, s[VCS_ENVF_X * n + i], c[VCC_ATK_D0F * n + i],
-                 c[VCC_ATK_TGT_F * n + i], c[VCC_DEC_D0F * n + i], c[VCC_REL_D0F * n + i], c[VCC_SUS_F * n + i]);
+        if constexpr (AMP)
+            ea.begin(gate, gprev_a, flags0 & 7u, s[VCS_ENVA_X * n + i], c[VCC_ATK_D0A * n + i],
+                     c[VCC_ATK_TGT_A * n + i], c[VCC_DEC_D0A * n + i], c[VCC_REL_D0A * n + i], c[VCC_SUS_A * n + i]);
+        if constexpr (CUT)
+            ef.begin(gate, gprev_f, (flags0 >> 3) & 7u, s[VCS_ENVF_X * n + i], c[VCC_ATK_D0F * n + i],
+                     c[VCC_ATK_TGT_F * n + i], c[VCC_DEC_D0F * n + i], c[VCC_REL_D0F * n + i], c[VCC_SUS_F * n + i]);
 
         for (uint32_t k = 0; k <= nchunks; ++k) {
             if (k < nchunks) {
                 const uint32_t f0 = k * kVcChunk;
                 const uint32_t m = nf - f0 < (uint32_t)kVcChunk ? nf - f0 : (uint32_t)kVcChunk;
                 float4 *qb = &q[k & 1][0][lane];
-                auto sample = [&](uint32_t j) {
-                    const float amp = ea.step() * amp_amt;
-                    // Port::Process (Portamento.h:218-221), Oscillator::SetFreq: phase_inc = f * sr_recip
-                    port_z = freq + port_c * (port_z - freq);
-                    const float inc = port_z * inv_sr;
-                    // Oscillator::Process, WAVE_POLYBLEP_SAW
-                    float o = (2.0f * phase) - 1.0f;
-                    o -= polyblep(inc, phase);
-                    o *= -1.0f;
-                    phase += inc;
-                    phase = phase > 1.0f ? phase - 1.0f : phase;
-                    const float src = o * 0.5f;
-                    const float fe = ef.step();
-                    const float fc_in = cutoff + ((fe * 20000.0f) * fenv_amt);
-                    float4 v;
-                    if (MOOG) {
-                        // LadderFilter::SetFreq -> SetAlpha, and Process's input scaling
-                        const float wc = fc_in * 2.0f * 3.1415927410125732f * wrec;
-                        const float wc2 = wc * wc;
-                        v.x = src * drive;
-                        v.y = amp;
-                        v.z = 0.9892f * wc - 0.4324f * wc2 + 0.1381f * wc * wc2 - 0.0202f * wc2 * wc2;
-                        v.w = 1.006f + 0.0536f * wc - 0.095f * wc2 - 0.05f * wc2 * wc2;
-                    } else {
-                        v.x = src;
-                        v.y = amp;
-                        v.z = fc_in;
-                        v.w = 0.0f;
+                for_chunk(m, [&](uint32_t j) {
+                    float2 ab, cd;
+                    if constexpr (AMP) {
+                        const float amp = ea.step() * amp_amt;
+                        // Port::Process (Portamento.h:218-221), Oscillator::SetFreq: inc = f * sr_recip
+                        port_z = freq + port_c * (port_z - freq);
+                        const float inc = port_z * inv_sr;
+                        // Oscillator::Process, WAVE_POLYBLEP_SAW
+                        float o = (2.0f * phase) - 1.0f;
+                        o -= polyblep(inc, phase);
+                        o *= -1.0f;
+                        phase += inc;
+                        phase = phase > 1.0f ? phase - 1.0f : phase;
+                        const float src = o * 0.5f;
+                        ab = make_float2(MOOG ? src * drive : src, amp);   // ladder: Process's input scaling
                     }
-                    qb[j * 64] = v;
-                };
-                if (m == (uint32_t)kVcChunk) {   // full chunk: unrolled, so the off-recurrence work of
-                #pragma unroll                   // neighbouring samples interleaves (ILP for a lone wave)
-                    for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) sample(j);
-                } else {
-                    for (uint32_t j = 0; j < m; ++j) sample(j);
-                }
+                    if constexpr (CUT) {
+                        const float fe = ef.step();
+                        const float fc_in = cutoff + ((fe * 20000.0f) * fenv_amt);
+                        if (MOOG) {
+                            // LadderFilter::SetFreq (unclamped) -> SetAlpha
+                            const float wc = fc_in * 2.0f * 3.1415927410125732f * fc_max;
+                            const float wc2 = wc * wc;
+                            cd.x = 0.9892f * wc - 0.4324f * wc2 + 0.1381f * wc * wc2 - 0.0202f * wc2 * wc2;
+                            cd.y = 1.006f + 0.0536f * wc - 0.095f * wc2 - 0.05f * wc2 * wc2;
+                        } else {
+                            // Svf::SetFreq; its divisions use the hardware reciprocal (~1 ulp, within
+                            // the voice tolerance, like sin_quarter)
+                            const float fc = fminf(fmaxf(fc_in, 1.0e-6f), fc_max);
+                            const float fcn = fc * inv_2sr;
+                            const float arg = 0.25f < fcn ? 0.25f : fcn;
+                            const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
+                            const float lim = 2.0f * __builtin_amdgcn_rcpf(fq) - fq * 0.5f;
+                            const float dlim = 2.0f < lim ? 2.0f : lim;
+                            cd.x = fq;
+                            cd.y = damp_res < dlim ? damp_res : dlim;
+                        }
+                    }
+                    if constexpr (AMP && CUT) {
+                        qb[j * 64] = make_float4(ab.x, ab.y, cd.x, cd.y);
+                    } else if constexpr (AMP) {
+                        reinterpret_cast<float2 *>(&qb[j * 64])[0] = ab;
+                    } else {
+                        reinterpret_cast<float2 *>(&qb[j * 64])[1] = cd;
+                    }
+                });
             }
             __syncthreads();
         }
-        if (live) {
-            flags = ea.mode | (ef.mode << 3) | ((uint32_t)gprev_a << 6) | ((uint32_t)gprev_f << 7) |
-                    ((uint32_t)gate << 8);
+        // the flags word holds both envelopes: the cutoff role hands its bits to the amp role
+        if constexpr (CUT && !AMP) fflags[lane] = ef.mode << 3 | (uint32_t)gprev_f << 7;
+        __syncthreads();
+        if constexpr (AMP) {
+            const uint32_t fbits = CUT ? (ef.mode << 3 | (uint32_t)gprev_f << 7) : fflags[lane];
             s[VCS_PHASE * n + i] = phase;
             s[VCS_PORT_Z * n + i] = port_z;
             s[VCS_ENVA_X * n + i] = ea.x;
-            s[VCS_ENVF_X * n + i] = ef.x;
-            s[VCS_FLAGS * n + i] = __uint_as_float(flags);
+            s[VCS_FLAGS * n + i] = __uint_as_float(ea.mode | fbits | (uint32_t)gprev_a << 6 | (uint32_t)gate << 8);
         }
+        if constexpr (CUT) s[VCS_ENVF_X * n + i] = ef.x;
+    };
+    if (!filt_role) {
+        if (MOOG) feed(std::true_type{}, std::true_type{});
+        else if (wave == 0) feed(std::true_type{}, std::false_type{});
+        else feed(std::false_type{}, std::true_type{});
     } else {
-        // ---------------- filter: Svf (SetFreq + two passes) or LadderFilter ----------------
-        const float damp_res = c[VCC_DAMP_RES * n + i], drive = c[VCC_DRIVE * n + i];
-        const float fc_max = c[VCC_FC_MAX * n + i], sr = c[VCC_SR * n + i];
-        const float inv_2sr = 1.0f / (sr * 2.0f);
+        // ---------------- filter role: Svf passes or LadderFilter::Process ----------------
+        const float k_or_unused = c[VCC_DAMP_RES * n + i];     // ladder: K (VCC_LADDER_K)
+        const float drive = c[VCC_DRIVE * n + i];              // Svf drive
         float low = 0.f, band = 0.f;
         Ladder L;
         if (MOOG) {
@@ -237,17 +277,17 @@ __global__ __launch_bounds__(128) void voice_block_v3(VoiceArgs a) {
                 const uint32_t f0 = (k - 1) * kVcChunk;
                 const uint32_t m = nf - f0 < (uint32_t)kVcChunk ? nf - f0 : (uint32_t)kVcChunk;
                 const float4 *qb = &q[(k - 1) & 1][0][lane];
-                auto sample = [&](uint32_t j) {
+                for_chunk(m, [&](uint32_t j) {
                     const float4 v = qb[j * 64];
                     float y;
                     if (MOOG) {
-                        // LadderFilter::Process, LP24; VCC_LADDER_K = damp_res
+                        // LadderFilter::Process, LP24
                         const float input = v.x, alpha = v.z, qadj = v.w;
                         float total = 0.0f, interp = 0.0f;
 #pragma unroll
                         for (int os = 0; os < 4; ++os) {
                             float u = (interp * L.old + (1.0f - interp) * input) -
-                                      (L.z1[3] - 0.5f * input) * damp_res * qadj;
+                                      (L.z1[3] - 0.5f * input) * k_or_unused * qadj;
                             u = ladder_tanh(u);
                             const float s1 = ladder_lpf(u, alpha, L.z0[0], L.z1[0]);
                             const float s2 = ladder_lpf(s1, alpha, L.z0[1], L.z1[1]);
@@ -259,17 +299,8 @@ __global__ __launch_bounds__(128) void voice_block_v3(VoiceArgs a) {
                         L.old = input;
                         y = total * v.y;
                     } else {
-                        const float src = v.x;
-                        const float fc = fminf(fmaxf(v.z, 1.0e-6f), fc_max);
-                        // Svf::SetFreq; its divisions use the hardware reciprocal (~1 ulp, within the
-                        // voice tolerance, like sin_quarter)
-                        const float fcn = fc * inv_2sr;
-                        const float arg = 0.25f < fcn ? 0.25f : fcn;
-                        const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
-                        const float lim = 2.0f * __builtin_amdgcn_rcpf(fq) - fq * 0.5f;
-                        const float dlim = 2.0f < lim ? 2.0f : lim;
-                        const float damp = damp_res < dlim ? damp_res : dlim;
                         // Svf::Process: two passes, Low() = average of the two low outputs
+                        const float src = v.x, fq = v.z, damp = v.w;
                         float notch = src - damp * band;
                         low = low + fq * band;
                         float high = notch - low;
@@ -283,37 +314,30 @@ __global__ __launch_bounds__(128) void voice_block_v3(VoiceArgs a) {
                         y = out_low * v.y;
                     }
                     out[(size_t)(f0 + j) * n] = y;
-                };
-                if (m == (uint32_t)kVcChunk) {   // full chunk: unrolled, so the off-recurrence work of
-                #pragma unroll                   // neighbouring samples interleaves (ILP for a lone wave)
-                    for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) sample(j);
-                } else {
-                    for (uint32_t j = 0; j < m; ++j) sample(j);
-                }
+                });
             }
             __syncthreads();
         }
-        if (live) {
-            if (MOOG) {
+        __syncthreads();                                      // the flags hand-off barrier
+        if (MOOG) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    s[(VCS_LZ0 + k) * n + i] = L.z0[k];
-                    s[(VCS_LZ1 + k) * n + i] = L.z1[k];
-                }
-                s[VCS_LOLD * n + i] = L.old;
-            } else {
-                s[VCS_LOW * n + i] = low;
-                s[VCS_BAND * n + i] = band;
+            for (int k = 0; k < 4; ++k) {
+                s[(VCS_LZ0 + k) * n + i] = L.z0[k];
+                s[(VCS_LZ1 + k) * n + i] = L.z1[k];
             }
+            s[VCS_LOLD * n + i] = L.old;
+        } else {
+            s[VCS_LOW * n + i] = low;
+            s[VCS_BAND * n + i] = band;
         }
     }
 }
 
 hipError_t launch_voice(const VoiceArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
-    const dim3 grid((a.n + 63) / 64);     // 64 voices per workgroup, a producer and a filter wave
-    if (a.moog) hipLaunchKernelGGL(voice_block_v3<true>, grid, dim3(128), 0, s, a);
-    else hipLaunchKernelGGL(voice_block_v3<false>, grid, dim3(128), 0, s, a);
+    const dim3 grid((a.n + 63) / 64);     // 64 voices per workgroup, one wave per role
+    if (a.moog) hipLaunchKernelGGL(voice_block_v4<true>, grid, dim3(128), 0, s, a);
+    else hipLaunchKernelGGL(voice_block_v4<false>, grid, dim3(192), 0, s, a);
     return hipGetLastError();
 }
 
