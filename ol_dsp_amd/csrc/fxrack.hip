@@ -139,6 +139,25 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v1(FxRackArgs a) {
 #pragma unroll
     for (int k = 0; k < kFrChunk; ++k) x[k] = k < C ? ch::ld1(rIn, io_v, (uint32_t)k * frame_b) : 0.f;
     load_window(t00);
+    // A chunk's stores (ring run and outputs) are issued at the start of the NEXT chunk, ahead of
+    // that chunk's loads: the compiler drains vmcnt to 0 at the loop head (the loop carries
+    // in-flight loads), so every memory operation should be issued early in the iteration, where
+    // the whole chunk's arithmetic covers its latency -- not at the end, where the drain would
+    // expose the stores' round trip once per chunk.
+    float o[kFrChunk];
+    auto flush = [&](uint32_t fp, int Cp) {             // the stores of the chunk at frame fp
+        const uint32_t tp = t00 + fp;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t q = (uint32_t)r * 64u + lane, oo = q >> 3, f2 = 2u * (q & 7u);
+            const float4 vv = *(const float4 *)(stage + oo * kFrStride + 2u * f2);
+            const uint32_t oi = inst0 + oo;
+            if (oi < n && (int)f2 < Cp) ch::st4(rR, oo * kRing + wrap48k((int64_t)tp + f2) * 8u, vv);
+        }
+#pragma unroll
+        for (int k = 0; k < kFrChunk; ++k)
+            if (k < Cp) ch::st1(rOut, out_v, (fp + (uint32_t)k) * frame_b, o[k]);
+    };
     for (uint32_t f0 = 0; f0 < nf; f0 += kFrChunk) {
         C = (int)min((uint32_t)kFrChunk, nf - f0);
         const int Cn = f0 + kFrChunk < nf ? (int)min((uint32_t)kFrChunk, nf - f0 - kFrChunk) : 0;
@@ -154,6 +173,7 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v1(FxRackArgs a) {
                 if (s >= 0 && s < kFrWin) wcol[s * 64] = y[k];
             }
         }
+        if (f0 > 0) flush(f0 - kFrChunk, kFrChunk);     // the previous chunk was full
         // ---- 2. the next chunk's inputs and window in flight (unconditional) ----
 #pragma unroll
         for (int k = 0; k < kFrChunk; ++k) {
@@ -181,8 +201,7 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v1(FxRackArgs a) {
             const float b0 = (vb * rbal) + (a0 * (1 - rbal));
             // FilterFx filter1 on channel 0; channel 1 of buf_c stays 0
             const float c = svf_tick(b0, ffreq, fdamp, fdrive, ftype, flow, fband);
-            const float o = (ch == 0 ? c : 0.0f) * master;
-            ch::st1(rOut, out_v, (f0 + (uint32_t)k) * frame_b, o);
+            o[k] = (ch == 0 ? c : 0.0f) * master;
         };
         if (C == kFrChunk) {
 #pragma unroll
@@ -191,21 +210,19 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v1(FxRackArgs a) {
 #pragma unroll
             for (int k = 0; k < kFrChunk; ++k) frame(std::true_type{}, k);
         }
-        // ---- 4. the chunk's writes -> ring (staged [instance][frame][ch], 8 lanes per 128 B) ----
+        // ---- 4. the chunk's writes -> LDS staging ([instance][frame][ch]); they leave as 128-B
+        //         runs (8 lanes each) with the next chunk's flush ----
         {
             float *st = stage + j * kFrStride + ch;
 #pragma unroll
             for (int k = 0; k < kFrChunk; ++k) st[2 * k] = y[k];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint32_t q = (uint32_t)r * 64u + lane, o = q >> 3, f2 = 2u * (q & 7u);
-                const float4 vv = *(const float4 *)(stage + o * kFrStride + 2u * f2);
-                const uint32_t oi = inst0 + o;
-                if (oi < n && (int)f2 < C) ch::st4(rR, o * kRing + wrap48k((int64_t)t + f2) * 8u, vv);
-            }
         }
 #pragma unroll
         for (int k = 0; k < kFrChunk; ++k) x[k] = xn[k];
+    }
+    {
+        const uint32_t fl = (nf - 1u) / kFrChunk * kFrChunk;   // the last chunk
+        flush(fl, (int)(nf - fl));
     }
     if (!valid || ch != 0) return;
     a.state[FRS_DLOW * n + i] = __float_as_uint(dlow);
