@@ -105,6 +105,28 @@ SIGNATURES = {
     "olfx_algorithmic_bytes_per_frame": (ctypes.c_double, [_P]),
     "olfx_kernel_name": (ctypes.c_char_p, [_P]),
     "olfx_last_error": (ctypes.c_char_p, [_P]),
+    # include/olfx_dattorro.h: pool control of the verb.h-compatible names
+    "olfx_dattorro_pool_config": (ctypes.c_int, [ctypes.c_int, _U32]),
+    "olfx_dattorro_latency": (_U32, [_P]),
+    "olfx_dattorro_generation_size": (_U32, [_P]),
+    "olfx_dattorro_index": (_U32, [_P]),
+}
+
+# include/olfx_dattorro.h: libs/dattorro-verb/verb.h:5-26 by name (C linkage; libolfx.so also
+# exports the C++-mangled twins the reference's own callers link to)
+DATTORRO_SIGNATURES = {
+    "DattorroVerb_create": (_P, []),
+    "DattorroVerb_delete": (None, [_P]),
+    "DattorroVerb_setPreDelay": (None, [_P, _F]),
+    "DattorroVerb_setPreFilter": (None, [_P, _F]),
+    "DattorroVerb_setInputDiffusion1": (None, [_P, _F]),
+    "DattorroVerb_setInputDiffusion2": (None, [_P, _F]),
+    "DattorroVerb_setDecayDiffusion": (None, [_P, _F]),
+    "DattorroVerb_setDecay": (None, [_P, _F]),
+    "DattorroVerb_setDamping": (None, [_P, _F]),
+    "DattorroVerb_process": (None, [_P, _F]),
+    "DattorroVerb_getLeft": (_F, [_P]),
+    "DattorroVerb_getRight": (_F, [_P]),
 }
 
 _lib = None
@@ -120,7 +142,7 @@ def load() -> ctypes.CDLL:
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(make -C ol_dsp_amd/csrc).  There is no CPU fallback.")
     lib = ctypes.CDLL(LIB_PATH)
-    for name, (res, args) in SIGNATURES.items():
+    for name, (res, args) in list(SIGNATURES.items()) + list(DATTORRO_SIGNATURES.items()):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
