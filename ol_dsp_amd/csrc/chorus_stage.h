@@ -47,20 +47,30 @@ __device__ __forceinline__ Rsrc rsrc(const void *p, uint64_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0,
                                              (int)(uint32_t)(bytes > 0xFFFFFFFFull ? 0xFFFFFFFFull : bytes), 0x00020000);
 }
+// cache policy of the streamed accesses (block input/output, ring stores): 0 = default,
+// 2 = nt (gfx950 aux bit 1).  A/B knob; the shipped value is measured.
+#ifndef OLFX_STREAM_AUX
+#define OLFX_STREAM_AUX 0
+#endif
+constexpr int kStreamAux = OLFX_STREAM_AUX;
+
+template <int AUX = 0>
 __device__ __forceinline__ float ld1(Rsrc r, uint32_t voff, uint32_t soff) {
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, AUX));
 }
+template <int AUX = 0>
 __device__ __forceinline__ void st1(Rsrc r, uint32_t voff, uint32_t soff, float v) {
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, AUX);
 }
 __device__ __forceinline__ float4 ld4(Rsrc r, uint32_t voff) {
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
+template <int AUX = 0>
 __device__ __forceinline__ void st4(Rsrc r, uint32_t voff, float4 v) {
     u32x4 u;
     u.x = __float_as_uint(v.x); u.y = __float_as_uint(v.y); u.z = __float_as_uint(v.z); u.w = __float_as_uint(v.w);
-    __builtin_amdgcn_raw_buffer_store_b128(u, r, voff, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u, r, voff, 0, AUX);
 }
 
 // exchange a value with the neighbouring lane (lanes 2j <-> 2j+1): DPP quad_perm [1,0,3,2]
@@ -239,8 +249,8 @@ struct ChStage {
             const float4 v = *(const float4 *)(region + base + o * kStride + 2u * f2);
             const uint32_t oi = inst0 + o;
             if (oi < n && (int)f2 < C) {
-                if (pitch) st4(rP, oi * pstride + ((w + f2) & pmask) * 8u, v);
-                else st4(rC, oi * cstride + ((w + f2) & cmask) * 8u, v);
+                if (pitch) st4<kStreamAux>(rP, oi * pstride + ((w + f2) & pmask) * 8u, v);
+                else st4<kStreamAux>(rC, oi * cstride + ((w + f2) & cmask) * 8u, v);
             }
         }
     }

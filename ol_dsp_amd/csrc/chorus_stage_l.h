@@ -1,0 +1,381 @@
+// ol_dsp_amd/csrc/chorus_stage_l.h -- the chorus / pitch-shifter stage with LINE CARRY (v11).
+//
+// Same spec, lane mapping, LDS window layout and per-frame recurrence as chorus_stage.h (v10); what
+// changes is how the windows get from HBM into LDS.  v10 fetched, for every tap of every chunk, a
+// fresh 24-position window (192 B at a 32-B aligned start: 2.25 128-B lines on average).  Each
+// 128-B line was therefore fetched by two consecutive chunks, and the L2 cannot keep it between
+// them (about 10 MB of other traffic passes through an XCD's 4 MB L2 in one chunk time), so the
+// taps cost 18 B/frame each against the 8 B/frame they read (profiles/traffic_chorus.json).
+//
+// v11 holds, per tap and instance, the two aligned lines L', L'+1 (L' = line of the window start)
+// in REGISTERS, cooperatively spread over the wave (8 lanes x 16 B per line, 4 parts of 8
+// instances): 3 taps x 2 lines x 4 float4 = 96 VGPRs.  A tap's window advances about one line per
+// chunk, so the line L'+1 of chunk c is the line L' of chunk c+1: each chunk loads only the new
+// line (the "hi" load, unconditional) and carries the other.  The two line sets alternate roles by
+// chunk parity (template PAR), so every register index is static.
+//
+// A carried line was loaded two chunks before its use; positions the kernel wrote after that load
+// are stale in it.  Carrying is therefore allowed only when the whole window lies far enough
+// behind the write head (floor delay >= kCarryMin* over the chunk, derivation in DESIGN.md
+// section 4) and the window advanced by exactly one line; otherwise the chunk is FRESH and also
+// reloads L' (the "lo" load, exec-masked so a carried line is never clobbered).  Fresh windows
+// have exactly v10's staleness (this chunk's inputs, the previous chunk's pitch-shifter outputs),
+// patched from registers as in v10.
+//
+// The chorus tap can span 18 positions (its delay may fall by one inside a chunk); when such a
+// window starts at the last position of a line, its highest position lies in line L'+2: that one
+// position per lane ("straggler") is loaded directly (4 B, own channel, exec-masked) and staged.
+#pragma once
+#include "chorus_stage.h"
+
+namespace olfx {
+namespace ch {
+
+constexpr int kCarryMinPitch = 32;    // pitch ring: carried line stored through w_c - 1
+constexpr int kCarryMinChorus = 48;   // chorus ring: carried line stored through w_c - 17
+
+struct PlanL {
+    int sA, sB, sC;           // window starts relative to the chunk's first write position (4-aligned)
+    int dA, dB, dC;           // minimum floor delay of any frame of the chunk
+    int hiC;                  // highest chorus-window position (relative)
+    bool okA, okB;
+};
+
+template <int kWin>
+__device__ __forceinline__ PlanL plan_chunk_l(uint32_t lfo_acc, uint32_t lfo_inc, uint32_t lfo_off, uint32_t ps_acc,
+                                              uint32_t ps_inc, int C, float D, float W, float pmax, float cmax,
+                                              bool full) {
+    PlanL p;
+    const uint32_t last = (uint32_t)(C - 1);
+    // pitch taps: the floor delay is non-decreasing over the chunk unless the phasor wraps
+    {
+        const uint32_t a0 = ps_acc, a1 = ps_acc + last * ps_inc;
+        const int d0 = floor_delay(unit24(a0) * W, 1.0f, pmax), d1 = floor_delay(unit24(a1) * W, 1.0f, pmax);
+        const int lo = -d1 - 1, hi = (int)last - d0;
+        p.sA = lo & ~3;
+        p.dA = d0;
+        p.okA = a1 >= a0 && hi - p.sA < kWin;
+    }
+    {
+        const uint32_t a0 = ps_acc + 0x80000000u, a1 = a0 + last * ps_inc;
+        const int d0 = floor_delay(unit24(a0) * W, 1.0f, pmax), d1 = floor_delay(unit24(a1) * W, 1.0f, pmax);
+        const int lo = -d1 - 1, hi = (int)last - d0;
+        p.sB = lo & ~3;
+        p.dB = d0;
+        p.okB = a1 >= a0 && hi - p.sB < kWin;
+    }
+    // chorus tap: the endpoint delays are computed exactly as the frames compute theirs; in between
+    // the delay stays within [min, max] of them up to the curvature of the LFO over 16 frames
+    // (< 1e-3 for every legal depth and rate), so floor(min - .01) .. floor(max + .01) bounds every
+    // frame's floor delay, and those two differ by at most one (|d'| <= 0.038 frame/frame)
+    p.sC = 0; p.dC = 0; p.hiC = 0;
+    if (full) {
+        const float e0 = cos2pi(unit24(lfo_acc + lfo_off)) * D + D;
+        const float e1 = cos2pi(unit24(lfo_acc + last * lfo_inc + lfo_off)) * D + D;
+        const int dhi = floor_delay(fmaxf(e0, e1) + 0.01f, 0.0f, cmax);
+        const int dlo = floor_delay(fminf(e0, e1) - 0.01f, 0.0f, cmax);
+        p.sC = (-dhi - 1) & ~3;
+        p.dC = dlo;
+        p.hiC = (int)last - dlo;
+    }
+    return p;
+}
+
+template <bool FULL>
+struct ChStageL {
+    static constexpr int kChunk = 16, kWin = 24, kSlots = kWin + 1;
+    static constexpr int kRegion = 3 * kSlots * kRow;   // floats of LDS per wave (4,800), as v10
+    static constexpr int kStride = 36;
+    static constexpr uint32_t kPsvBase = 32u * kStride;
+    static constexpr int kTaps = FULL ? 3 : 2;
+    static_assert(2 * 32 * kStride <= kRegion, "staging must fit in the window region");
+
+    uint32_t lane, j, ch, inst0, n, i;
+    bool valid;
+    uint32_t lfo_inc, lfo_off, ps_inc;
+    float D, W, b0, b1, b2, a1, a2, mix, dry;
+    uint32_t lfo_acc, ps_acc;
+    float z1, z2;
+    uint32_t pmask, cmask, pstride, cstride, own_pb, own_cb;
+    float pmax, cmax;
+    Rsrc rP, rC;
+    float *region;
+    float4 ln[3][2][4];       // [tap][line set][part]: piece (lane & 7) of a line of instance part*8 + lane/8
+    uint32_t s15;             // window start & 15 per (tap, part), 2 bits each (start is 4-aligned)
+    float strag;              // chorus straggler (own channel)
+    uint32_t strag_slot;      // its LDS slot (kWin = junk)
+    uint32_t lcur[3];         // owner: line L' of the current chunk's window, per tap
+    PlanL pl;
+    float psv[kChunk];
+    uint32_t wpos;
+    bool started;
+
+    __device__ __forceinline__ void init(const ChorusArgs &a, float *lds_region, uint32_t lane_, uint32_t inst0_) {
+        lane = lane_; j = lane >> 1; ch = lane & 1u; inst0 = inst0_; n = a.n;
+        const uint32_t i_raw = inst0 + j;
+        valid = i_raw < n;
+        i = valid ? i_raw : n - 1;
+        lfo_inc = a.coef[CHC_LFO_INC * n + i];
+        lfo_off = a.coef[CHC_LFO_OFF * n + i];
+        ps_inc = a.coef[CHC_PS_INC * n + i];
+        D = __uint_as_float(a.coef[CHC_DEPTH * n + i]);
+        W = __uint_as_float(a.coef[CHC_WINDOW * n + i]);
+        b0 = __uint_as_float(a.coef[CHC_B0 * n + i]);
+        b1 = __uint_as_float(a.coef[CHC_B1 * n + i]);
+        b2 = __uint_as_float(a.coef[CHC_B2 * n + i]);
+        a1 = __uint_as_float(a.coef[CHC_A1 * n + i]);
+        a2 = __uint_as_float(a.coef[CHC_A2 * n + i]);
+        mix = __uint_as_float(a.coef[CHC_MIX * n + i]);
+        dry = __uint_as_float(a.coef[CHC_DRY * n + i]);
+        lfo_acc = a.state[CHS_LFO_ACC * n + i];
+        ps_acc = a.state[CHS_PS_ACC * n + i];
+        z1 = __uint_as_float(a.state[(ch ? CHS_Z1R : CHS_Z1L) * n + i]);
+        z2 = __uint_as_float(a.state[(ch ? CHS_Z2R : CHS_Z2L) * n + i]);
+        pmask = a.psize - 1u; cmask = a.csize - 1u;
+        pmax = (float)(a.psize - 2u); cmax = (float)(a.csize - 2u);
+        rP = rsrc(a.pitch_ring, (uint64_t)n * 2 * a.psize * 4);
+        rC = rsrc(a.chorus_ring, (uint64_t)n * 2 * a.csize * 4);
+        pstride = a.psize * 8u; cstride = a.csize * 8u;
+        own_pb = i * pstride + ch * 4u;
+        own_cb = i * cstride + ch * 4u;
+        region = lds_region;
+        wpos = a.t0;
+        started = false;
+        s15 = 0;
+        strag = 0.f;
+        strag_slot = kWin;
+    }
+
+    // cooperative line geometry: part r (0..3) -> instance r*8 + lane/8, piece lane & 7
+    __device__ __forceinline__ uint32_t pjj(int r) const { return (uint32_t)r * 8u + (lane >> 3); }
+    __device__ __forceinline__ uint32_t pm() const { return lane & 7u; }
+
+    __device__ __forceinline__ uint32_t line_off(int t, uint32_t oi, uint32_t q) const {
+        const uint32_t pos = q * 16u + 2u * pm();
+        return t < 2 ? oi * pstride + (pos & pmask) * 8u : oi * cstride + (pos & cmask) * 8u;
+    }
+    __device__ __forceinline__ float4 ld_line(int t, uint32_t off) const { return ld4(t < 2 ? rP : rC, off); }
+
+    // Issue the line loads for the chunk whose plan is p and first write position w.  Owner lanes
+    // decide (carry / fresh) and publish per instance, through ds_bpermute, the packed value
+    // (window start relative to w) * 2 | fresh.  Lines go into set HI (the new line L'+1) and, for
+    // fresh instances only, set LO (L').
+    template <int HI>
+    __device__ __forceinline__ void load_lines(const PlanL &p, uint32_t w, bool first) {
+        constexpr int LO = HI ^ 1;
+        const int s[3] = {p.sA, p.sB, p.sC};
+        const int dmin[3] = {p.dA, p.dB, p.dC};
+        const int thr[3] = {kCarryMinPitch, kCarryMinPitch, kCarryMinChorus};
+        uint32_t s15n = 0;
+        int pk[3];
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t) {
+            const uint32_t lnext = (w + (uint32_t)s[t]) >> 4;
+            const bool carry = !first && lnext == lcur[t] + 1u && dmin[t] >= thr[t];
+            lcur[t] = lnext;
+            pk[t] = (int)((uint32_t)s[t] << 1) | (carry ? 0 : 1);
+        }
+        // all exchanges first (one LDS round trip), then the loads
+        int v[3][4];
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[t][r] = __builtin_amdgcn_ds_bpermute((int)(pjj(r) << 3), pk[t]);
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t jj = pjj(r);
+                const uint32_t sabs = w + (uint32_t)(v[t][r] >> 1);
+                const uint32_t q = sabs >> 4;
+                const uint32_t oi = min(inst0 + jj, n - 1);
+                s15n |= ((sabs & 15u) >> 2) << (2 * (t * 4 + r));
+                ln[t][HI][r] = ld_line(t, line_off(t, oi, q + 1u));
+                if (v[t][r] & 1) ln[t][LO][r] = ld_line(t, line_off(t, oi, q));
+            }
+        }
+        s15 = s15n;
+        // chorus straggler: a window of 18 positions starting at a line's last position
+        strag_slot = kWin;
+        if (FULL) {
+            const uint32_t top = (lcur[2] << 4) + 32u;           // first position past the two lines
+            const bool need = (w + (uint32_t)p.hiC) == top;
+            strag_slot = need ? top - ((w + (uint32_t)p.sC)) : (uint32_t)kWin;
+            if (need) strag = ld1(rC, own_cb + (top & cmask) * 8u, 0);
+        }
+    }
+
+    // lines -> the chunk's LDS windows ([tap][slot][lane], slot = position - window start)
+    template <int HI>
+    __device__ __forceinline__ void stage_lines() {
+        constexpr int LO = HI ^ 1;
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t) {
+            float *base = region + t * kSlots * kRow;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t jj = pjj(r);
+                const int st = (int)(((s15 >> (2 * (t * 4 + r))) & 3u) << 2);
+                const int slo = 2 * (int)pm() - st;          // line L' piece
+                const int shi = slo + 16;                     // line L'+1 piece
+                const int ulo = slo >= 0 ? slo : kWin;        // kWin = junk (pieces are 2 slots; the junk slot
+                const int uhi = shi < kWin ? shi : kWin;      //  row has 2 x 64 floats of room: see kRegion)
+                float *plo = base + ulo * kRow + 2 * jj;
+                float *phi = base + uhi * kRow + 2 * jj;
+                const float4 a = ln[t][LO][r], b = ln[t][HI][r];
+                *(float2 *)plo = make_float2(a.x, a.y);
+                *(float2 *)(plo + (ulo == kWin ? 0 : kRow)) = make_float2(a.z, a.w);
+                *(float2 *)phi = make_float2(b.x, b.y);
+                *(float2 *)(phi + (uhi == kWin ? 0 : kRow)) = make_float2(b.z, b.w);
+            }
+        }
+        if (FULL) region[2 * kSlots * kRow + strag_slot * kRow + lane] = strag;
+    }
+
+    __device__ __forceinline__ void stage_run(const float (&v)[kChunk], uint32_t base) {
+        float *st = region + base + j * kStride + ch;
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k) st[2 * k] = v[k];
+    }
+    __device__ __forceinline__ void coop_store(bool pitch, uint32_t base, uint32_t w, int C) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t q = (uint32_t)r * 64u + lane, o = q >> 3, f2 = 2u * (q & 7u);
+            const float4 v = *(const float4 *)(region + base + o * kStride + 2u * f2);
+            const uint32_t oi = inst0 + o;
+            if (oi < n && (int)f2 < C) {
+                if (pitch) st4<kStreamAux>(rP, oi * pstride + ((w + f2) & pmask) * 8u, v);
+                else st4<kStreamAux>(rC, oi * cstride + ((w + f2) & cmask) * 8u, v);
+            }
+        }
+    }
+
+    // first chunk of the launch: store its inputs, then load both lines of every window (fresh)
+    __device__ __forceinline__ void begin(const float (&x)[kChunk], int C) {
+        stage_run(x, 0);
+        coop_store(true, 0, wpos, C);
+        pl = plan_chunk_l<kWin>(lfo_acc, lfo_inc, lfo_off, ps_acc, ps_inc, C, D, W, pmax, cmax, FULL);
+        load_lines<0>(pl, wpos, true);
+    }
+
+    // One chunk; PAR = chunk parity (the line set holding this chunk's line L'+1).
+    template <int PAR, class Sink>
+    __device__ __forceinline__ void chunk(const float (&x)[kChunk], int C, int Cn, Sink &&sink) {
+        const uint32_t w0 = wpos;
+        const PlanL cur = pl;
+        float *wP0 = region + 0 * kSlots * kRow + lane;
+        float *wP1 = region + 1 * kSlots * kRow + lane;
+        float *wC = region + 2 * kSlots * kRow + lane;
+
+        if (started) {
+            stage_run(x, 0);
+            coop_store(true, 0, w0, C);
+        }
+        stage_lines<PAR>();
+        if (started) {
+            if (cur.sA > -kWin) {
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k)
+                    if (k < C && k - cur.sA < kWin) wP0[(k - cur.sA) * kRow] = x[k];
+            }
+            if (cur.sB > -kWin) {
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k)
+                    if (k < C && k - cur.sB < kWin) wP1[(k - cur.sB) * kRow] = x[k];
+            }
+            if (FULL && cur.sC > -kWin - kChunk) {
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) {
+                    const int jw = k - kChunk - cur.sC;
+                    if (jw >= 0 && jw < kWin) wC[jw * kRow] = psv[k];
+                }
+            }
+        }
+        started = true;
+
+        pl = plan_chunk_l<kWin>(lfo_acc + (uint32_t)C * lfo_inc, lfo_inc, lfo_off, ps_acc + (uint32_t)C * ps_inc,
+                                ps_inc, Cn > 0 ? Cn : 4, D, W, pmax, cmax, FULL);
+        load_lines<PAR ^ 1>(pl, w0 + kChunk, false);
+
+        float pl_lfo[2], pl_gA[2], pl_gB[2];
+        auto frame = [&](auto generic_tag, int k) {
+            constexpr bool GENERIC = decltype(generic_tag)::value;
+            if ((k & 1) == 0) {
+                const uint32_t la = lfo_acc + ch * lfo_inc, pa = ps_acc + ch * ps_inc;
+                const float m_lfo = cos2pi(unit24(la + lfo_off));
+                const float m_gA = cos2pi((unit24(pa) - 0.5f) * 0.5f);
+                const float m_gB = cos2pi((unit24(pa + 0x80000000u) - 0.5f) * 0.5f);
+                const float o_lfo = swap_pair(m_lfo), o_gA = swap_pair(m_gA), o_gB = swap_pair(m_gB);
+                pl_lfo[0] = ch ? o_lfo : m_lfo; pl_lfo[1] = ch ? m_lfo : o_lfo;
+                pl_gA[0] = ch ? o_gA : m_gA;    pl_gA[1] = ch ? m_gA : o_gA;
+                pl_gB[0] = ch ? o_gB : m_gB;    pl_gB[1] = ch ? m_gB : o_gB;
+            }
+            if (GENERIC && k >= C) { psv[k] = 0.f; return; }
+            const float lfo = pl_lfo[k & 1];
+            const float dch = lfo * D + D;
+            const float p0 = unit24(ps_acc);
+            const float p1 = unit24(ps_acc + 0x80000000u);
+            const float gA = pl_gA[k & 1];
+            const float gB = pl_gB[k & 1];
+            lfo_acc += lfo_inc;
+            ps_acc += ps_inc;
+            int di; float fr;
+            float tA, tB;
+            split_delay(p0 * W, 1.0f, pmax, di, fr);
+            if (GENERIC && !cur.okA) {
+                const uint32_t q = w0 + k - di;
+                tA = lerp_pair(ld1(rP, own_pb + (q & pmask) * 8u, 0), ld1(rP, own_pb + ((q - 1u) & pmask) * 8u, 0), fr);
+            } else {
+                const int jw = k - di - cur.sA;
+                tA = lerp_pair(wP0[jw * kRow], wP0[(jw - 1) * kRow], fr);
+            }
+            split_delay(p1 * W, 1.0f, pmax, di, fr);
+            if (GENERIC && !cur.okB) {
+                const uint32_t q = w0 + k - di;
+                tB = lerp_pair(ld1(rP, own_pb + (q & pmask) * 8u, 0), ld1(rP, own_pb + ((q - 1u) & pmask) * 8u, 0), fr);
+            } else {
+                const int jw = k - di - cur.sB;
+                tB = lerp_pair(wP1[jw * kRow], wP1[(jw - 1) * kRow], fr);
+            }
+            const float p = tB * gB + tA * gA;
+            psv[k] = p;
+            float out = p;
+            if (FULL) {
+                wC[min(k - cur.sC, kWin) * kRow] = p;
+                split_delay(dch, 0.0f, cmax, di, fr);
+                const int jw = k - di - cur.sC;
+                const float wet = lerp_pair(wC[jw * kRow], wC[(jw - 1) * kRow], fr);
+                const float lp = b0 * wet + z1;
+                z1 = (b1 * wet - a1 * lp) + z2;
+                z2 = b2 * wet - a2 * lp;
+                out = x[k] * dry + lp * mix;
+            }
+            sink(k, out);
+        };
+        if (C == kChunk && __all(cur.okA && cur.okB)) {
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) frame(std::false_type{}, k);
+        } else {
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) frame(std::true_type{}, k);
+        }
+        if (FULL) {
+            stage_run(psv, kPsvBase);
+            coop_store(false, kPsvBase, w0, C);
+        }
+        wpos = w0 + (uint32_t)C;
+    }
+
+    __device__ __forceinline__ void finish(const ChorusArgs &a) const {
+        if (!valid) return;
+        if (ch == 0) {
+            a.state[CHS_LFO_ACC * n + i] = lfo_acc;
+            a.state[CHS_PS_ACC * n + i] = ps_acc;
+        }
+        a.state[(ch ? CHS_Z1R : CHS_Z1L) * n + i] = __float_as_uint(z1);
+        a.state[(ch ? CHS_Z2R : CHS_Z2L) * n + i] = __float_as_uint(z2);
+    }
+};
+
+}  // namespace ch
+}  // namespace olfx

@@ -1034,7 +1034,7 @@ const char *olfx_kernel_name(const olfx_engine *e) {
     switch (e->kind) {
     case OLFX_KIND_DATTORRO: return "dattorro_block_v4";
     case OLFX_KIND_CHORUS:
-    case OLFX_KIND_PITCHSHIFT: return "chorus_block_v10";
+    case OLFX_KIND_PITCHSHIFT: return OLFX_CHORUS_V == 11 ? "chorus_block_v11" : "chorus_block_v10";
     case OLFX_KIND_VOICE: return "voice_block_v4";
     case OLFX_KIND_VOICE_MOOG: return "voice_block_v4<true>";
     case OLFX_KIND_CHAIN: return "chain_block_v1";

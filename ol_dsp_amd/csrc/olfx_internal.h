@@ -11,6 +11,12 @@
 
 #define OLFX_HD __host__ __device__ __forceinline__
 
+// chorus / pitch-shift kernel generation: 11 = line carry (chorus_stage_l.h), 10 = per-chunk
+// windows (chorus_stage.h).  A build knob for A/B timing (tools/ab.sh).
+#ifndef OLFX_CHORUS_V
+#define OLFX_CHORUS_V 11
+#endif
+
 namespace olfx {
 
 // ----------------------------------------------------------------------------------------------

@@ -226,6 +226,39 @@ def test_chorus_vs_oracle(cuda, n):
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
 
+@pytest.mark.parametrize("kind", ["chorus", "pitchshift"])
+def test_chorus_line_carry_stress(cuda, kind):
+    """Extreme depth/rate/pitch/window corners over 64 blocks: every tap window mode (carried
+    line, fresh reload, chorus straggler, pitch-phasor wrap) occurs many times; bit-exact."""
+    n, frames = 96, 256 * 64
+    rng = np.random.default_rng(77)
+    p = np.empty((8, n), np.float32)
+    p[0] = rng.choice([0.0, 0.01, 1.0, 2.5, 3.0], n)      # pitch (phasor Hz)
+    p[1] = rng.uniform(0, 1, n)                            # mix
+    p[2] = rng.uniform(0, 0.95, n)                         # q
+    p[3] = rng.uniform(0, 1, n)                            # cutoff
+    p[4] = rng.uniform(0, 1, n)                            # phase
+    p[5] = rng.choice([0.08, 0.2, 1.0], n)                 # depth
+    p[6] = rng.choice([0.01, 0.5, 1.0], n)                 # rate
+    p[7] = rng.choice([4.0, 7.3, 10.0], n)                 # window ms
+    x = fast_noise(n, frames, seed=9)
+    e = engine(kind, n)
+    ref = O.Chorus(n, mode=0 if kind == "chorus" else 1)
+    if kind == "chorus":
+        e.set_params(0, p)
+        for i in range(n):
+            for f in range(8):
+                ref.set(i, f, float(p[f, i]))
+    else:
+        e.set_params(0, p[[0, 7]])
+        for i in range(n):
+            ref.set(i, "pitch", float(p[0, i]))
+            ref.set(i, "window", float(p[7, i]))
+    y = run_gpu(e, x, [256] * 64, cuda)
+    yr = ref.process(x, threads=8)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
 def test_chorus_defaults_and_edges(cuda):
     """RNBO defaults, params clamped to @min/@max (out-of-range values), mix 0 == dry."""
     n = 5
