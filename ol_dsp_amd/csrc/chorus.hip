@@ -78,13 +78,18 @@ __global__ __launch_bounds__(ch::kThreads, 2) void chorus_block_v11(ChorusArgs a
     auto step = [&](auto par, uint32_t f0) {
         C = (int)min((uint32_t)kChunk, nf - f0);
         const int Cn = f0 + kChunk < nf ? (int)min((uint32_t)kChunk, nf - f0 - kChunk) : 0;
+        // the next chunk's input (unconditional loads, the frame clamped into the block; lanes
+        // past Cn get 0), issued by the stage once this chunk's stores and staging are out
+        auto prefetch = [&]() {
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k) {
-            const float v = ch::ld1<ch::kStreamAux>(rIn, io_v, min(f0 + kChunk + (uint32_t)k, nf - 1u) * frame_b);
-            xn[k] = k < Cn ? v : 0.f;
-        }
+            for (int k = 0; k < kChunk; ++k) {
+                const float v = ch::ld1<ch::kStreamAux>(rIn, io_v, min(f0 + kChunk + (uint32_t)k, nf - 1u) * frame_b);
+                xn[k] = k < Cn ? v : 0.f;
+            }
+        };
         st.template chunk<decltype(par)::value>(
-            x, C, Cn, [&](int k, float v) { ch::st1<ch::kStreamAux>(rOut, out_v, (f0 + (uint32_t)k) * frame_b, v); });
+            x, xn, C, Cn,
+            [&](int k, float v) { ch::st1<ch::kStreamAux>(rOut, out_v, (f0 + (uint32_t)k) * frame_b, v); }, prefetch);
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) x[k] = xn[k];
     };

@@ -14,13 +14,15 @@
 // line (the "hi" load, unconditional) and carries the other.  The two line sets alternate roles by
 // chunk parity (template PAR), so every register index is static.
 //
-// A carried line was loaded two chunks before its use; positions the kernel wrote after that load
-// are stale in it.  Carrying is therefore allowed only when the whole window lies far enough
-// behind the write head (floor delay >= kCarryMin* over the chunk, derivation in DESIGN.md
-// section 4) and the window advanced by exactly one line; otherwise the chunk is FRESH and also
-// reloads L' (the "lo" load, exec-masked so a carried line is never clobbered).  Fresh windows
-// have exactly v10's staleness (this chunk's inputs, the previous chunk's pitch-shifter outputs),
-// patched from registers as in v10.
+// A carried line was loaded during the chunk before the previous one; positions written since are
+// stale in it.  Each chunk therefore writes its pitch-shifter outputs (psv_c) and the NEXT chunk's
+// inputs (x_{c+1}, prefetched) to the rings BEFORE it issues the next chunk's line loads, so a
+// freshly loaded line holds everything up to the next chunk's own frames, and a carried line
+// lacks only x_c and psv_{c-1}: both are still at hand (x_c in registers, psv_{c-1} in its LDS
+// staging) and are patched into the windows, for every delay.  The chunk's pitch-shifter runs
+// before those stores and line loads, the chorus tap after them, as the loads' cover.  A window
+// that did not advance by exactly one line (or the first chunk of a launch) is FRESH: it also
+// reloads L' (the "lo" load, exec-masked, so a carried line is never clobbered).
 //
 // The chorus tap can span 18 positions (its delay may fall by one inside a chunk); when such a
 // window starts at the last position of a line, its highest position lies in line L'+2: that one
@@ -28,15 +30,40 @@
 #pragma once
 #include "chorus_stage.h"
 
+
 namespace olfx {
 namespace ch {
 
-constexpr int kCarryMinPitch = 32;    // pitch ring: carried line stored through w_c - 1
-constexpr int kCarryMinChorus = 48;   // chorus ring: carried line stored through w_c - 17
+// cos(2 pi x) for |x| <= 0.25: cos2pi() (olfx_internal.h) with its range reduction folded away.
+// There u = x - rint(x) = x, a = |x| <= 0.25 never takes the reflected branch, and
+// (x 2pi)^2 == (|x| 2pi)^2 exactly: bit-identical results, six fewer instructions.
+__device__ __forceinline__ float cos2pi_q(float x) {
+    const float th = x * 6.28318530717958647692f;
+    const float t2 = th * th;
+    return 1.0f + t2 * (-0.5f + t2 * (4.16666666666666666667e-2f +
+           t2 * (-1.38888888888888888889e-3f + t2 * (2.48015873015873015873e-5f +
+           t2 * (-2.75573192239858906526e-7f + t2 * (2.08767569878680989792e-9f +
+           t2 * (-1.14707455977297247139e-11f)))))));
+}
+// a value of lane 2j (EVEN) or 2j+1 (odd) to both lanes of the pair: DPP quad_perm [0,0,2,2] / [1,1,3,3]
+__device__ __forceinline__ float pair_even(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xA0, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float pair_odd(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xF5, 0xF, 0xF, false));
+}
+// split_delay with the clamp as one v_med3 (identical to fminf(fmaxf()) for non-NaN delays,
+// and delays here are phasor arithmetic, never NaN)
+__device__ __forceinline__ void split_delay3(float d, float dmin, float dmax, int &di, float &fr) {
+    d = __builtin_amdgcn_fmed3f(d, dmin, dmax);
+    const uint32_t u = (uint32_t)d;
+    di = (int)u;
+    fr = d - (float)u;
+}
+
 
 struct PlanL {
     int sA, sB, sC;           // window starts relative to the chunk's first write position (4-aligned)
-    int dA, dB, dC;           // minimum floor delay of any frame of the chunk
     int hiC;                  // highest chorus-window position (relative)
     bool okA, okB;
 };
@@ -53,7 +80,6 @@ __device__ __forceinline__ PlanL plan_chunk_l(uint32_t lfo_acc, uint32_t lfo_inc
         const int d0 = floor_delay(unit24(a0) * W, 1.0f, pmax), d1 = floor_delay(unit24(a1) * W, 1.0f, pmax);
         const int lo = -d1 - 1, hi = (int)last - d0;
         p.sA = lo & ~3;
-        p.dA = d0;
         p.okA = a1 >= a0 && hi - p.sA < kWin;
     }
     {
@@ -61,21 +87,19 @@ __device__ __forceinline__ PlanL plan_chunk_l(uint32_t lfo_acc, uint32_t lfo_inc
         const int d0 = floor_delay(unit24(a0) * W, 1.0f, pmax), d1 = floor_delay(unit24(a1) * W, 1.0f, pmax);
         const int lo = -d1 - 1, hi = (int)last - d0;
         p.sB = lo & ~3;
-        p.dB = d0;
         p.okB = a1 >= a0 && hi - p.sB < kWin;
     }
     // chorus tap: the endpoint delays are computed exactly as the frames compute theirs; in between
     // the delay stays within [min, max] of them up to the curvature of the LFO over 16 frames
     // (< 1e-3 for every legal depth and rate), so floor(min - .01) .. floor(max + .01) bounds every
     // frame's floor delay, and those two differ by at most one (|d'| <= 0.038 frame/frame)
-    p.sC = 0; p.dC = 0; p.hiC = 0;
+    p.sC = 0; p.hiC = 0;
     if (full) {
         const float e0 = cos2pi(unit24(lfo_acc + lfo_off)) * D + D;
         const float e1 = cos2pi(unit24(lfo_acc + last * lfo_inc + lfo_off)) * D + D;
         const int dhi = floor_delay(fmaxf(e0, e1) + 0.01f, 0.0f, cmax);
         const int dlo = floor_delay(fminf(e0, e1) - 0.01f, 0.0f, cmax);
         p.sC = (-dhi - 1) & ~3;
-        p.dC = dlo;
         p.hiC = (int)last - dlo;
     }
     return p;
@@ -96,7 +120,7 @@ struct ChStageL {
     float D, W, b0, b1, b2, a1, a2, mix, dry;
     uint32_t lfo_acc, ps_acc;
     float z1, z2;
-    uint32_t pmask, cmask, pstride, cstride, own_pb, own_cb;
+    uint32_t pmask, cmask, pstride, cstride;
     float pmax, cmax;
     Rsrc rP, rC;
     float *region;
@@ -106,7 +130,6 @@ struct ChStageL {
     uint32_t strag_slot;      // its LDS slot (kWin = junk)
     uint32_t lcur[3];         // owner: line L' of the current chunk's window, per tap
     PlanL pl;
-    float psv[kChunk];
     uint32_t wpos;
     bool started;
 
@@ -136,8 +159,6 @@ struct ChStageL {
         rP = rsrc(a.pitch_ring, (uint64_t)n * 2 * a.psize * 4);
         rC = rsrc(a.chorus_ring, (uint64_t)n * 2 * a.csize * 4);
         pstride = a.psize * 8u; cstride = a.csize * 8u;
-        own_pb = i * pstride + ch * 4u;
-        own_cb = i * cstride + ch * 4u;
         region = lds_region;
         wpos = a.t0;
         started = false;
@@ -145,6 +166,18 @@ struct ChStageL {
         strag = 0.f;
         strag_slot = kWin;
     }
+
+    // this lane's samples in its rings, recomputed where used.  The empty asm makes the lane index
+    // look loop-variant: otherwise the loop-invariant products are hoisted, spilled under the
+    // register pressure of the carried lines, and every reload (a scratch load) costs a
+    // vmcnt(0) drain of the whole prefetch.
+    __device__ __forceinline__ uint32_t own_i() const {
+        uint32_t l = lane;
+        asm volatile("" : "+v"(l));
+        return min(inst0 + (l >> 1), n - 1u);
+    }
+    __device__ __forceinline__ uint32_t own_pb() const { return own_i() * pstride + (lane & 1u) * 4u; }
+    __device__ __forceinline__ uint32_t own_cb() const { return own_i() * cstride + (lane & 1u) * 4u; }
 
     // cooperative line geometry: part r (0..3) -> instance r*8 + lane/8, piece lane & 7
     __device__ __forceinline__ uint32_t pjj(int r) const { return (uint32_t)r * 8u + (lane >> 3); }
@@ -164,14 +197,16 @@ struct ChStageL {
     __device__ __forceinline__ void load_lines(const PlanL &p, uint32_t w, bool first) {
         constexpr int LO = HI ^ 1;
         const int s[3] = {p.sA, p.sB, p.sC};
-        const int dmin[3] = {p.dA, p.dB, p.dC};
-        const int thr[3] = {kCarryMinPitch, kCarryMinPitch, kCarryMinChorus};
         uint32_t s15n = 0;
         int pk[3];
 #pragma unroll
         for (int t = 0; t < kTaps; ++t) {
             const uint32_t lnext = (w + (uint32_t)s[t]) >> 4;
-            const bool carry = !first && lnext == lcur[t] + 1u && dmin[t] >= thr[t];
+#ifdef OLFX_V11_FRESH
+            const bool carry = ((OLFX_V11_FRESH >> t) & 1) == 0 && !first && lnext == lcur[t] + 1u;   // debug: reload taps in mask
+#else
+            const bool carry = !first && lnext == lcur[t] + 1u;
+#endif
             lcur[t] = lnext;
             pk[t] = (int)((uint32_t)s[t] << 1) | (carry ? 0 : 1);
         }
@@ -201,35 +236,36 @@ struct ChStageL {
             const uint32_t top = (lcur[2] << 4) + 32u;           // first position past the two lines
             const bool need = (w + (uint32_t)p.hiC) == top;
             strag_slot = need ? top - ((w + (uint32_t)p.sC)) : (uint32_t)kWin;
-            if (need) strag = ld1(rC, own_cb + (top & cmask) * 8u, 0);
+            if (need) strag = ld1(rC, own_cb() + (top & cmask) * 8u, 0);
         }
     }
 
-    // lines -> the chunk's LDS windows ([tap][slot][lane], slot = position - window start)
-    template <int HI>
-    __device__ __forceinline__ void stage_lines() {
+    // lines of tap t -> the chunk's LDS window ([tap][slot][lane], slot = position - window start)
+    template <int HI, int t>
+    __device__ __forceinline__ void stage_tap() {
         constexpr int LO = HI ^ 1;
+        float *base = region + t * kSlots * kRow;
 #pragma unroll
-        for (int t = 0; t < kTaps; ++t) {
-            float *base = region + t * kSlots * kRow;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint32_t jj = pjj(r);
-                const int st = (int)(((s15 >> (2 * (t * 4 + r))) & 3u) << 2);
-                const int slo = 2 * (int)pm() - st;          // line L' piece
-                const int shi = slo + 16;                     // line L'+1 piece
-                const int ulo = slo >= 0 ? slo : kWin;        // kWin = junk (pieces are 2 slots; the junk slot
-                const int uhi = shi < kWin ? shi : kWin;      //  row has 2 x 64 floats of room: see kRegion)
-                float *plo = base + ulo * kRow + 2 * jj;
-                float *phi = base + uhi * kRow + 2 * jj;
-                const float4 a = ln[t][LO][r], b = ln[t][HI][r];
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t jj = pjj(r);
+            const int st = (int)(((s15 >> (2 * (t * 4 + r))) & 3u) << 2);
+            const int slo = 2 * (int)pm() - st;          // line L' piece -> slots slo, slo + 1
+            const int shi = slo + 16;                     // line L'+1 piece
+            // only pieces inside the window are written (exec-masked): the 8 lanes of an
+            // instance hit the same two banks, so every skipped write is a conflict saved
+            const float4 a = ln[t][LO][r], b = ln[t][HI][r];
+            if (slo >= 0) {
+                float *plo = base + slo * kRow + 2 * jj;
                 *(float2 *)plo = make_float2(a.x, a.y);
-                *(float2 *)(plo + (ulo == kWin ? 0 : kRow)) = make_float2(a.z, a.w);
+                *(float2 *)(plo + kRow) = make_float2(a.z, a.w);
+            }
+            if (shi < kWin) {
+                float *phi = base + shi * kRow + 2 * jj;
                 *(float2 *)phi = make_float2(b.x, b.y);
-                *(float2 *)(phi + (uhi == kWin ? 0 : kRow)) = make_float2(b.z, b.w);
+                *(float2 *)(phi + kRow) = make_float2(b.z, b.w);
             }
         }
-        if (FULL) region[2 * kSlots * kRow + strag_slot * kRow + lane] = strag;
+        if (t == 2) base[strag_slot * kRow + lane] = strag;
     }
 
     __device__ __forceinline__ void stage_run(const float (&v)[kChunk], uint32_t base) {
@@ -243,10 +279,9 @@ struct ChStageL {
             const uint32_t q = (uint32_t)r * 64u + lane, o = q >> 3, f2 = 2u * (q & 7u);
             const float4 v = *(const float4 *)(region + base + o * kStride + 2u * f2);
             const uint32_t oi = inst0 + o;
-            if (oi < n && (int)f2 < C) {
-                if (pitch) st4<kStreamAux>(rP, oi * pstride + ((w + f2) & pmask) * 8u, v);
-                else st4<kStreamAux>(rC, oi * cstride + ((w + f2) & cmask) * 8u, v);
-            }
+            const bool ok = oi < n && (int)f2 < C;      // else an offset past the buffer: dropped
+            if (pitch) st4<kStreamAux>(rP, ok ? oi * pstride + ((w + f2) & pmask) * 8u : 0xFFFFFFF0u, v);
+            else st4<kStreamAux>(rC, ok ? oi * cstride + ((w + f2) & cmask) * 8u : 0xFFFFFFF0u, v);
         }
     }
 
@@ -259,109 +294,208 @@ struct ChStageL {
     }
 
     // One chunk; PAR = chunk parity (the line set holding this chunk's line L'+1).
-    template <int PAR, class Sink>
-    __device__ __forceinline__ void chunk(const float (&x)[kChunk], int C, int Cn, Sink &&sink) {
+    // psv_c and x_{c+1} into the rings (the pitch windows are dead: their LDS is staging), then
+    // chunk c+1's plan and line loads
+    template <int PAR>
+    __device__ __forceinline__ void stores_and_next(const float (&psv)[kChunk], const float (&xn)[kChunk], uint32_t w0,
+                                                    int C, int Cn, uint32_t lfo0, uint32_t ps0) {
+        if (FULL) {
+            stage_run(psv, kPsvBase);
+            coop_store(false, kPsvBase, w0, C);
+        }
+        if (Cn > 0) {
+            stage_run(xn, 0);
+            coop_store(true, 0, w0 + (uint32_t)C, Cn);
+        }
+        pl = plan_chunk_l<kWin>(lfo0 + (uint32_t)C * lfo_inc, lfo_inc, lfo_off, ps0 + (uint32_t)C * ps_inc,
+                                ps_inc, Cn > 0 ? Cn : 4, D, W, pmax, cmax, FULL);
+        // the line loads below read positions the stores above just wrote (other lanes of this
+        // wave): vector memory operations of a wave reach the L1/L2 in issue order, as for the
+        // v10 chunk-start input store and the loads after it
+        load_lines<PAR ^ 1>(pl, w0 + (uint32_t)C, false);
+    }
+
+    // One chunk of C frames (multiple of 4) with input x; xn = the next chunk's input (Cn frames,
+    // 0 = none), whose loads prefetch() issues.  PAR = chunk parity (the line set holding this
+    // chunk's line L'+1).  Order (the staleness argument in the header):
+    //   stage this chunk's windows, patch in x_c and psv_{c-1} (not in carried lines)
+    //   A  pitch-shifter over the chunk -> psv_c; psv_c -> chorus window and chorus ring
+    //      x_{c+1} (= xn) -> pitch ring
+    //      plan chunk c+1, issue its line loads (they see both stores)
+    //   C  chorus tap + lores~ + outputs (the cover for those loads)
+    template <int PAR, class Sink, class Prefetch>
+    __device__ __forceinline__ void chunk(const float (&x)[kChunk], const float (&xn)[kChunk], int C, int Cn,
+                                          Sink &&sink, Prefetch &&prefetch) {
+        // Everything lane-dependent is recomputed per chunk from a lane index the compiler must
+        // treat as new: hoisted loop invariants (ring and LDS addresses) were spilled under the
+        // pressure of the 96 line registers, and each scratch reload is a vmcnt(0) drain.
+        asm volatile("" : "+v"(lane));
+        j = lane >> 1;
+        ch = lane & 1u;
         const uint32_t w0 = wpos;
+        const uint32_t lfo0 = lfo_acc, ps0 = ps_acc;     // the phasors at the chunk's first frame
         const PlanL cur = pl;
+        float psv[kChunk];
         float *wP0 = region + 0 * kSlots * kRow + lane;
         float *wP1 = region + 1 * kSlots * kRow + lane;
         float *wC = region + 2 * kSlots * kRow + lane;
 
-        if (started) {
-            stage_run(x, 0);
-            coop_store(true, 0, w0, C);
-        }
-        stage_lines<PAR>();
-        if (started) {
-            if (cur.sA > -kWin) {
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k)
-                    if (k < C && k - cur.sA < kWin) wP0[(k - cur.sA) * kRow] = x[k];
-            }
-            if (cur.sB > -kWin) {
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k)
-                    if (k < C && k - cur.sB < kWin) wP1[(k - cur.sB) * kRow] = x[k];
-            }
-            if (FULL && cur.sC > -kWin - kChunk) {
+        // tap C first: psv_{c-1}, still in its LDS staging (region + kPsvBase, under taps A/B),
+        // is not in a carried line -- patch it in, then stage taps A and B over the staging
+        if (FULL) {
+            stage_tap<PAR, 2>();
+            if (started && cur.sC > -kWin - kChunk) {
+                const float *prev = region + kPsvBase + j * kStride + ch;
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) {
                     const int jw = k - kChunk - cur.sC;
-                    if (jw >= 0 && jw < kWin) wC[jw * kRow] = psv[k];
+                    if (jw >= 0 && jw < kWin) wC[jw * kRow] = prev[2 * k];
                 }
             }
         }
-        started = true;
-
-        pl = plan_chunk_l<kWin>(lfo_acc + (uint32_t)C * lfo_inc, lfo_inc, lfo_off, ps_acc + (uint32_t)C * ps_inc,
-                                ps_inc, Cn > 0 ? Cn : 4, D, W, pmax, cmax, FULL);
-        load_lines<PAR ^ 1>(pl, w0 + kChunk, false);
-
-        float pl_lfo[2], pl_gA[2], pl_gB[2];
-        auto frame = [&](auto generic_tag, int k) {
-            constexpr bool GENERIC = decltype(generic_tag)::value;
-            if ((k & 1) == 0) {
-                const uint32_t la = lfo_acc + ch * lfo_inc, pa = ps_acc + ch * ps_inc;
-                const float m_lfo = cos2pi(unit24(la + lfo_off));
-                const float m_gA = cos2pi((unit24(pa) - 0.5f) * 0.5f);
-                const float m_gB = cos2pi((unit24(pa + 0x80000000u) - 0.5f) * 0.5f);
-                const float o_lfo = swap_pair(m_lfo), o_gA = swap_pair(m_gA), o_gB = swap_pair(m_gB);
-                pl_lfo[0] = ch ? o_lfo : m_lfo; pl_lfo[1] = ch ? m_lfo : o_lfo;
-                pl_gA[0] = ch ? o_gA : m_gA;    pl_gA[1] = ch ? m_gA : o_gA;
-                pl_gB[0] = ch ? o_gB : m_gB;    pl_gB[1] = ch ? m_gB : o_gB;
-            }
-            if (GENERIC && k >= C) { psv[k] = 0.f; return; }
-            const float lfo = pl_lfo[k & 1];
-            const float dch = lfo * D + D;
-            const float p0 = unit24(ps_acc);
-            const float p1 = unit24(ps_acc + 0x80000000u);
-            const float gA = pl_gA[k & 1];
-            const float gB = pl_gB[k & 1];
-            lfo_acc += lfo_inc;
-            ps_acc += ps_inc;
-            int di; float fr;
-            float tA, tB;
-            split_delay(p0 * W, 1.0f, pmax, di, fr);
-            if (GENERIC && !cur.okA) {
-                const uint32_t q = w0 + k - di;
-                tA = lerp_pair(ld1(rP, own_pb + (q & pmask) * 8u, 0), ld1(rP, own_pb + ((q - 1u) & pmask) * 8u, 0), fr);
-            } else {
-                const int jw = k - di - cur.sA;
-                tA = lerp_pair(wP0[jw * kRow], wP0[(jw - 1) * kRow], fr);
-            }
-            split_delay(p1 * W, 1.0f, pmax, di, fr);
-            if (GENERIC && !cur.okB) {
-                const uint32_t q = w0 + k - di;
-                tB = lerp_pair(ld1(rP, own_pb + (q & pmask) * 8u, 0), ld1(rP, own_pb + ((q - 1u) & pmask) * 8u, 0), fr);
-            } else {
-                const int jw = k - di - cur.sB;
-                tB = lerp_pair(wP1[jw * kRow], wP1[(jw - 1) * kRow], fr);
-            }
-            const float p = tB * gB + tA * gA;
-            psv[k] = p;
-            float out = p;
-            if (FULL) {
-                wC[min(k - cur.sC, kWin) * kRow] = p;
-                split_delay(dch, 0.0f, cmax, di, fr);
-                const int jw = k - di - cur.sC;
-                const float wet = lerp_pair(wC[jw * kRow], wC[(jw - 1) * kRow], fr);
-                const float lp = b0 * wet + z1;
-                z1 = (b1 * wet - a1 * lp) + z2;
-                z2 = b2 * wet - a2 * lp;
-                out = x[k] * dry + lp * mix;
-            }
-            sink(k, out);
-        };
-        if (C == kChunk && __all(cur.okA && cur.okB)) {
+        stage_tap<PAR, 0>();
+        stage_tap<PAR, 1>();
+        // x_c is not in a carried line either
+        if (cur.sA > -kWin) {
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) frame(std::false_type{}, k);
-        } else {
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) frame(std::true_type{}, k);
+            for (int k = 0; k < kChunk; ++k)
+                if (k < C && k - cur.sA < kWin) wP0[(k - cur.sA) * kRow] = x[k];
         }
-        if (FULL) {
-            stage_run(psv, kPsvBase);
-            coop_store(false, kPsvBase, w0, C);
+        if (cur.sB > -kWin) {
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k)
+                if (k < C && k - cur.sB < kWin) wP1[(k - cur.sB) * kRow] = x[k];
+        }
+        started = true;
+        prefetch();
+
+        const bool fast = C == kChunk && __all(cur.okA && cur.okB);
+        if (fast) {
+            // fast path, in phases with the per-frame arithmetic of frame() below:
+            //  A. the pitch-shifter for all 16 frames (reads only the pitch windows, no LDS store:
+            //     every frame's reads can be in flight together);
+            //  B. its outputs into the chorus window -- delay~ writes before it reads, and a frame
+            //     never reads a position newer than its own, so writing them all first is the same
+            //     as writing each just before its frame;
+            //  (C, the chorus tap, follows the ring stores and chunk c+1's line loads below)
+            // p W == (acc >> 8) (W 2^-24) exactly (scaling by a power of two is exact)
+            const float Ws = W * 5.9604644775390625e-8f;
+            float gA0 = 0.f, gA1 = 0.f, gB0 = 0.f, gB1 = 0.f;
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) {
+                if ((k & 1) == 0) {
+                    // gain arguments (p - 1/2)/2 lie in [-1/4, 1/4): cos2pi_q == cos2pi there
+                    const uint32_t pa = ps_acc + ch * ps_inc;
+                    const float m_gA = cos2pi_q((unit24(pa) - 0.5f) * 0.5f);
+                    const float m_gB = cos2pi_q((unit24(pa + 0x80000000u) - 0.5f) * 0.5f);
+                    gA0 = pair_even(m_gA); gA1 = pair_odd(m_gA);
+                    gB0 = pair_even(m_gB); gB1 = pair_odd(m_gB);
+                }
+                const float d0 = (float)(ps_acc >> 8) * Ws;
+                const float d1 = (float)((ps_acc + 0x80000000u) >> 8) * Ws;
+                ps_acc += ps_inc;
+                int di; float fr;
+                split_delay3(d0, 1.0f, pmax, di, fr);
+                int jw = k - di - cur.sA;
+                const float tA = lerp_pair(wP0[jw * kRow], wP0[(jw - 1) * kRow], fr);
+                split_delay3(d1, 1.0f, pmax, di, fr);
+                jw = k - di - cur.sB;
+                const float tB = lerp_pair(wP1[jw * kRow], wP1[(jw - 1) * kRow], fr);
+                psv[k] = tB * ((k & 1) ? gB1 : gB0) + tA * ((k & 1) ? gA1 : gA0);
+            }
+            if (FULL) {
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) wC[min(k - cur.sC, kWin) * kRow] = psv[k];
+            }
+        } else {
+            // generic chunk (partial, or a pitch window the lines cannot cover): per frame, with
+            // per-frame guards and direct ring reads for the uncovered pitch taps
+            float pl_lfo[2], pl_gA[2], pl_gB[2];
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) {
+                if ((k & 1) == 0) {
+                    const uint32_t la = lfo_acc + ch * lfo_inc, pa = ps_acc + ch * ps_inc;
+                    const float m_lfo = cos2pi(unit24(la + lfo_off));
+                    const float m_gA = cos2pi((unit24(pa) - 0.5f) * 0.5f);
+                    const float m_gB = cos2pi((unit24(pa + 0x80000000u) - 0.5f) * 0.5f);
+                    const float o_lfo = swap_pair(m_lfo), o_gA = swap_pair(m_gA), o_gB = swap_pair(m_gB);
+                    pl_lfo[0] = ch ? o_lfo : m_lfo; pl_lfo[1] = ch ? m_lfo : o_lfo;
+                    pl_gA[0] = ch ? o_gA : m_gA;    pl_gA[1] = ch ? m_gA : o_gA;
+                    pl_gB[0] = ch ? o_gB : m_gB;    pl_gB[1] = ch ? m_gB : o_gB;
+                }
+                if (k >= C) { psv[k] = 0.f; continue; }
+                const float lfo = pl_lfo[k & 1];
+                const float dch = lfo * D + D;
+                const float p0 = unit24(ps_acc);
+                const float p1 = unit24(ps_acc + 0x80000000u);
+                const float gA = pl_gA[k & 1];
+                const float gB = pl_gB[k & 1];
+                lfo_acc += lfo_inc;
+                ps_acc += ps_inc;
+                int di; float fr;
+                float tA, tB;
+                split_delay(p0 * W, 1.0f, pmax, di, fr);
+                if (!cur.okA) {
+                    const uint32_t q = w0 + k - di;
+                    tA = lerp_pair(ld1(rP, own_pb() + (q & pmask) * 8u, 0), ld1(rP, own_pb() + ((q - 1u) & pmask) * 8u, 0), fr);
+                } else {
+                    const int jw = k - di - cur.sA;
+                    tA = lerp_pair(wP0[jw * kRow], wP0[(jw - 1) * kRow], fr);
+                }
+                split_delay(p1 * W, 1.0f, pmax, di, fr);
+                if (!cur.okB) {
+                    const uint32_t q = w0 + k - di;
+                    tB = lerp_pair(ld1(rP, own_pb() + (q & pmask) * 8u, 0), ld1(rP, own_pb() + ((q - 1u) & pmask) * 8u, 0), fr);
+                } else {
+                    const int jw = k - di - cur.sB;
+                    tB = lerp_pair(wP1[jw * kRow], wP1[(jw - 1) * kRow], fr);
+                }
+                const float p = tB * gB + tA * gA;
+                psv[k] = p;
+                float out = p;
+                if (FULL) {
+                    wC[min(k - cur.sC, kWin) * kRow] = p;
+                    split_delay(dch, 0.0f, cmax, di, fr);
+                    const int jw = k - di - cur.sC;
+                    const float wet = lerp_pair(wC[jw * kRow], wC[(jw - 1) * kRow], fr);
+                    const float lp = b0 * wet + z1;
+                    z1 = (b1 * wet - a1 * lp) + z2;
+                    z2 = b2 * wet - a2 * lp;
+                    out = x[k] * dry + lp * mix;
+                }
+                sink(k, out);
+            }
+        }
+        // one call site: line registers loaded on two paths meet in a phi, and the copies it needs
+        // pushed the kernel from 211 VGPRs to 256 + spills
+        stores_and_next<PAR>(psv, xn, w0, C, Cn, lfo0, ps0);
+        if (fast) {
+            // C. the chorus tap + lores~ (reads independent of each other; only the biquad is serial),
+            //    the cover for chunk c+1's line loads
+            if (FULL) {
+                float l0 = 0.f, l1 = 0.f;
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) {
+                    if ((k & 1) == 0) {
+                        const float m_lfo = cos2pi(unit24(lfo_acc + ch * lfo_inc + lfo_off));
+                        l0 = pair_even(m_lfo); l1 = pair_odd(m_lfo);
+                    }
+                    const float dch = ((k & 1) ? l1 : l0) * D + D;
+                    lfo_acc += lfo_inc;
+                    int di; float fr;
+                    split_delay3(dch, 0.0f, cmax, di, fr);
+                    const int jw = k - di - cur.sC;
+                    const float wet = lerp_pair(wC[jw * kRow], wC[(jw - 1) * kRow], fr);
+                    const float lp = b0 * wet + z1;
+                    z1 = (b1 * wet - a1 * lp) + z2;
+                    z2 = b2 * wet - a2 * lp;
+                    sink(k, x[k] * dry + lp * mix);
+                }
+            } else {
+                lfo_acc += (uint32_t)kChunk * lfo_inc;
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) sink(k, psv[k]);
+            }
         }
         wpos = w0 + (uint32_t)C;
     }
