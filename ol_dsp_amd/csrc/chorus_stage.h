@@ -96,6 +96,34 @@ __device__ __forceinline__ int floor_delay(float d, float dmin, float dmax) {
 
 __device__ __forceinline__ float lerp_pair(float x0, float x1, float fr) { return x0 + fr * (x1 - x0); }
 
+// cos(2 pi x) for |x| <= 0.25: cos2pi() (olfx_internal.h) with its range reduction folded away.
+// There u = x - rint(x) = x, a = |x| <= 0.25 never takes the reflected branch, and
+// (x 2pi)^2 == (|x| 2pi)^2 exactly: bit-identical results, six fewer instructions.
+__device__ __forceinline__ float cos2pi_q(float x) {
+    const float th = x * 6.28318530717958647692f;
+    const float t2 = th * th;
+    return 1.0f + t2 * (-0.5f + t2 * (4.16666666666666666667e-2f +
+           t2 * (-1.38888888888888888889e-3f + t2 * (2.48015873015873015873e-5f +
+           t2 * (-2.75573192239858906526e-7f + t2 * (2.08767569878680989792e-9f +
+           t2 * (-1.14707455977297247139e-11f)))))));
+}
+// a value of lane 2j (EVEN) or 2j+1 (odd) to both lanes of the pair: DPP quad_perm [0,0,2,2] / [1,1,3,3]
+__device__ __forceinline__ float pair_even(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xA0, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float pair_odd(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xF5, 0xF, 0xF, false));
+}
+// split_delay with the clamp as one v_med3 (identical to fminf(fmaxf()) for non-NaN delays,
+// and delays here are phasor arithmetic, never NaN)
+__device__ __forceinline__ void split_delay3(float d, float dmin, float dmax, int &di, float &fr) {
+    d = __builtin_amdgcn_fmed3f(d, dmin, dmax);
+    const uint32_t u = (uint32_t)d;
+    di = (int)u;
+    fr = d - (float)u;
+}
+
+
 // Window geometry of one chunk for one lane: starts (relative to the chunk's first write
 // position, multiples of 4) of the two pitch windows and the chorus window.
 struct Plan {
@@ -378,8 +406,59 @@ struct ChStage {
             sink(k, out);
         };
         if (C == kChunk && __all(cur.okA && cur.okB)) {
+            // fast path in phases, with frame()'s per-frame arithmetic (bit-identical): the
+            // pitch-shifter for all 16 frames (its reads all in flight together), its outputs
+            // into the chorus window (a frame never reads a position newer than its own), then
+            // the chorus tap + lores~ (see chorus_stage_l.h)
+            const float Ws = W * 5.9604644775390625e-8f;
+            float gA0 = 0.f, gA1 = 0.f, gB0 = 0.f, gB1 = 0.f;
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) frame(std::false_type{}, k);
+            for (int k = 0; k < kChunk; ++k) {
+                if ((k & 1) == 0) {
+                    const uint32_t pa = ps_acc + ch * ps_inc;
+                    const float m_gA = cos2pi_q((unit24(pa) - 0.5f) * 0.5f);
+                    const float m_gB = cos2pi_q((unit24(pa + 0x80000000u) - 0.5f) * 0.5f);
+                    gA0 = pair_even(m_gA); gA1 = pair_odd(m_gA);
+                    gB0 = pair_even(m_gB); gB1 = pair_odd(m_gB);
+                }
+                const float d0 = (float)(ps_acc >> 8) * Ws;
+                const float d1 = (float)((ps_acc + 0x80000000u) >> 8) * Ws;
+                ps_acc += ps_inc;
+                int di; float fr;
+                split_delay3(d0, 1.0f, pmax, di, fr);
+                int jw = k - di - cur.sA;
+                const float tA = lerp_pair(wP0[jw * kRow], wP0[(jw - 1) * kRow], fr);
+                split_delay3(d1, 1.0f, pmax, di, fr);
+                jw = k - di - cur.sB;
+                const float tB = lerp_pair(wP1[jw * kRow], wP1[(jw - 1) * kRow], fr);
+                psv[k] = tB * ((k & 1) ? gB1 : gB0) + tA * ((k & 1) ? gA1 : gA0);
+            }
+            if (FULL) {
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) wC[min(k - cur.sC, kWin) * kRow] = psv[k];
+                float l0 = 0.f, l1 = 0.f;
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) {
+                    if ((k & 1) == 0) {
+                        const float m_lfo = cos2pi(unit24(lfo_acc + ch * lfo_inc + lfo_off));
+                        l0 = pair_even(m_lfo); l1 = pair_odd(m_lfo);
+                    }
+                    const float dch = ((k & 1) ? l1 : l0) * D + D;
+                    lfo_acc += lfo_inc;
+                    int di; float fr;
+                    split_delay3(dch, 0.0f, cmax, di, fr);
+                    const int jw = k - di - cur.sC;
+                    const float wet = lerp_pair(wC[jw * kRow], wC[(jw - 1) * kRow], fr);
+                    const float lp = b0 * wet + z1;
+                    z1 = (b1 * wet - a1 * lp) + z2;
+                    z2 = b2 * wet - a2 * lp;
+                    sink(k, x[k] * dry + lp * mix);
+                }
+            } else {
+                lfo_acc += (uint32_t)kChunk * lfo_inc;
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) sink(k, psv[k]);
+            }
         } else {
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) frame(std::true_type{}, k);
