@@ -14,9 +14,10 @@
  * compiled against verb.h links to the mangled names (_Z20DattorroVerb_processP13sDattorroVerbf
  * ...).  Either way a caller swaps verb.cpp for libolfx.so without a source change.
  *
- * How per-sample calls reach a batch GPU kernel: every instance created here joins a process-wide
- * pool.  Instances created before the pool first runs form one engine (a "generation") of N
- * instances on the GPU; instances created later start the next generation.  DattorroVerb_process
+ * How per-sample calls reach a batch GPU kernel: every instance created here is an olfx_sample
+ * of kind OLFX_KIND_DATTORRO at 48 kHz (include/olfx_sample.h) and joins that process-wide pool.
+ * Instances created before the pool first runs form one engine (a "generation") of N instances on
+ * the GPU; instances created later start the next generation.  DattorroVerb_process
  * buffers the sample; when every live instance of a generation has been given `block` samples,
  * the generation runs one olfx_process over the whole block for all of them.  Consequences,
  * stated as the interface contract:
@@ -59,8 +60,8 @@ t_sample DattorroVerb_getRight(struct sDattorroVerb *v);
 
 /* ---- pool control (new; not in verb.h) ---- */
 /* Device and block (frames per GPU call = the latency, a positive multiple of 4) used by
-   generations created after this call.  Defaults: device 0, block 256.  Returns OLFX_OK (0) or
-   OLFX_E_ARG. */
+   generations created after this call -- the setting of olfx_sample_pool_config, shared with the
+   other per-sample operators.  Defaults: device 0, block 256.  Returns OLFX_OK (0) or OLFX_E_ARG. */
 int olfx_dattorro_pool_config(int device, uint32_t block);
 /* The latency in samples of instance v (its generation's block). */
 uint32_t olfx_dattorro_latency(const struct sDattorroVerb *v);

@@ -14,6 +14,15 @@
  *   olfx::VoiceBank   <- ol::synth::SynthVoice (modules/synthlib/SynthVoice.h:31-98, :245-256):
  *                        Init / UpdateConfig / NoteOn / NoteOff / Process.
  *
+ * and, one object per reference object (include/olfx_sample.h: per-sample calls batched into one
+ * GPU block per generation, one block of latency, frame-major calls):
+ *   olfx::ChorusEffect <- ChorusEffect (README.md:114-128): init / setDepth / setRate / process(float)
+ *   olfx::SynthVoice   <- ol::synth::SynthVoice (SynthVoice.h:31-256): Init / UpdateConfig / NoteOn /
+ *                         NoteOff / UpdateMidiControl / UpdateHardwareControl / Process(frame_out)
+ *   olfx::FxRack       <- ol::fx::FxRack<2> (Fx.h:398-492): Init / Process(frame_in, frame_out) /
+ *                         UpdateMidiControl / UpdateHardwareControl
+ *   (the reverb: DattorroVerb_* by name, include/olfx_dattorro.h)
+ *
  * Each per-instance setter takes the same value as the reference setter and applies it at the
  * next Process call (block-boundary parameter updates, modules/juce/host/host.cpp:646-653).
  *
@@ -36,6 +45,7 @@
 #include <vector>
 
 #include "olfx.h"
+#include "olfx_sample.h"
 
 namespace olfx {
 
@@ -204,6 +214,100 @@ private:
         ev.inst = i; ev.type = type; ev.note = note; ev.velocity = vel;
         check(olfx_note_events(e_, &ev, 1), e_, "olfx_note_events");
     }
+};
+
+/* ------------------------------------------------------------------------------------------
+ * Per-instance, per-sample operators: the reference's objects one for one.  The k-th Process /
+ * process call returns the reference's output of frame k - latency() (zeros before); setters,
+ * notes and controls land at the next block boundary.  Calls must be frame-major across the
+ * instances of a generation (include/olfx_sample.h); a violation throws OLFX_E_STATE.
+ * ------------------------------------------------------------------------------------------ */
+class SampleOperator {
+public:
+    SampleOperator() = default;
+    SampleOperator(const SampleOperator &) = delete;
+    SampleOperator &operator=(const SampleOperator &) = delete;
+    ~SampleOperator() { release(); }
+    uint32_t latency() const { return s_ ? olfx_sample_latency(s_) : 0; }
+    void set(uint32_t field, float value) { check(olfx_sample_set_param(need(), field, value), nullptr, "olfx_sample_set_param"); }
+
+protected:
+    void create(int kind, float sample_rate) {
+        release();
+        check(olfx_sample_create(kind, sample_rate, &s_), nullptr, "olfx_sample_create");
+    }
+    void frame(const float *in, float *out) { check(olfx_sample_process(need(), in, out), nullptr, "olfx_sample_process"); }
+    void note(uint8_t type, uint8_t midi_note, uint8_t velocity) {
+        check(olfx_sample_note(need(), type, midi_note, velocity), nullptr, "olfx_sample_note");
+    }
+    void control(uint8_t cc, int source, float value) {
+        check(olfx_sample_control(need(), cc, source, value), nullptr, "olfx_sample_control");
+    }
+
+private:
+    olfx_sample *need() const {
+        if (!s_) throw Error(OLFX_E_STATE, "operator used before init()/Init()");
+        return s_;
+    }
+    void release() {
+        if (s_) olfx_sample_destroy(s_);
+        s_ = nullptr;
+    }
+    olfx_sample *s_ = nullptr;
+};
+
+/* README.md:114-128's ChorusEffect: mono in, mono out.  The mono sample drives both channels of
+   the stereo RNBO chorus, whose L and R are then identical (one LFO, stereo-chorus.rnbopat:546,
+   1196); process returns L.  Values are RNBO param values, clamped to @min/@max. */
+class ChorusEffect : public SampleOperator {
+public:
+    void init(float sample_rate) { create(OLFX_KIND_CHORUS, sample_rate); }
+    void setDepth(float v) { set(OLFX_CH_DEPTH, v); }
+    void setRate(float v) { set(OLFX_CH_RATE, v); }
+    void setMix(float v) { set(OLFX_CH_MIX, v); }
+    void setCutoff(float v) { set(OLFX_CH_CUTOFF, v); }
+    void setQ(float v) { set(OLFX_CH_Q, v); }
+    void setPitch(float v) { set(OLFX_CH_PITCH, v); }
+    void setPhase(float v) { set(OLFX_CH_PHASE, v); }
+    void setWindow(float v) { set(OLFX_CH_WINDOW, v); }
+    float process(float in) {
+        const float x[2] = {in, in};
+        float y[2];
+        frame(x, y);
+        return y[0];
+    }
+};
+
+/* ol::synth::SynthVoice (SynthVoice.h:31-256) with its SvfFilter or the Daisy firmware's
+   MoogFilter (ol_daisy/app/synth/main.cpp:49-52). */
+class SynthVoice : public SampleOperator {
+public:
+    enum class Filter { Svf, Moog };
+    explicit SynthVoice(Filter filter = Filter::Svf) : kind_(filter == Filter::Moog ? OLFX_KIND_VOICE_MOOG : OLFX_KIND_VOICE) {}
+    void Init(float sample_rate) { create(kind_, sample_rate); }
+    /* Voice::Config in field order (Voice.h:14-31 == OLFX_VC_*), then Update() */
+    void UpdateConfig(const float config[OLFX_VC_NPARAMS]) {
+        for (uint32_t f = 0; f < OLFX_VC_NPARAMS; ++f) set(f, config[f]);
+    }
+    void NoteOn(uint8_t midi_note, uint8_t velocity) { note(OLFX_EV_NOTE_ON, midi_note, velocity); }
+    void NoteOff(uint8_t midi_note, uint8_t velocity) { note(OLFX_EV_NOTE_OFF, midi_note, velocity); }
+    void UpdateMidiControl(uint8_t control_, uint8_t value) { control(control_, OLFX_CTL_MIDI, value); }
+    void UpdateHardwareControl(uint8_t control_, float value) { control(control_, OLFX_CTL_HARDWARE, value); }
+    /* frame_out[0] = this voice's sample (SynthVoice.h:41-53) */
+    void Process(float *frame_out) { frame(nullptr, frame_out); }
+
+private:
+    int kind_;
+};
+
+/* ol::fx::FxRack<2> (Fx.h:398-492): delay -> reverb (ReverbSc stub) -> filter -> master volume.
+   Members are the OLFX_FR_* fields (set(field, value)). */
+class FxRack : public SampleOperator {
+public:
+    void Init(float sample_rate) { create(OLFX_KIND_FXRACK, sample_rate); }
+    void Process(const float *frame_in, float *frame_out) { frame(frame_in, frame_out); }
+    void UpdateMidiControl(uint8_t control_, uint8_t value) { control(control_, OLFX_CTL_MIDI, value); }
+    void UpdateHardwareControl(uint8_t control_, float value) { control(control_, OLFX_CTL_HARDWARE, value); }
 };
 
 }  // namespace olfx

@@ -105,6 +105,17 @@ SIGNATURES = {
     "olfx_algorithmic_bytes_per_frame": (ctypes.c_double, [_P]),
     "olfx_kernel_name": (ctypes.c_char_p, [_P]),
     "olfx_last_error": (ctypes.c_char_p, [_P]),
+    # include/olfx_sample.h: per-instance, per-sample operators (one block of latency)
+    "olfx_sample_pool_config": (ctypes.c_int, [ctypes.c_int, _U32]),
+    "olfx_sample_create": (ctypes.c_int, [ctypes.c_int, _F, ctypes.POINTER(_P)]),
+    "olfx_sample_destroy": (ctypes.c_int, [_P]),
+    "olfx_sample_set_param": (ctypes.c_int, [_P, _U32, _F]),
+    "olfx_sample_note": (ctypes.c_int, [_P, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
+    "olfx_sample_control": (ctypes.c_int, [_P, ctypes.c_uint8, ctypes.c_int, _F]),
+    "olfx_sample_process": (ctypes.c_int, [_P, ctypes.POINTER(_F), ctypes.POINTER(_F)]),
+    "olfx_sample_latency": (_U32, [_P]),
+    "olfx_sample_generation_size": (_U32, [_P]),
+    "olfx_sample_index": (_U32, [_P]),
     # include/olfx_dattorro.h: pool control of the verb.h-compatible names
     "olfx_dattorro_pool_config": (ctypes.c_int, [ctypes.c_int, _U32]),
     "olfx_dattorro_latency": (_U32, [_P]),

@@ -37,6 +37,14 @@ void set_global_error(const char *fmt, ...) {
     g_err = buf;
 }
 
+}  // namespace
+
+// for the per-sample pool (olfx_sample_pool.cpp): its failures are reported through
+// olfx_last_error(NULL) like engine-less errors here
+void olfx::internal_set_error(const char *msg) { set_global_error("%s", msg); }
+
+namespace {
+
 uint32_t pow2_at_least(uint32_t x) {
     uint32_t p = 1;
     while (p < x) p <<= 1;

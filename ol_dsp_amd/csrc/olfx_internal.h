@@ -229,4 +229,7 @@ hipError_t launch_chain(const ChainArgs &a, hipStream_t s);
 hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s);
 hipError_t launch_voice(const VoiceArgs &a, hipStream_t s);
 
+// host side: record a global error message (olfx_last_error(NULL))
+void internal_set_error(const char *msg);
+
 }  // namespace olfx

@@ -293,6 +293,134 @@ TEST(Boundary, ErrorsThrowWithCode) {
     EXPECT_TRUE(same);
 }
 
+/* ---- per-instance, per-sample operators (include/olfx_sample.h): the reference's objects one
+   for one, called one frame at a time in frame-major order; output = the oracle delayed by one
+   block; calls land at the first block boundary at or after them ---- */
+TEST(PerSample, ChorusEffectReadmeSurface) {
+    const uint32_t n = 3, B = 256, F = 4 * B;
+    olfx::ChorusEffect fx[n];
+    oracle_chorus *ref = oracle_chorus_create((int)n, 48000.f, 0);
+    const float depth[n] = {0.5f, 0.9f, 0.2f}, rate[n] = {0.2f, 1.0f, 0.05f};
+    for (uint32_t i = 0; i < n; ++i) {            /* README.md:119-121 */
+        fx[i].init(48000.f);
+        fx[i].setDepth(depth[i]);
+        fx[i].setRate(rate[i]);
+        oracle_chorus_set(ref, (int)i, OCH_DEPTH, depth[i]);
+        oracle_chorus_set(ref, (int)i, OCH_RATE, rate[i]);
+    }
+    EXPECT_EQ(fx[0].latency(), B);
+    std::vector<float> x = noise(1, F, n, 21), y((size_t)F * n);
+    for (uint32_t t = 0; t < F; ++t) {
+        if (t == B + 7) fx[1].setMix(0.9f);       /* mid-block 1: lands at frame 2B */
+        for (uint32_t i = 0; i < n; ++i) y[(size_t)t * n + i] = fx[i].process(x[(size_t)t * n + i]);
+    }
+    /* oracle: stereo input with L = R = x, blocks of B, the mix change before block 2 */
+    std::vector<float> x2(2 * (size_t)F * n);
+    std::memcpy(x2.data(), x.data(), x.size() * 4);
+    std::memcpy(x2.data() + x.size(), x.data(), x.size() * 4);
+    uint32_t done = 0;
+    std::vector<float> yr = run_blocks([&](const float *xi, float *yo, uint32_t b) {
+        if (done == 2 * B) oracle_chorus_set(ref, 1, OCH_MIX, 0.9f);
+        oracle_chorus_process(ref, xi, yo, (int)b, 1);
+        done += b;
+    }, x2, 2, 2, F, n, B);
+    bool ok = true;
+    for (uint32_t t = 0; t < F && ok; ++t)
+        for (uint32_t i = 0; i < n && ok; ++i) {
+            const float want = t < B ? 0.f : yr[(size_t)(t - B) * n + i];   /* channel 0 (L) */
+            ok = std::memcmp(&y[(size_t)t * n + i], &want, 4) == 0;
+            if (!ok) std::printf("  first mismatch t=%u i=%u: %.9g vs %.9g\n", t, i, y[(size_t)t * n + i], want);
+        }
+    EXPECT_TRUE(ok);
+    oracle_chorus_destroy(ref);
+}
+
+TEST(PerSample, SynthVoiceNoteOffAtNextBoundary) {
+    const uint32_t n = 2, B = 256, F = 4 * B;
+    olfx::SynthVoice v[n];
+    oracle_voice *ref = oracle_voice_create_model((int)n, 48000.f, 0);
+    const uint8_t notes[n] = {60, 67};
+    for (uint32_t i = 0; i < n; ++i) {
+        float c[OLFX_VC_NPARAMS] = {2000.f + 1000.f * i, 0.3f, 0.1f, 0.5f, 0.01f, 0.f, 0.2f, 0.5f, 0.1f,
+                                    1.f, 0.005f, 0.f, 0.1f, 0.7f, 0.05f, 0.f};
+        v[i].Init(48000.f);
+        v[i].UpdateConfig(c);
+        v[i].NoteOn(notes[i], 100);
+        oracle_voice_config(ref, (int)i, c);
+        oracle_voice_note(ref, (int)i, 1, notes[i]);
+    }
+    std::vector<float> y((size_t)F * n);
+    for (uint32_t t = 0; t < F; ++t) {
+        if (t == B + 44)                          /* mid-block 1: NoteOff lands at frame 2B */
+            for (uint32_t i = 0; i < n; ++i) v[i].NoteOff(notes[i], 0);
+        for (uint32_t i = 0; i < n; ++i) v[i].Process(&y[(size_t)t * n + i]);
+    }
+    std::vector<float> yr((size_t)F * n);
+    oracle_voice_process(ref, yr.data(), (int)(2 * B), 1);
+    for (uint32_t i = 0; i < n; ++i) oracle_voice_note(ref, (int)i, 0, notes[i]);
+    oracle_voice_process(ref, yr.data() + (size_t)2 * B * n, (int)(2 * B), 1);
+    for (uint32_t i = 0; i < n; ++i) {            /* |y - ref| <= 1e-5 max(|ref|, rms), as the bank test */
+        double ss = 0, mx = 0, err = 0;
+        for (uint32_t t = B; t < F; ++t) {
+            const double a = yr[(size_t)(t - B) * n + i];
+            ss += a * a; mx = std::max(mx, std::fabs(a));
+            err = std::max(err, std::fabs((double)y[(size_t)t * n + i] - a));
+        }
+        const double scale = std::max(mx, std::sqrt(ss / (F - B)));
+        EXPECT_TRUE(std::isfinite(err) && err <= 1e-5 * std::max(scale, 1e-30));
+        for (uint32_t t = 0; t < B; ++t) EXPECT_EQ(y[(size_t)t * n + i], 0.f);
+    }
+    oracle_voice_destroy(ref);
+}
+
+TEST(PerSample, FxRackPerFrameBitExact) {
+    const uint32_t n = 2, B = 256, F = 3 * B;
+    olfx::FxRack rack[n];
+    oracle_fxrack *ref = oracle_fxrack_create((int)n, 48000.f);
+    const float inv127 = 1.f / 127.f;
+    for (uint32_t i = 0; i < n; ++i) {
+        rack[i].Init(48000.f);
+        const uint8_t t = (uint8_t)(1 + 2 * i);
+        rack[i].UpdateMidiControl(35, t);         /* CC_DELAY_TIME: short echoes inside the run */
+        oracle_fxrack_set(ref, (int)i, OFR_DELAY_TIME, (float)t * inv127 * 1.f + 0.f);
+    }
+    std::vector<float> x = noise(2, F, n, 31), y(2 * (size_t)F * n);
+    for (uint32_t t = 0; t < F; ++t)
+        for (uint32_t i = 0; i < n; ++i) {
+            const float in[2] = {x[(size_t)t * n + i], x[((size_t)F + t) * n + i]};
+            float out[2];
+            rack[i].Process(in, out);
+            y[(size_t)t * n + i] = out[0];
+            y[((size_t)F + t) * n + i] = out[1];
+        }
+    std::vector<float> yr(y.size());
+    oracle_fxrack_process(ref, x.data(), yr.data(), (int)F, 1);
+    bool ok = true;
+    for (uint32_t c = 0; c < 2 && ok; ++c)
+        for (uint32_t t = 0; t < F && ok; ++t)
+            for (uint32_t i = 0; i < n && ok; ++i) {
+                const float want = t < B ? 0.f : yr[((size_t)c * F + t - B) * n + i];
+                ok = std::memcmp(&y[((size_t)c * F + t) * n + i], &want, 4) == 0;
+            }
+    EXPECT_TRUE(ok);
+    oracle_fxrack_destroy(ref);
+}
+
+TEST(PerSample, LockstepViolationThrows) {
+    olfx::ChorusEffect a, b;
+    a.init(48000.f);
+    b.init(48000.f);
+    int code = 0;
+    try {
+        for (uint32_t t = 0; t <= a.latency(); ++t) a.process(0.25f);   /* b never called */
+    } catch (const olfx::Error &e) { code = e.code(); }
+    EXPECT_EQ(code, OLFX_E_STATE);
+    olfx::ChorusEffect c;
+    code = 0;
+    try { c.process(0.f); } catch (const olfx::Error &e) { code = e.code(); }   /* before init() */
+    EXPECT_EQ(code, OLFX_E_STATE);
+}
+
 int main() {
     for (auto &c : cases()) {
         int before = g_failures;

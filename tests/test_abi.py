@@ -12,7 +12,7 @@ from ol_dsp_amd import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "olfx.h")
-C_HEADERS = [os.path.join(ROOT, "include", h) for h in ("olfx.h", "olfx_dattorro.h")]
+C_HEADERS = [os.path.join(ROOT, "include", h) for h in ("olfx.h", "olfx_sample.h", "olfx_dattorro.h")]
 
 
 def declared_functions(prefix="olfx_"):

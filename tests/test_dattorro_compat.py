@@ -94,7 +94,7 @@ def test_without_gpu_process_aborts_loudly():
         print("unreachable")
     """)
     assert r.returncode != 0 and "unreachable" not in r.stdout
-    assert "olfx DattorroVerb: olfx_create" in r.stderr and "no HIP device" in r.stderr
+    assert "olfx DattorroVerb: process: olfx_create" in r.stderr and "no HIP device" in r.stderr
 
 
 # ---------------------------------------------------------------------------------------- GPU
