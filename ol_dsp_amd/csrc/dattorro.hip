@@ -52,6 +52,9 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v4(DattorroArgs a) {
 hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
     if ((a.t0 & 3u) || (a.n_frames & 3u)) return hipErrorInvalidValue;   // 4-frame chunks
+    // the modulated taps' buffer loads take 32-bit offsets into their (1024-position) rings
+    if ((uint64_t)kDtSize[DT_AP1A] * a.n * 4u >= (1ull << 32) || (uint64_t)kDtSize[DT_AP1B] * a.n * 4u >= (1ull << 32))
+        return hipErrorInvalidValue;
     const uint32_t threads = 64;      // one wave per workgroup: spreads small engines over all CUs
     const uint32_t blocks = (a.n + threads - 1) / threads;
     hipLaunchKernelGGL(dattorro_block_v4, dim3(blocks), dim3(threads), 0, s, a);

@@ -70,16 +70,19 @@ struct Tap {
 };
 
 // A modulated tank all-pass tap (verb.cpp:262-270): delay D + ex(t), with ex wave-uniform and
-// constant for 512 chunks at a time.  The prefetch loads BOTH groups of the next chunk's window,
-// computed from the next chunk's own offset, so no chunk branches on a step of ex: a load under
-// a branch made the compiler wait for every outstanding load (the whole prefetch) at the merge,
-// which cost more than the second 16-B load (+8 B/frame for the two taps).
+// constant for 512 chunks at a time.  The window of a chunk is 2 groups from its start q; while ex
+// is constant the next window starts 4 later, so its first group is this chunk's second one and
+// only one new group is loaded (as the fixed taps).  At a step of ex the first group is loaded
+// too.  That load is never under a branch (a load under a branch made the compiler wait for every
+// outstanding load, the whole prefetch, at the merge): it is a buffer load whose offset is past
+// the end of the ring when the group is carried -- no memory access, the returned zeros unused.
 template <int L, uint32_t D>
 struct ModTap {
     float c0, c1, c2, c3, n0, n1, n2, n3;             // this chunk's window
-    float p0, p1, p2, p3, r0, r1, r2, r3;             // the next chunk's, in flight
+    float p0, p1, p2, p3, r0, r1, r2, r3;             // the next chunk's groups, in flight
     float v[4];
     uint32_t q, qn;                                   // window start of this / the next chunk
+    bool carry;                                       // next window's first group = n0..n3
     __device__ __forceinline__ void prime(const DattorroArgs &a, uint32_t t0, uint32_t i) {
         q = t0 - (D + dt_ap1_extra(t0 & 0xFFFFu));
         const float4 g0 = *grp<L>(a, q >> 2, i), g1 = *grp<L>(a, (q >> 2) + 1u, i);
@@ -89,8 +92,16 @@ struct ModTap {
     __device__ __forceinline__ void prefetch(const DattorroArgs &a, uint32_t t0, uint32_t i) {
         const uint32_t t0n = t0 + 4u;
         qn = t0n - (D + dt_ap1_extra(t0n & 0xFFFFu));
-        const float4 g0 = *grp<L>(a, qn >> 2, i), g1 = *grp<L>(a, (qn >> 2) + 1u, i);
-        p0 = g0.x; p1 = g0.y; p2 = g0.z; p3 = g0.w;
+        const uint32_t gq = qn >> 2;
+        carry = gq == (q >> 2) + 1u;
+        const float4 g1 = *grp<L>(a, gq + 1u, i);
+        constexpr uint32_t gm = kDtSize[L] / 4u - 1u;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            a.ring[L], (short)0, (int)(uint32_t)((uint64_t)kDtSize[L] * a.n * 4u), 0x00020000);
+        const uint32_t off = carry ? 0xFFFFFFF0u : ((gq & gm) * a.n + i) * 16u;
+        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+        const u4 g0 = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        p0 = __uint_as_float(g0.x); p1 = __uint_as_float(g0.y); p2 = __uint_as_float(g0.z); p3 = __uint_as_float(g0.w);
         r0 = g1.x; r1 = g1.y; r2 = g1.z; r3 = g1.w;
     }
     __device__ __forceinline__ void resolve() {       // shift q & 3 (wave-uniform) by selects
@@ -104,7 +115,9 @@ struct ModTap {
         v[3] = sel4(s, c3, n0, n1, n2);
     }
     __device__ __forceinline__ void advance() {
-        c0 = p0; c1 = p1; c2 = p2; c3 = p3;
+        uint32_t k;                                   // VGPR copy of the uniform flag, as in resolve()
+        asm volatile("v_mov_b32 %0, %1" : "=v"(k) : "s"(carry ? 1u : 0u));
+        c0 = k ? n0 : p0; c1 = k ? n1 : p1; c2 = k ? n2 : p2; c3 = k ? n3 : p3;
         n0 = r0; n1 = r1; n2 = r2; n3 = r3;
         q = qn;
     }
