@@ -22,6 +22,7 @@
 // registers -- so every delay 0..47999 takes the same branch-free path.
 // Bound: HBM (32 B per stereo frame: ring write 8 + ring read 8 + I/O 16).
 #include <type_traits>
+#include <utility>
 
 #include "chorus_stage.h"
 
@@ -58,6 +59,16 @@ __device__ __forceinline__ float svf_tick(float in, float freq, float damp, floa
     return type == 1 ? o_band : (type == 2 ? o_high : (type == 3 ? o_notch : (type == 4 ? o_peak : o_low)));
 }
 
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>), unrolled at compile time
+template <class F, int... K>
+__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, K...>) {
+    (f(std::integral_constant<int, K>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 __device__ __forceinline__ uint32_t wrap48k(int64_t p) {
     const int64_t m = p % (int64_t)kFrMaxDelay;
     return (uint32_t)(m < 0 ? m + kFrMaxDelay : m);
@@ -65,7 +76,7 @@ __device__ __forceinline__ uint32_t wrap48k(int64_t p) {
 
 }  // namespace
 
-__global__ __launch_bounds__(kFrThreads) void fxrack_block_v1(FxRackArgs a) {
+__global__ __launch_bounds__(kFrThreads) void fxrack_block_v2(FxRackArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const uint32_t tid = threadIdx.x;
     const uint32_t wib = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
@@ -91,17 +102,22 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v1(FxRackArgs a) {
     const float fdrive = __uint_as_float(a.coef[FRC_FDRIVE * n + i]);
     const uint32_t ftype = a.coef[FRC_FTYPE * n + i];
     const float master = __uint_as_float(a.coef[FRC_MASTER * n + i]);
-    float dlow = __uint_as_float(a.state[FRS_DLOW * n + i]);
-    float dband = __uint_as_float(a.state[FRS_DBAND * n + i]);
-    float flow = __uint_as_float(a.state[FRS_FLOW * n + i]);
-    float fband = __uint_as_float(a.state[FRS_FBAND * n + i]);
+    // Lane roles (v2): both filters act on channel 0 only (Fx.h:88-108, DelayFx filter_), so the
+    // lane pair of an instance splits them: lane ch 0 ("D") runs DelayFx's filter_, lane ch 1 ("F")
+    // runs FxRack's filter1 one tick behind, on D's reverb output of the previous frame (a DPP
+    // broadcast).  A chunk of C frames is C + 1 ticks of ONE svf_tick per lane instead of two.
+    const float sfreq = ch ? ffreq : dfreq, sdamp = ch ? fdamp : ddamp, sdrive = ch ? fdrive : ddrive;
+    const uint32_t stype = ch ? ftype : 0u;
+    float slow = __uint_as_float(a.state[(ch ? FRS_FLOW : FRS_DLOW) * n + i]);
+    float sband = __uint_as_float(a.state[(ch ? FRS_FBAND : FRS_DBAND) * n + i]);
 
     // the wave's 32 rings (12.3 MB) get their own descriptor, so 32-bit offsets cover any n
     const ch::Rsrc rR = ch::rsrc(a.ring + (size_t)inst0 * kFrMaxDelay * 2, (uint64_t)min(32u, n - inst0) * kFrMaxDelay * 8);
     const ch::Rsrc rIn = ch::rsrc(a.in, (a.plane + (uint64_t)nf * n) * 4);
     const ch::Rsrc rOut = ch::rsrc(a.out, (a.plane + (uint64_t)nf * n) * 4);
     const uint32_t io_v = ch * (uint32_t)a.plane * 4u + i * 4u, frame_b = n * 4u;
-    const uint32_t out_v = valid ? io_v : 0xFFFFFFF0u;
+    // lane F holds channel 0's output, lane D channel 1's (0): each stores the other plane
+    const uint32_t out_v = valid ? (1u - ch) * (uint32_t)a.plane * 4u + i * 4u : 0xFFFFFFF0u;
     constexpr uint32_t kRing = kFrMaxDelay * 8u;        // bytes per instance ring
 
     float *win = lds + wib * kFrRegion;                 // [kFrSlots][64]
@@ -181,35 +197,43 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v1(FxRackArgs a) {
             xn[k] = k < Cn ? vv : 0.f;
         }
         load_window(t + kFrChunk);
-        // ---- 3. the frames ----
-        auto frame = [&](auto generic_tag, int k) {
+        // ---- 3. the frames: C + 1 ticks; tick k runs frame k's delay line (both lanes, own
+        //         channel) and one filter step per lane: D on frame k, F on frame k - 1 ----
+        float b0p = 0.f;                                // F's input: D's b0 of the previous tick
+        auto tick = [&](auto generic_tag, auto k_tag) {
             constexpr bool GENERIC = decltype(generic_tag)::value;
-            if (GENERIC && k >= C) return;
-            // DelayLine::Read: a at delay D, b at D + 1 (slots k - D - rel, one below)
-            const int sa = k - (int)D - rel;
-            const float av = wcol[sa * 64], bv = wcol[(sa - 1) * 64];
-            const float r = av + (bv - av) * frac;
-            const float w = x[k] + (feedback * r);      // DelayLine::Write
-            y[k] = w;
-            wcol[min(k - rel, kFrWin) * 64] = w;        // visible to later frames of this chunk
-            // DelayFx: filter_ (LowPass) on channel 0, in place
-            const float fr = svf_tick(r, dfreq, ddamp, ddrive, 0u, dlow, dband);
-            const float buf = ch == 0 ? fr : r;
-            const float a0 = (buf * dbal) + (x[k] * (1 - dbal));
-            // ReverbFx over the ReverbSc stub
-            const float vb = a0 * 0.8f;
-            const float b0 = (vb * rbal) + (a0 * (1 - rbal));
-            // FilterFx filter1 on channel 0; channel 1 of buf_c stays 0
-            const float c = svf_tick(b0, ffreq, fdamp, fdrive, ftype, flow, fband);
-            o[k] = (ch == 0 ? c : 0.0f) * master;
+            constexpr int k = decltype(k_tag)::value;
+            constexpr int kk = k < kFrChunk ? k : kFrChunk - 1;   // array index (tick kFrChunk has no frame)
+            if (GENERIC && k > C) return;
+            const bool frame_k = !GENERIC ? k < kFrChunk : k < C;   // this tick has a frame k
+            float r = 0.f;
+            if (frame_k) {
+                // DelayLine::Read: a at delay D, b at D + 1 (slots k - D - rel, one below)
+                const int sa = k - (int)D - rel;
+                const float av = wcol[sa * 64], bv = wcol[(sa - 1) * 64];
+                r = av + (bv - av) * frac;
+                const float w = x[kk] + (feedback * r); // DelayLine::Write
+                y[kk] = w;
+                wcol[min(k - rel, kFrWin) * 64] = w;    // visible to later frames of this chunk
+            }
+            float lo = slow, ba = sband;
+            const float so = svf_tick(ch ? b0p : r, sfreq, sdamp, sdrive, stype, lo, ba);
+            // D steps on frames 0..C-1, F on frames -1+1..C: the idle end of each lane keeps its state
+            const bool commit = ch ? k >= 1 : frame_k;
+            slow = commit ? lo : slow;
+            sband = commit ? ba : sband;
+            if constexpr (k >= 1) o[k - 1] = (ch ? so : 0.0f) * master;   // F: channel 0 of frame k-1
+            if (frame_k) {
+                // DelayFx: a = filtered * balance + in * (1 - balance) (D lane: channel 0)
+                const float a0 = (so * dbal) + (x[kk] * (1 - dbal));
+                // ReverbFx over the ReverbSc stub
+                const float vb = a0 * 0.8f;
+                const float b0 = (vb * rbal) + (a0 * (1 - rbal));
+                b0p = ch::pair_even(b0);
+            }
         };
-        if (C == kFrChunk) {
-#pragma unroll
-            for (int k = 0; k < kFrChunk; ++k) frame(std::false_type{}, k);
-        } else {
-#pragma unroll
-            for (int k = 0; k < kFrChunk; ++k) frame(std::true_type{}, k);
-        }
+        if (C == kFrChunk) static_for<kFrChunk + 1>([&](auto kt) { tick(std::false_type{}, kt); });
+        else static_for<kFrChunk + 1>([&](auto kt) { tick(std::true_type{}, kt); });
         // ---- 4. the chunk's writes -> LDS staging ([instance][frame][ch]); they leave as 128-B
         //         runs (8 lanes each) with the next chunk's flush ----
         {
@@ -224,11 +248,9 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v1(FxRackArgs a) {
         const uint32_t fl = (nf - 1u) / kFrChunk * kFrChunk;   // the last chunk
         flush(fl, (int)(nf - fl));
     }
-    if (!valid || ch != 0) return;
-    a.state[FRS_DLOW * n + i] = __float_as_uint(dlow);
-    a.state[FRS_DBAND * n + i] = __float_as_uint(dband);
-    a.state[FRS_FLOW * n + i] = __float_as_uint(flow);
-    a.state[FRS_FBAND * n + i] = __float_as_uint(fband);
+    if (!valid) return;
+    a.state[(ch ? FRS_FLOW : FRS_DLOW) * n + i] = __float_as_uint(slow);
+    a.state[(ch ? FRS_FBAND : FRS_DBAND) * n + i] = __float_as_uint(sband);
 }
 
 hipError_t launch_fxrack(const FxRackArgs &a, hipStream_t s) {
@@ -238,7 +260,7 @@ hipError_t launch_fxrack(const FxRackArgs &a, hipStream_t s) {
     const uint32_t waves = (a.n + 31) / 32;
     const uint32_t blocks = (waves + kFrThreads / 64 - 1) / (kFrThreads / 64);
     const size_t lds = (size_t)(kFrThreads / 64) * kFrRegion * sizeof(float);
-    hipLaunchKernelGGL(fxrack_block_v1, dim3(blocks), dim3(kFrThreads), lds, s, a);
+    hipLaunchKernelGGL(fxrack_block_v2, dim3(blocks), dim3(kFrThreads), lds, s, a);
     return hipGetLastError();
 }
 
