@@ -48,6 +48,8 @@ WORKLOADS = {
     "chain": ("chain", 16384, "configs[4]: 131,072 chorus->pitch-shift->dattorro chains = 16,384 per GPU x 8"),
     "pitchshift": ("pitchshift", 65536, "pitch-shift stage alone"),
     "fxrack": ("fxrack", 65536, "SURVEY 8f row 1: fxlib FxRack<2> (delay -> reverb -> filter -> master), 65,536 instances"),
+    "voice_poly": ("voice", 32768, "SURVEY 8a A17: configs[3] voices summed into Polyvoice buses of 8 voices "
+                   "(olfx_mix) inside every step"),
 }
 
 
@@ -168,11 +170,17 @@ def main():
     out = torch.empty((och, B, n), device=dev)
     if kind in VOICE_KINDS:   # NoteOn for every voice at block 0
         eng.note_events([(i, 1, 36 + (i * 7) % 61) for i in range(n)])
+    bus = None
+    if args.workload == "voice_poly":       # Polyvoice buses of 8 voices (Polyvoice.h:28-33)
+        eng.mix_config([list(range(g, min(g + 8, n))) for g in range(0, n, 8)])
+        bus = torch.zeros((B, eng.n_buses), device=dev)
     stream = torch.cuda.Stream(dev)        # dedicated non-default stream: events see the kernels
     torch.cuda.synchronize(dev)
 
     def step(k):
         eng.process(pool[k % pool_n], out=out, n_frames=B, stream=stream.cuda_stream)
+        if bus is not None:
+            eng.mix(out, bus, stream=stream.cuda_stream)
 
     for k in range(args.warmup):
         step(k)

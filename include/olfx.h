@@ -20,6 +20,9 @@
  *                                  (verb.cpp:258-325), ReverbFx glue (modules/fxlib/ReverbFx.cpp:11-27),
  *                                  ChorusEffect::process(sample) (README.md:124), SynthVoice::Process
  *                                  (SynthVoice.h:41-53) -- batched: n_frames x n_inst per call
+ *   olfx_mix_config / olfx_mix  <- Polyvoice::Process (modules/synthlib/Polyvoice.h:28-33) and
+ *                                  VoiceMap::Process (VoiceMap.h:64-73): voices added into one
+ *                                  frame, voice by voice
  *   olfx_last_error             <- (reference has none: void returns / NULL, verb.cpp:89-90,227)
  *
  * Audio layout (both host and device pointers accepted, see OLFX_IO_*):
@@ -210,6 +213,22 @@ int olfx_note_events(olfx_engine *e, const olfx_event *ev, uint32_t n);
 int olfx_process(olfx_engine *e, const float *in, float *out, uint32_t n_frames, int io_flags,
                  void *stream);
 
+/* ---- voice buses (voice engines): the Polyvoice / VoiceMap sums ----
+   Polyvoice::Process (modules/synthlib/Polyvoice.h:28-33) and VoiceMap::Process (VoiceMap.h:64-73)
+   add their voices' samples into the caller's frame one voice at a time (`*frame_out += sample`).
+   A bus is such a list.  olfx_mix_config sets the buses (host arrays, copied): bus b adds the
+   voices order[offsets[b] .. offsets[b+1]) in that order; offsets has n_buses + 1 entries and
+   starts at 0.  A voice may appear at most once over all buses (listed twice, the reference would
+   run it twice per frame); n_buses = 0 removes the buses.
+   olfx_mix adds, for every frame f and bus b, the bus's voice samples voice_out[f][v] into
+   bus_out[f][b] in list order: the reference's float adds, bit for bit.  voice_out is
+   [n_frames][n_inst] (this engine's olfx_process output); bus_out is [n_frames][n_buses] and is
+   accumulated into (the reference's caller zeroes its frame).  Both host (OLFX_IO_HOST) or both
+   device pointers (OLFX_IO_DEVICE: asynchronous on `stream`, as olfx_process). */
+int olfx_mix_config(olfx_engine *e, uint32_t n_buses, const uint32_t *offsets, const uint32_t *order);
+int olfx_mix(olfx_engine *e, const float *voice_out, float *bus_out, uint32_t n_frames, int io_flags,
+             void *stream);
+
 /* Block until all work queued by this engine is done. */
 int olfx_sync(olfx_engine *e);
 /* The engine's own non-blocking hipStream_t (valid until olfx_destroy). */
@@ -219,6 +238,7 @@ void *olfx_stream(const olfx_engine *e);
 uint32_t olfx_num_instances(const olfx_engine *e);
 int      olfx_kind(const olfx_engine *e);
 uint64_t olfx_frames_processed(const olfx_engine *e);   /* per instance, since create/reset */
+uint32_t olfx_num_buses(const olfx_engine *e);          /* voice buses (olfx_mix_config) */
 /* Algorithmic ("compulsory") HBM bytes per instance-frame of the dominant kernel, the figure
    bench.py's roofline uses. */
 double   olfx_algorithmic_bytes_per_frame(const olfx_engine *e);

@@ -21,6 +21,9 @@
  *                         NoteOff / UpdateMidiControl / UpdateHardwareControl / Process(frame_out)
  *   olfx::FxRack       <- ol::fx::FxRack<2> (Fx.h:398-492): Init / Process(frame_in, frame_out) /
  *                         UpdateMidiControl / UpdateHardwareControl
+ *   olfx::Polyvoice    <- ol::synth::Polyvoice (Polyvoice.h:11-86): the NoteOn / NoteOff allocation
+ *                         and the in-order sum of its SynthVoices
+ *   olfx::VoiceMap<CH> <- ol::synth::VoiceMap<CH> (VoiceMap.h:14-84)
  *   (the reverb: DattorroVerb_* by name, include/olfx_dattorro.h)
  *
  * Each per-instance setter takes the same value as the reference setter and applies it at the
@@ -205,6 +208,20 @@ public:
     void Process(float *frame_out, uint32_t n_frames, int io = OLFX_IO_HOST, void *stream = nullptr) {
         process(nullptr, frame_out, n_frames, io, stream);
     }
+    /* Buses: the Polyvoice / VoiceMap sums (Polyvoice.h:28-33, VoiceMap.h:64-73).  buses[b] lists the
+       voices bus b adds, in order; each voice at most once (olfx_mix_config). */
+    void SetBuses(const std::vector<std::vector<uint32_t>> &buses) {
+        std::vector<uint32_t> off(1, 0), order;
+        for (const auto &b : buses) {
+            order.insert(order.end(), b.begin(), b.end());
+            off.push_back((uint32_t)order.size());
+        }
+        check(olfx_mix_config(e_, (uint32_t)buses.size(), off.data(), order.data()), e_, "olfx_mix_config");
+    }
+    /* bus_out [F][n_buses] += each bus's voices of voice_out [1][F][N], added in bus order */
+    void Mix(const float *voice_out, float *bus_out, uint32_t n_frames, int io = OLFX_IO_HOST, void *stream = nullptr) {
+        check(olfx_mix(e_, voice_out, bus_out, n_frames, io, stream), e_, "olfx_mix");
+    }
 
 private:
     /* the engine queues note events itself and applies them, in call order, at the next process
@@ -289,8 +306,20 @@ public:
     void UpdateConfig(const float config[OLFX_VC_NPARAMS]) {
         for (uint32_t f = 0; f < OLFX_VC_NPARAMS; ++f) set(f, config[f]);
     }
-    void NoteOn(uint8_t midi_note, uint8_t velocity) { note(OLFX_EV_NOTE_ON, midi_note, velocity); }
-    void NoteOff(uint8_t midi_note, uint8_t velocity) { note(OLFX_EV_NOTE_OFF, midi_note, velocity); }
+    /* NoteOn / NoteOff also set Playing() and Gate() as SynthVoice.h:231-260 does (host side, at the
+       call; the engine applies the note at the next block boundary) */
+    void NoteOn(uint8_t midi_note, uint8_t velocity) {
+        note(OLFX_EV_NOTE_ON, midi_note, velocity);
+        gate_ = true;
+        playing_ = midi_note;
+    }
+    void NoteOff(uint8_t midi_note, uint8_t velocity) {
+        note(OLFX_EV_NOTE_OFF, midi_note, velocity);
+        gate_ = false;
+        playing_ = 0;
+    }
+    uint8_t Playing() const { return playing_; }
+    bool Gate() const { return gate_; }
     void UpdateMidiControl(uint8_t control_, uint8_t value) { control(control_, OLFX_CTL_MIDI, value); }
     void UpdateHardwareControl(uint8_t control_, float value) { control(control_, OLFX_CTL_HARDWARE, value); }
     /* frame_out[0] = this voice's sample (SynthVoice.h:41-53) */
@@ -298,6 +327,84 @@ public:
 
 private:
     int kind_;
+    uint8_t playing_ = 0;
+    bool gate_ = false;
+};
+
+/* ol::synth::Polyvoice (modules/synthlib/Polyvoice.h:11-86) over per-sample SynthVoices: NoteOn goes
+   to the first voice not Playing(), NoteOff to the first voice Playing() that note, and Process
+   adds each voice's sample into *frame_out in vector order (the caller zeroes it, as in the
+   reference).  The batch form of the same sum is VoiceBank::SetBuses / Mix (olfx_mix). */
+class Polyvoice {
+public:
+    explicit Polyvoice(std::vector<SynthVoice *> &voices) : voices_(voices) {}
+    void Init(float sample_rate) { for (SynthVoice *v : voices_) v->Init(sample_rate); }
+    void Process(float *frame_out) {
+        for (SynthVoice *v : voices_) {
+            v->Process(&frame_buffer_);
+            *frame_out += frame_buffer_;
+        }
+    }
+    void NoteOn(uint8_t note, uint8_t velocity) {
+        for (SynthVoice *v : voices_)
+            if (!v->Playing()) { v->NoteOn(note, velocity); break; }
+    }
+    void NoteOff(uint8_t note, uint8_t velocity) {
+        for (SynthVoice *v : voices_)
+            if (v->Playing() == note) { v->NoteOff(note, velocity); break; }
+    }
+    void UpdateMidiControl(uint8_t control, uint8_t value) { for (SynthVoice *v : voices_) v->UpdateMidiControl(control, value); }
+    void UpdateHardwareControl(uint8_t control, float value) { for (SynthVoice *v : voices_) v->UpdateHardwareControl(control, value); }
+    void UpdateConfig(const float config[OLFX_VC_NPARAMS]) { for (SynthVoice *v : voices_) v->UpdateConfig(config); }
+    uint8_t Playing() const { return 0; }      /* Polyvoice.h:79-81 */
+    bool Gate() const { return false; }        /* Polyvoice.h:83-85 */
+
+private:
+    std::vector<SynthVoice *> &voices_;
+    float frame_buffer_ = 0.f;
+};
+
+/* ol::synth::VoiceMap<CHANNEL_COUNT> (modules/synthlib/VoiceMap.h:14-84): note -> voice slots.
+   Process runs the voices of slots 0..127 in note order and adds frame_buffer[0..CH) into
+   frame_out (SynthVoice writes channel 0 only, so the other channels add the buffer's zeros). */
+template <int CHANNEL_COUNT>
+class VoiceMap {
+public:
+    void NoteOn(uint8_t note, uint8_t velocity) {
+        if (note < 128 && note2voice_[note].voice) note2voice_[note].voice->NoteOn(note, velocity);
+    }
+    void NoteOff(uint8_t note, uint8_t velocity) {
+        if (note < 128 && note2voice_[note].voice) note2voice_[note].voice->NoteOff(note, velocity);
+    }
+    void SetVoice(uint8_t channel, uint8_t note, SynthVoice *voice) {
+        if (note < 128 && channel < 16) {
+            note2voice_[note] = Slot{voice, channel, note};
+            channel2voice_[channel] = Slot{voice, channel, note};
+        }
+    }
+    void Init(float sample_rate) {
+        for (Slot &s : note2voice_)
+            if (s.voice) s.voice->Init(sample_rate);
+    }
+    void Process(float *frame_out) {
+        for (Slot &s : note2voice_) {
+            if (!s.voice) continue;
+            s.voice->Process(frame_buffer_);
+            for (int i = 0; i < CHANNEL_COUNT; ++i) frame_out[i] += frame_buffer_[i];
+        }
+    }
+    void UpdateMidiControl(uint8_t channel, uint8_t control, uint8_t value) {
+        if (channel < 16 && channel2voice_[channel].voice) channel2voice_[channel].voice->UpdateMidiControl(control, value);
+    }
+
+private:
+    struct Slot {
+        SynthVoice *voice = nullptr;
+        uint8_t channel = 0, note = 0;
+    };
+    Slot note2voice_[128] = {};
+    Slot channel2voice_[16] = {};
+    float frame_buffer_[CHANNEL_COUNT] = {};
 };
 
 /* ol::fx::FxRack<2> (Fx.h:398-492): delay -> reverb (ReverbSc stub) -> filter -> master volume.

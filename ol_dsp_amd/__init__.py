@@ -6,10 +6,10 @@ bench.py; it never computes audio on the CPU.
 """
 from ._lib import (IO_DEVICE, IO_HOST, KIND_CHAIN, KIND_CHORUS, KIND_DATTORRO, KIND_FXRACK, KIND_PITCHSHIFT,
                    KIND_VOICE, KIND_VOICE_MOOG, LIB_PATH, OlfxError, load)
-from .engine import KIND_NAMES, PARAMS, Engine, control_map, kind_info
+from .engine import KIND_NAMES, PARAMS, Engine, Polyvoice, control_map, kind_info
 
 __all__ = [
-    "Engine", "OlfxError", "PARAMS", "KIND_NAMES", "kind_info", "control_map", "load", "LIB_PATH",
+    "Engine", "Polyvoice", "OlfxError", "PARAMS", "KIND_NAMES", "kind_info", "control_map", "load", "LIB_PATH",
     "KIND_DATTORRO", "KIND_CHORUS", "KIND_PITCHSHIFT", "KIND_VOICE", "KIND_CHAIN", "KIND_FXRACK", "KIND_VOICE_MOOG",
     "IO_DEVICE", "IO_HOST",
 ]

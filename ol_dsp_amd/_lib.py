@@ -105,6 +105,9 @@ SIGNATURES = {
     "olfx_algorithmic_bytes_per_frame": (ctypes.c_double, [_P]),
     "olfx_kernel_name": (ctypes.c_char_p, [_P]),
     "olfx_last_error": (ctypes.c_char_p, [_P]),
+    "olfx_mix_config": (ctypes.c_int, [_P, _U32, ctypes.POINTER(_U32), ctypes.POINTER(_U32)]),
+    "olfx_mix": (ctypes.c_int, [_P, _P, _P, _U32, ctypes.c_int, _P]),
+    "olfx_num_buses": (_U32, [_P]),
     # include/olfx_sample.h: per-instance, per-sample operators (one block of latency)
     "olfx_sample_pool_config": (ctypes.c_int, [ctypes.c_int, _U32]),
     "olfx_sample_create": (ctypes.c_int, [ctypes.c_int, _F, ctypes.POINTER(_P)]),

@@ -1,0 +1,48 @@
+// ol_dsp_amd/csrc/mix.hip -- voice buses: the Polyvoice / VoiceMap sums.
+//
+// Reference (modules/synthlib): Polyvoice::Process (Polyvoice.h:28-33) runs each of its voices into
+// a one-sample buffer and adds it to the caller's frame, `*frame_out += frame_buffer`, voice by
+// voice in vector order; VoiceMap::Process (VoiceMap.h:64-73) does the same over its note slots
+// 0..127.  Per frame and bus that is the float sequence (((out + v0) + v1) + ...): one IEEE add per
+// voice, in order.  A bus here is that list of voices (CSR: order[off[b] .. off[b+1])), and the
+// kernel performs exactly those adds, so a bus is bit-identical to the reference's sum of the same
+// voice samples.
+//
+// HBM-bound and small beside the voice kernel: one 4-B read per voice sample, one 4-B read and one
+// 4-B write per bus sample.  One lane = (bus, frame), buses fastest: the lanes of a wave read the
+// voices of neighbouring buses in one frame row, so the lines one add step touches are the lines
+// the next step reuses (from the L1).
+#include "olfx_internal.h"
+
+namespace olfx {
+
+__global__ __launch_bounds__(256) void voice_mix_v1(MixArgs a) {
+    const uint32_t b = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t f = blockIdx.y;
+    if (b >= a.n_buses) return;
+    const float *row = a.in + (size_t)f * a.n;
+    float *dst = a.out + (size_t)f * a.n_buses + b;
+    const uint32_t k1 = a.off[b + 1];
+    uint32_t k = a.off[b];
+    float acc = *dst;
+    // four loads in flight per step; the adds stay in order
+    for (; k + 4 <= k1; k += 4) {
+        const float v0 = row[a.order[k]], v1 = row[a.order[k + 1]];
+        const float v2 = row[a.order[k + 2]], v3 = row[a.order[k + 3]];
+        acc = acc + v0;
+        acc = acc + v1;
+        acc = acc + v2;
+        acc = acc + v3;
+    }
+    for (; k < k1; ++k) acc = acc + row[a.order[k]];
+    *dst = acc;
+}
+
+hipError_t launch_mix(const MixArgs &a, hipStream_t s) {
+    if (a.n_buses == 0 || a.n_frames == 0) return hipSuccess;
+    const dim3 grid((a.n_buses + 255) / 256, a.n_frames);
+    hipLaunchKernelGGL(voice_mix_v1, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace olfx

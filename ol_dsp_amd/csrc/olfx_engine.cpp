@@ -377,6 +377,9 @@ struct olfx_engine {
     // voice
     float *vc_state = nullptr, *vc_coef = nullptr;
     std::vector<olfx_event> events;
+    // voice buses (olfx_mix_config): [n_buses + 1] offsets, then the voice lists
+    uint32_t *mix_dev = nullptr;
+    uint32_t n_buses = 0;
     std::vector<float> h_vstate;                         // host copy for event application
 
     // host-pointer I/O staging
@@ -828,6 +831,7 @@ int olfx_destroy(olfx_engine *e) {
     if (e->h_out) (void)hipHostFree(e->h_out);
     if (e->d_in) (void)hipFree(e->d_in);
     if (e->d_out) (void)hipFree(e->d_out);
+    if (e->mix_dev) (void)hipFree(e->mix_dev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return OLFX_OK;
@@ -1008,6 +1012,81 @@ int olfx_process(olfx_engine *e, const float *in, float *out, uint32_t n_frames,
     return OLFX_OK;
 }
 
+// ---- voice buses: Polyvoice::Process / VoiceMap::Process (Polyvoice.h:28-33, VoiceMap.h:64-73) ----
+int olfx_mix_config(olfx_engine *e, uint32_t n_buses, const uint32_t *offsets, const uint32_t *order) {
+    if (!e) return OLFX_E_ARG;
+    if (!is_voice_kind(e->kind)) return e->fail(OLFX_E_STATE, "olfx_mix_config: not a voice engine");
+    std::vector<uint32_t> h;
+    if (n_buses) {
+        if (!offsets || offsets[0] != 0) return e->fail(OLFX_E_ARG, "olfx_mix_config: offsets must start at 0");
+        for (uint32_t b = 0; b < n_buses; ++b)
+            if (offsets[b + 1] < offsets[b])
+                return e->fail(OLFX_E_ARG, "olfx_mix_config: offsets decrease at bus %u", b);
+        const uint32_t len = offsets[n_buses];
+        if (len > e->n)
+            return e->fail(OLFX_E_ARG, "olfx_mix_config: %u entries for %u voices (each voice at most once)", len, e->n);
+        if (len && !order) return e->fail(OLFX_E_ARG, "olfx_mix_config: null order");
+        std::vector<uint8_t> seen(e->n, 0);
+        for (uint32_t k = 0; k < len; ++k) {
+            if (order[k] >= e->n)
+                return e->fail(OLFX_E_ARG, "olfx_mix_config: order[%u] = %u out of range", k, order[k]);
+            // listed twice, the reference would run the voice twice per frame (Polyvoice.h:28-33)
+            if (seen[order[k]]++) return e->fail(OLFX_E_ARG, "olfx_mix_config: voice %u listed twice", order[k]);
+        }
+        h.assign(offsets, offsets + n_buses + 1);
+        h.insert(h.end(), order, order + len);
+    }
+    HIPCHK(e, hipSetDevice(e->device));
+    if (e->mix_dev) {                       // a mix still in flight may read the old lists
+        HIPCHK(e, hipDeviceSynchronize());
+        HIPCHK(e, hipFree(e->mix_dev));
+        e->mix_dev = nullptr;
+    }
+    e->n_buses = 0;
+    if (!n_buses) return OLFX_OK;
+    HIPCHK(e, hipMalloc((void **)&e->mix_dev, h.size() * 4));
+    HIPCHK(e, hipMemcpy(e->mix_dev, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    e->n_buses = n_buses;
+    return OLFX_OK;
+}
+
+int olfx_mix(olfx_engine *e, const float *voice_out, float *bus_out, uint32_t n_frames, int io_flags, void *stream) {
+    if (!e) return OLFX_E_ARG;
+    if (!e->n_buses) return e->fail(OLFX_E_STATE, "olfx_mix: no buses (olfx_mix_config)");
+    if (n_frames == 0) return OLFX_OK;
+    if (!voice_out || !bus_out) return e->fail(OLFX_E_ARG, "olfx_mix: null buffer");
+    if (io_flags != OLFX_IO_DEVICE && io_flags != OLFX_IO_HOST) return e->fail(OLFX_E_ARG, "olfx_mix: bad io_flags");
+    HIPCHK(e, hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    MixArgs a{};
+    a.off = e->mix_dev;
+    a.order = e->mix_dev + e->n_buses + 1;
+    a.n = e->n;
+    a.n_buses = e->n_buses;
+    a.n_frames = n_frames;
+    const size_t fin = (size_t)n_frames * e->n, fout = (size_t)n_frames * e->n_buses;
+    hipError_t r;
+    if (io_flags == OLFX_IO_HOST) {
+        const int rc = ensure_staging(e, fin, fout);
+        if (rc) return rc;
+        std::memcpy(e->h_in, voice_out, fin * 4);
+        std::memcpy(e->h_out, bus_out, fout * 4);
+        HIPCHK(e, hipMemcpyAsync(e->d_in, e->h_in, fin * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(e, hipMemcpyAsync(e->d_out, e->h_out, fout * 4, hipMemcpyHostToDevice, s));
+        a.in = e->d_in;
+        a.out = e->d_out;
+        if ((r = launch_mix(a, s)) != hipSuccess) return e->hip_fail(r, "mix launch");
+        HIPCHK(e, hipMemcpyAsync(e->h_out, e->d_out, fout * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(e, hipStreamSynchronize(s));
+        std::memcpy(bus_out, e->h_out, fout * 4);
+        return OLFX_OK;
+    }
+    a.in = voice_out;
+    a.out = bus_out;
+    if ((r = launch_mix(a, s)) != hipSuccess) return e->hip_fail(r, "mix launch");
+    return OLFX_OK;
+}
+
 int olfx_sync(olfx_engine *e) {
     if (!e) return OLFX_E_ARG;
     HIPCHK(e, hipSetDevice(e->device));
@@ -1021,6 +1100,7 @@ void *olfx_stream(const olfx_engine *e) { return e ? (void *)e->stream : nullptr
 uint32_t olfx_num_instances(const olfx_engine *e) { return e ? e->n : 0; }
 int olfx_kind(const olfx_engine *e) { return e ? e->kind : 0; }
 uint64_t olfx_frames_processed(const olfx_engine *e) { return e ? e->frames : 0; }
+uint32_t olfx_num_buses(const olfx_engine *e) { return e ? e->n_buses : 0; }
 
 double olfx_algorithmic_bytes_per_frame(const olfx_engine *e) {
     if (!e) return 0.0;
@@ -1043,7 +1123,7 @@ const char *olfx_kernel_name(const olfx_engine *e) {
     case OLFX_KIND_DATTORRO: return "dattorro_block_v4";
     case OLFX_KIND_CHORUS:
     case OLFX_KIND_PITCHSHIFT: return OLFX_CHORUS_V == 11 ? "chorus_block_v11" : "chorus_block_v10";
-    case OLFX_KIND_VOICE: return "voice_block_v4";
+    case OLFX_KIND_VOICE: return OLFX_VOICE_V == 5 ? "voice_block_v5" : "voice_block_v4";
     case OLFX_KIND_VOICE_MOOG: return "voice_block_v4<true>";
     case OLFX_KIND_CHAIN: return "chain_block_v1";
     case OLFX_KIND_FXRACK: return "fxrack_block_v2";

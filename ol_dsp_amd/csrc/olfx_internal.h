@@ -16,6 +16,11 @@
 #ifndef OLFX_CHORUS_V
 #define OLFX_CHORUS_V 11
 #endif
+// Svf voice kernel generation: 5 = four balanced role waves (voice_block_v5), 4 = three role
+// waves (voice_block_v4).  A build knob for A/B timing.
+#ifndef OLFX_VOICE_V
+#define OLFX_VOICE_V 5
+#endif
 
 namespace olfx {
 
@@ -228,6 +233,20 @@ hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s);
 hipError_t launch_chain(const ChainArgs &a, hipStream_t s);
 hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s);
 hipError_t launch_voice(const VoiceArgs &a, hipStream_t s);
+
+// ----------------------------------------------------------------------------------------------
+// Voice buses (mix.hip): the Polyvoice / VoiceMap sums.  Bus b of frame f = out[f][b] plus the
+// voices order[off[b] .. off[b+1]) of in[f][*], added one at a time in that order
+// (modules/synthlib/Polyvoice.h:28-33, VoiceMap.h:64-73).
+// ----------------------------------------------------------------------------------------------
+struct MixArgs {
+    const float *in;            // [n_frames][n] voice outputs
+    float *out;                 // [n_frames][n_buses], accumulated into
+    const uint32_t *off;        // [n_buses + 1]
+    const uint32_t *order;      // [off[n_buses]] voice indices
+    uint32_t n, n_buses, n_frames;
+};
+hipError_t launch_mix(const MixArgs &a, hipStream_t s);
 
 // host side: record a global error message (olfx_last_error(NULL))
 void internal_set_error(const char *msg);

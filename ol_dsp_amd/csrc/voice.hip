@@ -333,10 +333,176 @@ __global__ __launch_bounds__(MOOG ? 128 : 192) void voice_block_v4(VoiceArgs a) 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// voice_block_v5 (SvfFilter voices, OLFX_VOICE_V 5): v4's arithmetic, operation for operation, over
+// FOUR role waves per workgroup of 64 voices, balanced across the SIMDs of a CU.
+//   v4's roles cost about 40 / 34 / 30 VALU instructions per sample (amp / cutoff / filter; with
+//   -ffp-contract=off every a*b+c is two).  Two workgroups share a CU: six waves on four SIMDs, so
+//   two SIMDs carry two roles each and the per-chunk barrier holds every wave to the busiest.
+//   v5's roles:
+//     ENV  : both envelopes, portamento, the phase accumulator, the cutoff sum -> (t, inc, amp, fc_in)
+//     OSC  : the polyBLEP saw from (t, inc)                                     -> (src, amp)
+//     FREQ : Svf::SetFreq(fc_in)                                                -> (fq, damp)
+//     FILT : the two Svf passes, Low() * amp, the output store
+//   about 22 / 23 / 30 / 29 instructions: eight waves per CU, two per SIMD.  Two co-resident
+//   workgroups whose roles differ by two on every SIMD pair ENV with FREQ and OSC with FILT; the
+//   rotation is taken from the workgroup's slot on its CU (OLFX_VC_ROT).
+// A three-stage pipeline over 16-sample chunks: at step k ENV makes chunk k, OSC and FREQ chunk
+// k-1, FILT chunk k-2; one barrier per step; 64 KB of LDS per workgroup.
+// ---------------------------------------------------------------------------------------------
+#ifndef OLFX_VC_ROT
+#define OLFX_VC_ROT 1   // 0: role = wave; 1: rotated by HW_ID.TG_ID parity; 2: by (blockIdx >> 8)
+#endif                  // parity; 3: roles follow the SIMDs (HW_ID.SIMD_ID), rotated as 1
+
+__global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
+    __shared__ float4 eq[2][kVcChunk][64];      // ENV -> OSC, FREQ: (t, inc, amp, fc_in)
+    __shared__ float2 sq[2][kVcChunk][64];      // OSC -> FILT: (src, amp)
+    __shared__ float2 fdq[2][kVcChunk][64];     // FREQ -> FILT: (fq, damp)
+    const uint32_t n = a.n;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t i0 = blockIdx.x * 64 + lane;
+    const uint32_t i = i0 < n ? i0 : n - 1;      // dead lanes mirror voice n-1, as in v4
+    const uint32_t nf = a.n_frames;
+    const uint32_t nsteps = (nf + kVcChunk - 1) / kVcChunk + 2;
+    const float *c = a.coef;
+    float *s = a.state;
+#if OLFX_VC_ROT == 0
+    const uint32_t role = wave;
+#else
+    // every wave publishes its HW_ID (one word per wave of chunk buffer 1, first written at step 1)
+    uint32_t *ids = reinterpret_cast<uint32_t *>(&eq[1][0][0]);
+    if (lane == 0) ids[wave] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+    __syncthreads();
+#if OLFX_VC_ROT == 2
+    const uint32_t rot = ((blockIdx.x >> 8) & 1u) << 1;
+#else
+    const uint32_t rot = ((ids[0] >> 16) & 1u) << 1;          // TG_ID parity: the slot on the CU
+#endif
+#if OLFX_VC_ROT == 3
+    uint32_t seen = 0;
+    for (uint32_t w = 0; w < 4; ++w) seen |= 1u << ((ids[w] >> 4) & 3u);
+    const uint32_t base = seen == 15u ? (ids[wave] >> 4) & 3u : wave;
+#else
+    const uint32_t base = wave;
+#endif
+    const uint32_t role = (uint32_t)__builtin_amdgcn_readfirstlane((int)((base + rot) & 3u));
+#endif
+    auto len = [&](uint32_t k) {             // frames of chunk k (the last may be short)
+        const uint32_t f0 = k * kVcChunk;
+        return nf - f0 < (uint32_t)kVcChunk ? nf - f0 : (uint32_t)kVcChunk;
+    };
+
+    if (role == 0) {
+        // ---- ENV (SynthVoice.h:42-48): Adsr x2, Port, the oscillator's phase, the cutoff sum ----
+        const uint32_t flags0 = __float_as_uint(s[VCS_FLAGS * n + i]);
+        const bool gate = (flags0 >> 8) & 1u;
+        bool gprev_a = (flags0 >> 6) & 1u, gprev_f = (flags0 >> 7) & 1u;
+        const float amp_amt = c[VCC_AMP_AMT * n + i], port_c = c[VCC_PORT_COEF * n + i];
+        const float inv_sr = c[VCC_INV_SR * n + i], freq = s[VCS_FREQ * n + i];
+        const float cutoff = c[VCC_CUTOFF * n + i], fenv_amt = c[VCC_FENV_AMT * n + i];
+        float phase = s[VCS_PHASE * n + i], port_z = s[VCS_PORT_Z * n + i];
+        Env ea, ef;
+        ea.begin(gate, gprev_a, flags0 & 7u, s[VCS_ENVA_X * n + i], c[VCC_ATK_D0A * n + i],
+                 c[VCC_ATK_TGT_A * n + i], c[VCC_DEC_D0A * n + i], c[VCC_REL_D0A * n + i], c[VCC_SUS_A * n + i]);
+        ef.begin(gate, gprev_f, (flags0 >> 3) & 7u, s[VCS_ENVF_X * n + i], c[VCC_ATK_D0F * n + i],
+                 c[VCC_ATK_TGT_F * n + i], c[VCC_DEC_D0F * n + i], c[VCC_REL_D0F * n + i], c[VCC_SUS_F * n + i]);
+        for (uint32_t k = 0; k < nsteps; ++k) {
+            if (k + 2 < nsteps) {
+                float4 *qo = &eq[k & 1][0][lane];
+                for_chunk(len(k), [&](uint32_t j) {
+                    const float amp = ea.step() * amp_amt;
+                    port_z = freq + port_c * (port_z - freq);     // Port::Process (Portamento.h:218-221)
+                    const float inc = port_z * inv_sr;             // Oscillator::SetFreq
+                    const float t = phase;                         // Oscillator::Process reads, then advances
+                    phase += inc;
+                    phase = phase > 1.0f ? phase - 1.0f : phase;
+                    const float fe = ef.step();
+                    qo[j * 64] = make_float4(t, inc, amp, cutoff + ((fe * 20000.0f) * fenv_amt));
+                });
+            }
+            __syncthreads();
+        }
+        s[VCS_PHASE * n + i] = phase;
+        s[VCS_PORT_Z * n + i] = port_z;
+        s[VCS_ENVA_X * n + i] = ea.x;
+        s[VCS_ENVF_X * n + i] = ef.x;
+        s[VCS_FLAGS * n + i] = __uint_as_float(ea.mode | ef.mode << 3 | (uint32_t)gprev_a << 6 |
+                                               (uint32_t)gprev_f << 7 | (uint32_t)gate << 8);
+    } else if (role == 1) {
+        // ---- OSC: Oscillator::Process, WAVE_POLYBLEP_SAW, amp 0.5 ----
+        for (uint32_t k = 0; k < nsteps; ++k) {
+            if (k >= 1 && k + 1 < nsteps) {
+                const float4 *qi = &eq[(k - 1) & 1][0][lane];
+                float2 *qo = &sq[(k - 1) & 1][0][lane];
+                for_chunk(len(k - 1), [&](uint32_t j) {
+                    const float4 v = qi[j * 64];
+                    float o = (2.0f * v.x) - 1.0f;
+                    o -= polyblep(v.y, v.x);
+                    o *= -1.0f;
+                    qo[j * 64] = make_float2(o * 0.5f, v.z);
+                });
+            }
+            __syncthreads();
+        }
+    } else if (role == 2) {
+        // ---- FREQ: Svf::SetFreq (its divisions use the hardware reciprocal, as in v4) ----
+        const float damp_res = c[VCC_DAMP_RES * n + i], fc_max = c[VCC_FC_MAX * n + i];
+        const float inv_2sr = 1.0f / (c[VCC_SR * n + i] * 2.0f);
+        for (uint32_t k = 0; k < nsteps; ++k) {
+            if (k >= 1 && k + 1 < nsteps) {
+                const float4 *qi = &eq[(k - 1) & 1][0][lane];
+                float2 *qo = &fdq[(k - 1) & 1][0][lane];
+                for_chunk(len(k - 1), [&](uint32_t j) {
+                    const float fc = fminf(fmaxf(qi[j * 64].w, 1.0e-6f), fc_max);
+                    const float fcn = fc * inv_2sr;
+                    const float arg = 0.25f < fcn ? 0.25f : fcn;
+                    const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
+                    const float lim = 2.0f * __builtin_amdgcn_rcpf(fq) - fq * 0.5f;
+                    const float dlim = 2.0f < lim ? 2.0f : lim;
+                    qo[j * 64] = make_float2(fq, damp_res < dlim ? damp_res : dlim);
+                });
+            }
+            __syncthreads();
+        }
+    } else {
+        // ---- FILT: Svf::Process; Low() = the average of the two passes' low outputs; * amp ----
+        const float drive = c[VCC_DRIVE * n + i];
+        float low = s[VCS_LOW * n + i], band = s[VCS_BAND * n + i];
+        float *out = a.out + i;
+        for (uint32_t k = 0; k < nsteps; ++k) {
+            if (k >= 2) {
+                const uint32_t f0 = (k - 2) * kVcChunk;
+                const float2 *qs = &sq[k & 1][0][lane];        // chunk k-2: (k-2) & 1 == k & 1
+                const float2 *qf = &fdq[k & 1][0][lane];
+                for_chunk(len(k - 2), [&](uint32_t j) {
+                    const float2 sa = qs[j * 64], fd = qf[j * 64];
+                    const float src = sa.x, fq = fd.x, damp = fd.y;
+                    float notch = src - damp * band;
+                    low = low + fq * band;
+                    float high = notch - low;
+                    band = fq * high + band - drive * band * band * band;
+                    float out_low = 0.5f * low;
+                    notch = src - damp * band;
+                    low = low + fq * band;
+                    high = notch - low;
+                    band = fq * high + band - drive * band * band * band;
+                    out_low += 0.5f * low;
+                    out[(size_t)(f0 + j) * n] = out_low * sa.y;
+                });
+            }
+            __syncthreads();
+        }
+        s[VCS_LOW * n + i] = low;
+        s[VCS_BAND * n + i] = band;
+    }
+}
+
 hipError_t launch_voice(const VoiceArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
     const dim3 grid((a.n + 63) / 64);     // 64 voices per workgroup, one wave per role
     if (a.moog) hipLaunchKernelGGL(voice_block_v4<true>, grid, dim3(128), 0, s, a);
+    else if (OLFX_VOICE_V == 5) hipLaunchKernelGGL(voice_block_v5, grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(voice_block_v4<false>, grid, dim3(192), 0, s, a);
     return hipGetLastError();
 }

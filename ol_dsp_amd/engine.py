@@ -9,6 +9,7 @@ Reference surfaces this mirrors (per instance, batched here):
   DattorroVerb_create/set*/process/getLeft/getRight   libs/dattorro-verb/verb.h:5-26
   ChorusEffect init/setDepth/setRate/process           README.md:114-128 (+ RNBO params)
   SynthVoice Init/UpdateConfig/NoteOn/NoteOff/Process  modules/synthlib/SynthVoice.h:31-256
+  Polyvoice NoteOn/NoteOff/Process (voice buses)       modules/synthlib/Polyvoice.h:11-86
 """
 from __future__ import annotations
 
@@ -198,6 +199,51 @@ class Engine:
                                     ctypes.c_void_p(stream)), self._h)
         return out
 
+    # ---- voice buses: the Polyvoice / VoiceMap sums (Polyvoice.h:28-33, VoiceMap.h:64-73) ----
+    def mix_config(self, buses: Sequence[Sequence[int]]) -> None:
+        """Bus b adds the voices buses[b] in list order, one float add per voice (the reference's
+        `*frame_out += frame_buffer`); each voice at most once over all buses; [] removes them."""
+        lists = [np.asarray(b, dtype=np.uint32).ravel() for b in buses]
+        off = np.zeros(len(lists) + 1, np.uint32)
+        if lists:
+            off[1:] = np.cumsum([len(b) for b in lists])
+        order = np.ascontiguousarray(np.concatenate(lists) if off[-1] else np.zeros(1, np.uint32))
+        u32 = ctypes.POINTER(ctypes.c_uint32)
+        check(self.lib.olfx_mix_config(self._h, len(lists), off.ctypes.data_as(u32), order.ctypes.data_as(u32)),
+              self._h)
+
+    @property
+    def n_buses(self) -> int:
+        return int(self.lib.olfx_num_buses(self._h))
+
+    def mix(self, voice_out, bus_out=None, stream=None):
+        """bus_out [frames][n_buses] += each bus's voices of voice_out ([1][frames][n] or
+        [frames][n]), added in bus order.  Torch CUDA tensors (device path) or numpy arrays (host
+        path); bus_out defaults to zeros."""
+        nb = self.n_buses
+        frames = int(voice_out.shape[-2])
+        assert tuple(voice_out.shape[-2:]) == (frames, self.n), (tuple(voice_out.shape), self.n)
+        if _is_torch(voice_out):
+            import torch
+            assert voice_out.is_cuda and voice_out.dtype == torch.float32 and voice_out.is_contiguous()
+            if bus_out is None:
+                bus_out = torch.zeros((frames, nb), dtype=torch.float32, device=voice_out.device)
+            assert bus_out.is_contiguous() and tuple(bus_out.shape) == (frames, nb)
+            if stream is None:
+                stream = torch.cuda.current_stream(voice_out.device).cuda_stream
+            check(self.lib.olfx_mix(self._h, ctypes.c_void_p(voice_out.data_ptr()), ctypes.c_void_p(bus_out.data_ptr()),
+                                    frames, _lib.IO_DEVICE, ctypes.c_void_p(stream)), self._h)
+            return bus_out
+        v = np.ascontiguousarray(np.asarray(voice_out, dtype=np.float32))
+        if bus_out is None:
+            bus_out = np.zeros((frames, nb), np.float32)
+        assert bus_out.dtype == np.float32 and bus_out.flags.c_contiguous and bus_out.shape == (frames, nb)
+        if stream is None:
+            stream = self.lib.olfx_stream(self._h)
+        check(self.lib.olfx_mix(self._h, ctypes.c_void_p(v.ctypes.data), ctypes.c_void_p(bus_out.ctypes.data),
+                                frames, _lib.IO_HOST, ctypes.c_void_p(stream)), self._h)
+        return bus_out
+
     def sync(self) -> None:
         check(self.lib.olfx_sync(self._h), self._h)
 
@@ -232,3 +278,38 @@ def control_map(kind, control: int, value: float, source: str = "midi"):
         return "update_only", val.value
     return PARAMS[k][field.value], val.value
 
+
+
+class Polyvoice:
+    """ol::synth::Polyvoice (modules/synthlib/Polyvoice.h:11-86), batched: each group of voices of a
+    voice Engine is one Polyvoice and one bus.  note_on takes the group's first voice not Playing(),
+    note_off its first voice Playing() that note (Polyvoice.h:35-51; SynthVoice::Playing() is the
+    last NoteOn's note and 0 after NoteOff, SynthVoice.h:245-260, tracked here on the host).
+    process() runs the voice block, then adds each group's voices into its bus in group order
+    (olfx_mix): bit-identical to Polyvoice::Process over the same voice samples."""
+
+    def __init__(self, engine: Engine, groups: Sequence[Sequence[int]]):
+        self.engine = engine
+        self.groups = [[int(v) for v in g] for g in groups]
+        self.playing = np.zeros(engine.n, np.int64)
+        engine.mix_config(self.groups)
+
+    def note_on(self, group: int, note: int, velocity: int = 100) -> None:
+        for v in self.groups[group]:
+            if not self.playing[v]:
+                self.engine.note_events([(v, 1, note, velocity)])
+                self.playing[v] = note
+                return
+
+    def note_off(self, group: int, note: int, velocity: int = 0) -> None:
+        for v in self.groups[group]:
+            if self.playing[v] == note:
+                self.engine.note_events([(v, 0, note, velocity)])
+                self.playing[v] = 0
+                return
+
+    def process(self, voice_out, bus_out=None, stream=None):
+        """One block: voice_out [1][frames][n] is written, the buses [frames][groups] are added into
+        (zeros if None) and returned."""
+        self.engine.process(None, out=voice_out, stream=stream)
+        return self.engine.mix(voice_out, bus_out, stream=stream)

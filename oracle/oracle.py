@@ -254,3 +254,19 @@ class FxRack(_Bank):
         out = np.empty_like(x)
         assert self.L.oracle_fxrack_process(self.h, _pf(x), _pf(out), frames, threads) == 0
         return out
+
+
+def mix_ref(voice_out: np.ndarray, buses, bus_init=None) -> np.ndarray:
+    """Polyvoice::Process (modules/synthlib/Polyvoice.h:28-33) / VoiceMap::Process (VoiceMap.h:64-73):
+    per frame, `*frame_out += frame_buffer` voice by voice, in list order -- float32 adds, one
+    rounding each, vectorised over frames only.  voice_out [1][F][n] or [F][n] -> [F][len(buses)]."""
+    v = np.asarray(voice_out, np.float32)
+    v = v.reshape(v.shape[-2], v.shape[-1])
+    out = (np.zeros((v.shape[0], len(buses)), np.float32) if bus_init is None
+           else np.array(bus_init, dtype=np.float32, copy=True))
+    for b, voices in enumerate(buses):
+        acc = out[:, b].copy()
+        for i in voices:
+            acc = acc + v[:, int(i)]
+        out[:, b] = acc
+    return out

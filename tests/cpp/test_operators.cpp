@@ -421,6 +421,57 @@ TEST(PerSample, LockstepViolationThrows) {
     EXPECT_EQ(code, OLFX_E_STATE);
 }
 
+/* ol::synth::Polyvoice over per-sample SynthVoices (Polyvoice.h:11-86): NoteOn takes the first voice
+   not playing, NoteOff the first playing that note, Process adds the voices in order.  Equals the
+   voice bank with the same notes and buses (olfx_mix), one block later, bit for bit. */
+TEST(PerSample, PolyvoiceEqualsBankBuses) {
+    const uint32_t B = 256, F = 4 * B;
+    const float cfg[OLFX_VC_NPARAMS] = {3000.f, 0.4f, 0.1f, 0.5f, 0.01f, 0.f, 0.2f, 0.5f, 0.1f,
+                                        1.f, 0.005f, 0.f, 0.1f, 0.7f, 0.05f, 0.f};
+    olfx::SynthVoice v[6];
+    std::vector<olfx::SynthVoice *> ga = {&v[0], &v[1], &v[2]}, gb = {&v[3], &v[4], &v[5]};
+    olfx::Polyvoice pa(ga), pb(gb);
+    pa.Init(48000.f);
+    pb.Init(48000.f);
+    pa.UpdateConfig(cfg);
+    pb.UpdateConfig(cfg);
+    pa.NoteOn(60, 100);
+    pa.NoteOn(64, 100);
+    pb.NoteOn(67, 100);
+    EXPECT_TRUE(v[0].Playing() == 60 && v[1].Playing() == 64 && v[2].Playing() == 0 && v[3].Playing() == 67);
+    std::vector<float> y(2 * (size_t)F);
+    for (uint32_t t = 0; t < F; ++t) {
+        if (t == B + 9) pa.NoteOff(60, 0);        /* lands at frame 2B */
+        float a = 0.f, b = 0.f;                   /* the caller zeroes the frame */
+        pa.Process(&a);
+        pb.Process(&b);
+        y[2 * (size_t)t] = a;
+        y[2 * (size_t)t + 1] = b;
+    }
+    EXPECT_TRUE(v[0].Playing() == 0 && !v[0].Gate() && v[1].Gate());
+    olfx::VoiceBank bank(6, 48000.f, B);
+    for (uint32_t i = 0; i < 6; ++i) bank.UpdateConfig(i, cfg);
+    bank.NoteOn(0, 60, 100);
+    bank.NoteOn(1, 64, 100);
+    bank.NoteOn(3, 67, 100);
+    bank.SetBuses({{0, 1, 2}, {3, 4, 5}});
+    std::vector<float> vo((size_t)B * 6), bo(2 * (size_t)(F - B), 0.f);
+    for (uint32_t blk = 0; blk < 3; ++blk) {
+        if (blk == 2) bank.NoteOff(0, 60, 0);
+        bank.Process(vo.data(), B);
+        bank.Mix(vo.data(), bo.data() + (size_t)blk * B * 2, B);
+    }
+    bool ok = true;
+    for (uint32_t t = 0; t < F && ok; ++t)
+        for (uint32_t g = 0; g < 2 && ok; ++g) {
+            const float want = t < B ? 0.f : bo[(size_t)(t - B) * 2 + g];
+            ok = std::memcmp(&y[2 * (size_t)t + g], &want, 4) == 0;
+            if (!ok) std::printf("  first mismatch t=%u bus=%u: %.9g vs %.9g\n", t, g, y[2 * (size_t)t + g], want);
+        }
+    EXPECT_TRUE(ok);
+    EXPECT_TRUE(bo[(size_t)100 * 2] != 0.f && bo[(size_t)100 * 2 + 1] != 0.f);
+}
+
 int main() {
     for (auto &c : cases()) {
         int before = g_failures;

@@ -47,4 +47,4 @@ def test_cpp_operators_on_gpu():
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=600)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "13 tests, 0 failures" in r.stdout
+    assert "14 tests, 0 failures" in r.stdout

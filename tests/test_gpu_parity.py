@@ -529,3 +529,103 @@ def test_control_changes_equal_mapped_params(cuda):
         v.note_events([(i, 1, 48 + 5 * i) for i in range(nv)])
     a, b = _voice_run(v1, 1024, cuda), _voice_run(v2, 1024, cuda)
     assert bits_equal(a, b), first_mismatch(a, b)
+
+
+# ---------------------------------------------------------- voice buses: Polyvoice (8a A17)
+def test_mix_buses_bit_exact(cuda):
+    """olfx_mix adds each bus's voices in list order, one float add per voice: bit-identical to the
+    reference's `*frame_out += frame_buffer` (Polyvoice.h:28-33) over the same voice samples, on
+    the device and through host buffers, accumulating into a non-zero bus buffer; ragged buses."""
+    import torch
+    n = 300
+    rng = np.random.default_rng(5)
+    cfg = voice_configs(rng, n)
+    cfg[2] *= 0.25              # moderate Svf drive: every voice stays finite (NaN payloads differ)
+    notes = [int(v) for v in rng.integers(36, 97, n)]
+    e, _ = _voice_pair(n, cfg, notes)
+    perm = [int(v) for v in rng.permutation(n)]
+    buses = [perm[k:k + 8] for k in range(0, 240, 8)] + [perm[240:241], [], perm[241:300]]
+    e.mix_config(buses)
+    assert e.n_buses == len(buses)
+    y = _voice_run(e, 512, cuda)
+    assert np.all(np.isfinite(y))
+    init = rng.standard_normal((512, len(buses))).astype(np.float32)
+    want = O.mix_ref(y, buses, init)
+    dev = e.mix(torch.from_numpy(y).to(cuda), torch.from_numpy(init.copy()).to(cuda))
+    torch.cuda.synchronize()
+    assert bits_equal(dev.cpu().numpy(), want)
+    assert bits_equal(e.mix(y, init.copy()), want)
+    back = perm[241:300][::-1]                   # the order of the adds is the list's
+    e.mix_config([back])
+    assert bits_equal(e.mix(y), O.mix_ref(y, [back]))
+
+
+def test_mix_config_rejects_bad_lists(cuda):
+    import ol_dsp_amd as ofx
+    e = engine("voice", 16)
+    for bad in ([[0, 1], [1]], [[16]]):
+        with pytest.raises(ofx.OlfxError):
+            e.mix_config(bad)
+    with pytest.raises(ofx.OlfxError):            # no buses configured
+        e.mix(np.zeros((1, 4, 16), np.float32))
+    e.mix_config([[3, 2], [5]])
+    assert e.n_buses == 2
+    e.mix_config([])
+    assert e.n_buses == 0
+    with pytest.raises(ofx.OlfxError):
+        engine("chorus", 4).mix_config([[0]])
+
+
+def test_polyvoice_allocation_vs_oracle(cuda):
+    """ol::synth::Polyvoice (Polyvoice.h:35-51): NoteOn takes the group's first voice not Playing(),
+    NoteOff its first voice Playing() that note.  The GPU voices follow oracle voices driven by that
+    rule (within the voice tolerance) and every bus is the in-order sum of its voices."""
+    import torch
+    import ol_dsp_amd as ofx
+    n, k = 12, 3
+    rng = np.random.default_rng(8)
+    cfg = voice_configs(rng, n)
+    cfg[2] *= 0.25
+    e, ref = _voice_pair(n, cfg, None, on=False)
+    groups = [list(range(g * k, g * k + k)) for g in range(n // k)]
+    poly = ofx.Polyvoice(e, groups)
+    playing = [0] * n                                   # the reference rule, for the oracle side
+
+    def on(g, note):
+        poly.note_on(g, note)
+        for v in groups[g]:
+            if not playing[v]:
+                ref.note(v, True, note)
+                playing[v] = note
+                return
+
+    def off(g, note):
+        poly.note_off(g, note)
+        for v in groups[g]:
+            if playing[v] == note:
+                ref.note(v, False, note)
+                playing[v] = 0
+                return
+
+    for g in range(len(groups)):
+        for note in (48, 55, 60, 67):                   # the fourth finds no free voice
+            on(g, note + g)
+    ys, bs, yrs = [], [], []
+    for blk in range(6):
+        if blk == 2:
+            for g in range(len(groups)):
+                off(g, 55 + g)
+        if blk == 3:
+            for g in range(len(groups)):
+                on(g, 72 + g)                           # takes the voice freed at block 2
+        vo = torch.empty((1, 256, n), device=cuda)
+        bus = poly.process(vo)
+        torch.cuda.synchronize()
+        ys.append(vo.cpu().numpy())
+        bs.append(bus.cpu().numpy())
+        yrs.append(ref.process(256))
+    y, yr, bus = np.concatenate(ys, 1), np.concatenate(yrs, 1), np.concatenate(bs, 0)
+    assert poly.playing.tolist() == playing
+    assert np.all(np.isfinite(y))
+    assert rel_err(y[0].T, yr[0].T) <= VOICE_TOL
+    assert bits_equal(bus, O.mix_ref(y, groups))

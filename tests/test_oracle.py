@@ -311,3 +311,20 @@ def test_fxrack_blocked_equals_unblocked_and_golden(golden):
     assert bits_equal(ya, yb), first_mismatch(ya, yb)
     assert [f"{O.fnv1a64_lr(ya[0, :, i], ya[1, :, i]):016x}" for i in range(g["n"])] == g["fnv1a64"]
 
+
+
+# ------------------------------------------------------------- voice buses (Polyvoice, 8a A17)
+def test_mix_ref_is_the_in_order_float32_sum():
+    """oracle.mix_ref restates Polyvoice::Process's `*frame_out += frame_buffer` (Polyvoice.h:28-33):
+    checked against a scalar float32 loop, with an empty bus and a non-zero starting frame."""
+    rng = np.random.default_rng(3)
+    v = (rng.standard_normal((1, 7, 12)) * 1e3).astype(np.float32)
+    buses = [[3, 1, 7], [], [0, 2, 4, 5, 6, 8, 9, 10, 11], [11]]
+    init = rng.standard_normal((7, 4)).astype(np.float32)
+    got = O.mix_ref(v, buses, init)
+    for f in range(7):
+        for b, vs in enumerate(buses):
+            acc = np.float32(init[f, b])
+            for i in vs:
+                acc = np.float32(acc + v[0, f, i])
+            assert got[f, b].tobytes() == acc.tobytes()

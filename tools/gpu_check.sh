@@ -29,6 +29,7 @@ if [ "$mode" = full ] || [ "$mode" = prof ]; then
     step bench_chain 400 python bench.py --workload chain --steps 40 --warmup 5 --cpu-seconds 3
     step bench_fxrack 400 python bench.py --workload fxrack --steps 60 --warmup 5 --cpu-seconds 3
     step bench_voice_moog 300 python bench.py --workload voice_moog --steps 60 --warmup 5 --cpu-seconds 3
+    step bench_voice_poly 300 python bench.py --workload voice_poly --steps 100 --warmup 10 --cpu-seconds 0
 fi
 if [ "$mode" = prof ]; then
     export TMPDIR=/tmp
@@ -44,5 +45,7 @@ if [ "$mode" = prof ]; then
         python3 bench.py --workload fxrack --steps 30 --warmup 3 --cpu-seconds 0
     step prof_voice_moog 600 rocprofv3 --kernel-trace --stats -d "$out/prof_voice_moog" -o run --output-format csv -- \
         python3 bench.py --workload voice_moog --steps 30 --warmup 3 --cpu-seconds 0
+    step prof_voice_poly 600 rocprofv3 --kernel-trace --stats -d "$out/prof_voice_poly" -o run --output-format csv -- \
+        python3 bench.py --workload voice_poly --steps 50 --warmup 3 --cpu-seconds 0
 fi
 echo "== done $(date +%T)"

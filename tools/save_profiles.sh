@@ -4,7 +4,7 @@
 # the GPU pytest log.  Usage: bash tools/save_profiles.sh [round=r1] [tag=latest] [workloads...]
 set -eu
 rnd=${1:-r1}; tag=${2:-latest}; shift 2 || true
-wls=${*:-chorus dattorro voice chain fxrack voice_moog}
+wls=${*:-chorus dattorro voice chain fxrack voice_moog voice_poly}
 dst=profiles/$rnd
 mkdir -p "$dst"
 for w in $wls; do
