@@ -38,10 +38,55 @@ __global__ __launch_bounds__(256) void voice_mix_v1(MixArgs a) {
     *dst = acc;
 }
 
+// v2: one lane = (bus, four frames).  A bus's voice indices are read once per four frames instead
+// of once per frame, and the four frames' loads of one voice are independent, so eight loads are
+// in flight per unrolled step.  Every frame's adds still run voice by voice in list order.
+constexpr uint32_t kMixFr = 4;
+
+__global__ __launch_bounds__(256) void voice_mix_v2(MixArgs a) {
+    const uint32_t b = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t f0 = blockIdx.y * kMixFr;
+    if (b >= a.n_buses) return;
+    const uint32_t nfr = a.n_frames - f0 < kMixFr ? a.n_frames - f0 : kMixFr;   // uniform per block
+    const float *row = a.in + (size_t)f0 * a.n;
+    float *dst = a.out + (size_t)f0 * a.n_buses + b;
+    const uint32_t k1 = a.off[b + 1];
+    uint32_t k = a.off[b];
+    if (nfr == kMixFr) {
+        float acc[kMixFr];
+#pragma unroll
+        for (uint32_t j = 0; j < kMixFr; ++j) acc[j] = dst[(size_t)j * a.n_buses];
+        for (; k + 2 <= k1; k += 2) {
+            const uint32_t i0 = a.order[k], i1 = a.order[k + 1];
+            float v0[kMixFr], v1[kMixFr];
+#pragma unroll
+            for (uint32_t j = 0; j < kMixFr; ++j) {
+                v0[j] = row[(size_t)j * a.n + i0];
+                v1[j] = row[(size_t)j * a.n + i1];
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < kMixFr; ++j) acc[j] = (acc[j] + v0[j]) + v1[j];
+        }
+        if (k < k1) {
+            const uint32_t i0 = a.order[k];
+#pragma unroll
+            for (uint32_t j = 0; j < kMixFr; ++j) acc[j] = acc[j] + row[(size_t)j * a.n + i0];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kMixFr; ++j) dst[(size_t)j * a.n_buses] = acc[j];
+    } else {
+        for (uint32_t j = 0; j < nfr; ++j) {
+            float acc = dst[(size_t)j * a.n_buses];
+            for (uint32_t q = k; q < k1; ++q) acc = acc + row[(size_t)j * a.n + a.order[q]];
+            dst[(size_t)j * a.n_buses] = acc;
+        }
+    }
+}
+
 hipError_t launch_mix(const MixArgs &a, hipStream_t s) {
     if (a.n_buses == 0 || a.n_frames == 0) return hipSuccess;
-    const dim3 grid((a.n_buses + 255) / 256, a.n_frames);
-    hipLaunchKernelGGL(voice_mix_v1, grid, dim3(256), 0, s, a);
+    const dim3 grid((a.n_buses + 255) / 256, (a.n_frames + kMixFr - 1) / kMixFr);
+    hipLaunchKernelGGL(voice_mix_v2, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
