@@ -4,19 +4,28 @@
 One step = one 256-frame block (48 kHz) processed for every instance on every rank, inputs
 already resident in HBM (a pool of distinct synthetic blocks, cycled, larger than the 256 MiB
 Infinity Cache).  Default workload = BASELINE.json configs[1]: 65,536 stereo ChorusEffect
-instances per GPU.  Multi-GPU: one process per GPU (torchrun), instances sharded with no
-data-path collective (weak scaling); one RCCL all-reduce after the timed region gathers the
-counters.
+instances per GPU.  Multi-GPU: one process per GPU (torchrun); the job is `instances per GPU x
+world` GLOBAL instances, each rank takes its contiguous shard (ol_dsp_amd.dist.shard) and derives
+every instance's parameters and input stream from its global index (ol_dsp_amd.workload), so an
+N-GPU run processes exactly the instances a one-GPU run of the same total would.  No data-path
+collective (weak scaling); one RCCL all-reduce after each timed region gathers the counters.
 
 Prints ONE JSON line (rank 0): metric/value/unit/... plus
   roofline     : algorithmic bytes of the dominant kernel / its HIP-event-timed duration vs 8 TB/s
-  cpu_baseline : the CPU oracle (port) or the compiled reference (reference) on host cores
+                 (frac = read+write, frac_read = the read share: the north star's HBM-read roofline)
+  cpu_baseline : the CPU oracle (port) or the compiled reference (reference) on all host cores
+                 given to this process, at -O2 and -O0 (the reference's CMake default)
+  cpu_c1       : BASELINE configs[0]: one chorus instance, one core, per-frame calls
+  also         : the other BASELINE configs timed in the same run (dattorro = configs[2], the
+                 north star's >= 64k chorus+reverb chains, configs[4]'s per-GPU shard, configs[3]'s
+                 voices, the fxlib rack), each with its own roofline and cpu_baseline
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -46,11 +55,14 @@ WORKLOADS = {
     "voice_moog": ("voice_moog", 32768, "SURVEY 8f row 3: configs[3] with the Daisy firmware's MoogFilter "
                    "(daisysp::LadderFilter) voices, 32,768 per GPU"),
     "chain": ("chain", 16384, "configs[4]: 131,072 chorus->pitch-shift->dattorro chains = 16,384 per GPU x 8"),
+    "chain_65536": ("chain", 65536, "north_star: >= 64k concurrent chorus+reverb instances on 1xMI355X "
+                    "(fused chorus->pitch-shift->dattorro chains)"),
     "pitchshift": ("pitchshift", 65536, "pitch-shift stage alone"),
     "fxrack": ("fxrack", 65536, "SURVEY 8f row 1: fxlib FxRack<2> (delay -> reverb -> filter -> master), 65,536 instances"),
     "voice_poly": ("voice", 32768, "SURVEY 8a A17: configs[3] voices summed into Polyvoice buses of 8 voices "
                    "(olfx_mix) inside every step"),
 }
+DEFAULT_ALSO = "dattorro,chain_65536,chain,voice,fxrack"
 
 
 def parse():
@@ -60,85 +72,284 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="chorus", choices=sorted(WORKLOADS))
     ap.add_argument("--instances", type=int, default=0, help="instances per GPU (0 = workload default)")
+    ap.add_argument("--also", default=None,
+                    help=f"comma list of extra workloads timed in the same run (default for chorus: {DEFAULT_ALSO}; "
+                         "'' = none)")
     ap.add_argument("--block", type=int, default=256)
     ap.add_argument("--sample-rate", type=float, default=48000.0)
-    ap.add_argument("--pool-bytes", type=float, default=1.2e9, help="bytes of distinct input blocks")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall budget of the CPU baseline (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--pool-bytes", type=float, default=1.0e9, help="bytes of distinct input blocks (> 256 MiB IC)")
+    ap.add_argument("--cpu-seconds", type=float, default=4.0, help="wall budget of each -O2 CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may run on")
     ap.add_argument("--traffic-json", default="", help="PMC traffic summary (tools/pmc_traffic.py)")
     return ap.parse_args()
 
 
-def draw_params(kind: str, n: int, seed: int) -> np.ndarray:
-    """Per-instance params, seeded uniform within the reference ranges."""
-    rng = np.random.default_rng(seed)
-    u = lambda lo, hi: rng.uniform(lo, hi, n).astype(np.float32)  # noqa: E731
-    chorus = [u(0, 3), u(0, 1), u(0, .95), u(0, 1), u(0, 1), u(.08, 1), u(.01, 1), np.full(n, 10, np.float32)]
-    pitch = [u(0, 3), np.full(n, 10, np.float32)]
-    verb = [np.full(n, 0.1, np.float32), u(.5, .95), np.full(n, .75, np.float32), np.full(n, .625, np.float32),
-            np.full(n, .70, np.float32), u(.25, .95), u(.05, .95)]
-    voice = [u(100, 8000), u(0, .9), u(0, 1), u(0, 1), u(.001, .5), u(0, 1), u(.001, .5), u(0, 1), u(.001, .5),
-             u(.2, 1), u(.001, .5), u(0, 1), u(.001, .5), u(0, 1), u(.001, .5), u(0, .05)]
-    rack = [u(0.05, 1), u(0, .9), u(0, 1), u(100, 12000), u(0, .8), u(0, 1), u(100, 12000), u(0, .8),
-            u(0, 1), rng.integers(0, 5, n).astype(np.float32), u(0, 1)]
-    table = {"chorus": chorus, "pitchshift": pitch, "dattorro": verb, "voice": voice, "voice_moog": voice,
-             "chain": chorus + pitch + verb, "fxrack": rack}
-    return np.stack(table[kind])
+# ------------------------------------------------------------------------------------------------
+# CPU baseline (rank 0, N=1): the oracle restatement or the compiled reference, bounded sample
+# ------------------------------------------------------------------------------------------------
+def host_facts() -> dict:
+    """nproc (the cores this process is given: OMP_NUM_THREADS where set -- the GPU box's CPU share
+    per GPU, which `nproc` reports too -- else the affinity mask), the machine's CPU count and model
+    (lscpu)."""
+    try:
+        nproc = len(os.sched_getaffinity(0))
+    except AttributeError:
+        nproc = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        nproc = min(nproc, int(omp))
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": nproc, "host_cpus": os.cpu_count(), "cpu_model": model}
 
 
-def cpu_baseline(kind: str, block: int, sr: float, budget_s: float, threads: int) -> dict:
-    """Time the CPU oracle (or the compiled reference for dattorro) on a bounded sample of the
-    same workload: a bank of instances, 256-frame blocks, until the wall budget is spent."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+def _cpu_bank(kind: str, n: int, sr: float, o0: bool, ref: bool):
     import oracle as O
-    n = 8192 if kind not in VOICE_KINDS else 32768
-    rng = np.random.default_rng(7)
-    p = draw_params(kind, n, 7)
-    x = (rng.random((2, block, n), dtype=np.float32) - 0.5)
-    kind_used = "port"
+    from ol_dsp_amd.workload import instance_params, voice_notes
+    p = instance_params(kind, 0, n)
     if kind == "dattorro":
-        ref = O.ref_available()
-        bank = O.Dattorro(n, ref=ref)
-        kind_used = "reference" if ref else "port"
+        bank = O.Dattorro(n, ref=ref, o0=o0)
         for i in range(n):
             for f in range(7):
                 bank.set(i, f, float(p[f, i]))
-        step = lambda: bank.process(x, threads)  # noqa: E731
-    elif kind in ("chorus", "pitchshift"):
-        bank = O.Chorus(n, sr, 0 if kind == "chorus" else 1)
+        return lambda x, t: bank.process(x, t), bank
+    if kind in ("chorus", "pitchshift"):
+        bank = O.Chorus(n, sr, 0 if kind == "chorus" else 1, o0=o0)
         for i in range(n):
             for f in range(p.shape[0]):
                 bank.set(i, f if kind == "chorus" else (0, 7)[f], float(p[f, i]))
-        step = lambda: bank.process(x, threads)  # noqa: E731
-    elif kind == "fxrack":
-        bank = O.FxRack(n, sr)
+        return lambda x, t: bank.process(x, t), bank
+    if kind == "fxrack":
+        bank = O.FxRack(n, sr, o0=o0)
         for i in range(n):
             for f in range(p.shape[0]):
                 bank.set(i, f, float(p[f, i]))
-        step = lambda: bank.process(x, threads)  # noqa: E731
-    elif kind in VOICE_KINDS:
-        bank = O.Voice(n, sr, moog=kind == "voice_moog")
+        return lambda x, t: bank.process(x, t), bank
+    if kind in VOICE_KINDS:
+        bank = O.Voice(n, sr, moog=kind == "voice_moog", o0=o0)
+        notes = voice_notes(0, n)
         for i in range(n):
             bank.config(i, p[:, i])
-            bank.note(i, True, 36 + i % 60)
-        step = lambda: bank.process(block, threads)  # noqa: E731
-    else:  # chain: compose the three stages
-        c1, c2, d = O.Chorus(n, sr), O.Chorus(n, sr, 1), O.Dattorro(n, ref=O.ref_available())
-        step = lambda: d.process(c2.process(c1.process(x, threads), threads), threads)  # noqa: E731
-    step()  # warm
-    t0 = time.perf_counter()
-    blocks = 0
-    while True:
-        step()
-        blocks += 1
+            bank.note(i, True, int(notes[i]))
+        return lambda x, t: bank.process(x.shape[1], t), bank
+    # chain: the composed stages, each a real bank with the chain's parameters
+    c1, c2, d = O.Chorus(n, sr, 0, o0=o0), O.Chorus(n, sr, 1, o0=o0), O.Dattorro(n, ref=ref, o0=o0)
+    for i in range(n):
+        for f in range(8):
+            c1.set(i, f, float(p[f, i]))
+        c2.set(i, 0, float(p[8, i]))
+        c2.set(i, 7, float(p[9, i]))
+        for f in range(7):
+            d.set(i, f, float(p[10 + f, i]))
+    return lambda x, t: d.process(c2.process(c1.process(x, t), t), t), (c1, c2, d)
+
+
+def cpu_baseline(kind: str, block: int, sr: float, budget_s: float, threads: int) -> dict:
+    """Time the CPU oracle (or, for the reverb, the reference verb.cpp compiled here) on a bounded
+    sample of the same workload: the same global instances 0..n-1 with the same parameters and
+    input streams, 256-frame blocks, OpenMP schedule(static) over instances, until the wall
+    budget is spent; then the same at -O0 for a quarter of the budget."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from ol_dsp_amd.workload import noise_np
+    n = 8192 if kind not in VOICE_KINDS else 32768
+    ich = 0 if kind in VOICE_KINDS else 2
+    x = noise_np(0, n, block, 2) if ich else np.zeros((1, block, n), np.float32)
+    ref = kind in ("dattorro", "chain") and O.ref_available() and O.ref_available(o0=True)
+
+    def timed(o0: bool, budget: float):
+        step, _keep = _cpu_bank(kind, n, sr, o0, ref)
+        step(x, threads)  # warm
+        t0 = time.perf_counter()
+        blocks = 0
+        while True:
+            step(x, threads)
+            blocks += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return blocks * block * n / el, blocks, el
+
+    v2, b2, e2 = timed(False, budget_s)
+    v0, b0, e0 = timed(True, max(0.5, budget_s / 4))
+    src = ("oracle/_ref = libs/dattorro-verb/verb.cpp compiled here (reverb stage)" if ref
+           else "oracle C restatement")
+    res = {"value": v2, "unit": "stereo samples/s" if kind not in VOICE_KINDS else "voice samples/s",
+           "cores": threads, "kind": "reference" if kind == "dattorro" and ref else "port",
+           "sample": f"{n} instances x {b2} blocks x {block} frames ({e2:.1f} s wall, {threads} OpenMP threads, "
+                     f"{src}, -O2 -ffp-contract=off)",
+           "value_O0": v0, "sample_O0": f"{n} instances x {b0} blocks ({e0:.1f} s), -O0 (reference CMake default)"}
+    res.update(host_facts())
+    return res
+
+
+def cpu_c1(sr: float, block: int) -> dict:
+    """BASELINE configs[0]: one ChorusEffect instance, one core, 60 s of audio in
+    256-frame blocks, one process() call per frame as in the reference's fx_test.cpp:45-54 loop."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from ol_dsp_amd.workload import instance_params
+    p = instance_params("chorus", 0, 1)[:, 0]
+    frames = int(60 * sr)
+    out = {}
+    for o0 in (False, True):
+        t0 = time.perf_counter()
+        nans, _ = O.chorus_c1(p, frames, block, sr, o0=o0)
         el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    frames = blocks * block * n
-    return {"value": frames / el, "unit": "stereo samples/s" if kind not in VOICE_KINDS else "voice samples/s",
-            "cores": threads, "kind": kind_used,
-            "sample": f"{n} instances x {blocks} blocks x {block} frames ({el:.1f} s wall, {threads} OpenMP threads"
-                      f"{', oracle/_ref = libs/dattorro-verb/verb.cpp -O2' if kind_used == 'reference' else ', oracle C restatement -O2'})"}
+        out["value_O0" if o0 else "value"] = frames / el
+        out["nan_outputs_O0" if o0 else "nan_outputs"] = nans
+    out.update({"unit": "stereo samples/s", "cores": 1, "kind": "port",
+                "sample": f"1 instance, {frames} frames (60 s @ {sr:.0f} Hz), {block}-frame blocks, per-frame "
+                          "process() calls (fx_test.cpp:45-54 loop shape), oracle C restatement -O2 / -O0"})
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# GPU workloads
+# ------------------------------------------------------------------------------------------------
+def _traffic(name: str, n: int, B: int, override: str = ""):
+    for tj in ([override] if override else []) + [os.path.join(ROOT, "profiles", f"traffic_{name}_{n}.json"),
+                                                  os.path.join(ROOT, "profiles", f"traffic_{name}.json")]:
+        if tj and os.path.exists(tj):
+            try:
+                with open(tj) as f:
+                    tr = json.load(f)
+                if tr.get("instances") == n and tr.get("block") == B:
+                    return tr.get("hbm_bytes_per_launch")
+            except Exception:
+                pass
+    return None
+
+
+def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, with_cpu: bool) -> dict:
+    import torch
+
+    import ol_dsp_amd as ofx
+    from ol_dsp_amd.dist import RunStats, reduce_stats, shard
+    from ol_dsp_amd.workload import instance_params, noise_torch, voice_notes
+
+    kind, _, desc = WORKLOADS[name]
+    total = n_per_gpu * world
+    first, n = shard(total, world, rank)
+    B = args.block
+    eng = ofx.Engine(kind, n, sample_rate=args.sample_rate, block=B, device=dev.index or 0)
+    eng.set_params(0, instance_params(kind, first, n))
+    ich, och = eng.info.in_channels, eng.info.out_channels
+
+    # input pool: distinct synthetic blocks of each global instance's own stream, on the device
+    blk_bytes = max(ich, 1) * B * n * 4
+    pool_n = max(2, int(args.pool_bytes // blk_bytes)) if ich else 1
+    pool = noise_torch(first, n, B, ich, dev, blocks=pool_n) if ich else [None]
+    out = torch.empty((och, B, n), device=dev)
+    voice = kind in VOICE_KINDS
+    notes = voice_notes(first, n)
+    note_off = None
+    if voice:   # NoteOn for every voice at block 0, NoteOff at the middle of the timed blocks (SURVEY 8d)
+        eng.note_events(eng.make_events(np.arange(n), 1, notes))
+        note_off = eng.make_events(np.arange(n), 0, notes)
+    bus = None
+    if name == "voice_poly":       # Polyvoice buses of 8 voices (Polyvoice.h:28-33)
+        eng.mix_config([list(range(g, min(g + 8, n))) for g in range(0, n, 8)])
+        bus = torch.zeros((B, eng.n_buses), device=dev)
+    stream = torch.cuda.Stream(dev)        # dedicated non-default stream: events see the kernels
+    torch.cuda.synchronize(dev)
+    K, W = args.steps, args.warmup
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    evm = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)] if bus is not None else None
+
+    def step(k, t=None):
+        if voice and k == W + K // 2:
+            eng.note_events(note_off)
+        if t is not None:
+            ev[t][0].record(stream)
+        eng.process(pool[k % pool_n], out=out, n_frames=B, stream=stream.cuda_stream)
+        if t is not None:
+            ev[t][1].record(stream)
+        if bus is not None:
+            if t is not None:
+                evm[t][0].record(stream)
+            eng.mix(out, bus, stream=stream.cuda_stream)
+            if t is not None:
+                evm[t][1].record(stream)
+
+    for k in range(W):
+        step(k)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(K):
+        step(W + k, k)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    mix_ms = float(np.mean([a.elapsed_time(b) for a, b in evm])) if evm else None
+
+    # sum |y| over the finite outputs of the last block (a voice whose Svf diverges -- possible in
+    # the reference DaisySP arithmetic at high cutoff, low resonance and high drive -- yields
+    # inf/NaN there too; DESIGN.md section 5); the count of non-finite samples beside it
+    finite = torch.isfinite(out)
+    nonfinite = int((~finite).sum().item())
+    checksum = float(torch.where(finite, out.abs(), torch.zeros_like(out)).sum().item())
+    bus_sum = float(bus.abs().sum().item()) if bus is not None else None
+    stats = reduce_stats(RunStats(elapsed, kern_ms, float(n) * B * K, checksum), device=dev)
+    bpf, rbpf, kname = eng.algorithmic_bytes_per_frame, eng.algorithmic_read_bytes_per_frame, eng.kernel_name
+    eng.close()
+    del pool, out
+    torch.cuda.empty_cache()
+    if rank != 0:
+        return {}
+
+    elapsed, kern_ms, frames = stats.elapsed_s, stats.kernel_ms, stats.frames
+    per_launch = n * B
+    achieved = bpf * per_launch / (kern_ms * 1e-3) / 1e9
+    achieved_r = rbpf * per_launch / (kern_ms * 1e-3) / 1e9
+    traffic = _traffic(name, n, B, args.traffic_json if name == args.workload else "")
+    if voice:
+        fps = VOICE_MOOG_FLOPS_PER_SAMPLE if kind == "voice_moog" else VOICE_FLOPS_PER_SAMPLE
+        tflops = fps * per_launch / (kern_ms * 1e-3) / 1e12
+        roofline = {"bound": "valu", "achieved": tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,
+                    "kernel": kname, "kernel_ms": kern_ms, "algorithmic_flops_per_frame": fps,
+                    "algorithmic_bytes_per_frame": bpf, "hbm_gbs": achieved, "frames_per_launch": per_launch}
+    else:
+        roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                    "achieved_read": achieved_r, "frac_read": achieved_r / HBM_PEAK_GBS,
+                    "kernel": kname, "kernel_ms": kern_ms,
+                    "algorithmic_bytes_per_frame": bpf, "algorithmic_read_bytes_per_frame": rbpf,
+                    "frames_per_launch": per_launch}
+    res = {"metric": METRIC, "value": frames / elapsed,
+           "unit": "voice samples/s" if voice else "stereo samples/s",
+           "ms_per_step": elapsed / K * 1e3,
+           "config": {"workload": name, "restates": desc, "instances_per_gpu": n_per_gpu,
+                      "instances_total": total, "block": B, "sample_rate": args.sample_rate,
+                      "input_pool_blocks": pool_n, "parallelism": f"instance-shard x{world} (no data-path collective)"},
+           "roofline": roofline,
+           "output_checksum": stats.checksum, "output_nonfinite_rank0": nonfinite}
+    if mix_ms is not None:
+        nb = (n + 7) // 8
+        mix_bytes = 4.0 * n * B + 8.0 * nb * B          # voice reads + bus read-modify-write
+        res["mix"] = {"kernel": "voice_mix_v2", "kernel_ms": mix_ms, "bound": "hbm",
+                      "achieved": mix_bytes / (mix_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                      "frac": mix_bytes / (mix_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                      "algorithmic_bytes_per_launch": mix_bytes, "bus_checksum_rank0": bus_sum}
+    if with_cpu and world == 1 and args.cpu_seconds > 0:
+        threads = args.cpu_threads or host_facts()["nproc"]
+        res["cpu_baseline"] = cpu_baseline(kind, B, args.sample_rate, args.cpu_seconds, threads)
+    else:
+        res["cpu_baseline"] = None
+    return res
 
 
 def main():
@@ -146,7 +357,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from ol_dsp_amd.dist import RunStats, env_ranks, reduce_stats
+    from ol_dsp_amd.dist import env_ranks
     rank, world, local = env_ranks()
     if world > 1:
         torch.cuda.set_device(local)
@@ -154,116 +365,44 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    import ol_dsp_amd as ofx
-    kind, n_default, desc = WORKLOADS[args.workload]
-    n = args.instances or n_default
-    B = args.block
-    eng = ofx.Engine(kind, n, sample_rate=args.sample_rate, block=B, device=local)
-    eng.set_params(0, draw_params(kind, n, 1000 + rank))
-    ich, och = eng.info.in_channels, eng.info.out_channels
-
-    # input pool: distinct synthetic blocks (uniform +-0.5 white noise), generated on the device
-    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    blk_bytes = max(ich, 1) * B * n * 4
-    pool_n = max(2, int(args.pool_bytes // blk_bytes)) if ich else 1
-    pool = [torch.rand((ich, B, n), generator=gen, device=dev) - 0.5 for _ in range(pool_n)] if ich else [None]
-    out = torch.empty((och, B, n), device=dev)
-    if kind in VOICE_KINDS:   # NoteOn for every voice at block 0
-        eng.note_events([(i, 1, 36 + (i * 7) % 61) for i in range(n)])
-    bus = None
-    if args.workload == "voice_poly":       # Polyvoice buses of 8 voices (Polyvoice.h:28-33)
-        eng.mix_config([list(range(g, min(g + 8, n))) for g in range(0, n, 8)])
-        bus = torch.zeros((B, eng.n_buses), device=dev)
-    stream = torch.cuda.Stream(dev)        # dedicated non-default stream: events see the kernels
-    torch.cuda.synchronize(dev)
-
-    def step(k):
-        eng.process(pool[k % pool_n], out=out, n_frames=B, stream=stream.cuda_stream)
-        if bus is not None:
-            eng.mix(out, bus, stream=stream.cuda_stream)
-
-    for k in range(args.warmup):
-        step(k)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record(stream)
-        step(args.warmup + k)
-        ev[k][1].record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-
-    # the single collective of the run (RCCL over xGMI when world > 1): outside the timed region
-    # sum |y| over the finite outputs (a voice whose Svf diverges -- possible in the reference
-    # DaisySP arithmetic at high cutoff, low resonance and high drive -- yields inf/NaN there too;
-    # DESIGN.md section 5); the count of non-finite samples is reported beside it
-    finite = torch.isfinite(out)
-    nonfinite = int((~finite).sum().item())
-    checksum = float(torch.where(finite, out.abs(), torch.zeros_like(out)).sum().item())
-    stats = reduce_stats(RunStats(elapsed, kern_ms, float(n) * B * args.steps, checksum), device=dev)
-    elapsed, kern_ms, frames = stats.elapsed_s, stats.kernel_ms, stats.frames
+    n = args.instances or WORKLOADS[args.workload][1]
+    main_res = run_workload(args.workload, n, args, rank, world, dev, with_cpu=True)
+    also = args.also if args.also is not None else (DEFAULT_ALSO if args.workload == "chorus" else "")
+    also_res = {}
+    for name in [a for a in also.split(",") if a]:
+        r = run_workload(name, WORKLOADS[name][1], args, rank, world, dev, with_cpu=True)
+        if rank == 0:
+            key = name if name != "chain" else "chain_16384"
+            also_res[key] = {k: r[k] for k in ("value", "unit", "ms_per_step", "config", "roofline",
+                                                "cpu_baseline", "output_checksum", "output_nonfinite_rank0") if k in r}
 
     if rank == 0:
-        value = frames / elapsed
-        bpf = eng.algorithmic_bytes_per_frame
-        per_launch_bytes = bpf * n * B
-        achieved = per_launch_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = None
-        tj = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
-        if os.path.exists(tj):
-            try:
-                with open(tj) as f:
-                    tr = json.load(f)
-                if tr.get("instances") == n and tr.get("block") == B:
-                    traffic = tr.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        if kind in VOICE_KINDS:
-            fps = VOICE_MOOG_FLOPS_PER_SAMPLE if kind == "voice_moog" else VOICE_FLOPS_PER_SAMPLE
-            tflops = fps * n * B / (kern_ms * 1e-3) / 1e12
-            roofline = {"bound": "valu", "achieved": tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,
-                        "kernel": eng.kernel_name, "kernel_ms": kern_ms,
-                        "algorithmic_flops_per_frame": fps,
-                        "algorithmic_bytes_per_frame": bpf, "hbm_gbs": achieved, "frames_per_launch": n * B}
-        else:
-            roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                        "kernel": eng.kernel_name, "kernel_ms": kern_ms,
-                        "algorithmic_bytes_per_frame": bpf, "frames_per_launch": n * B}
-        cpu = None
-        if world == 1 and args.cpu_seconds > 0:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(kind, B, args.sample_rate, args.cpu_seconds, threads)
         res = {
             "metric": METRIC,
-            "value": value,
-            "unit": "voice samples/s" if kind in VOICE_KINDS else "stereo samples/s",
+            "value": main_res["value"],
+            "unit": main_res["unit"],
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": main_res["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (device-generated uniform +-0.5 noise pool, seeded per-instance params)",
-            "config": {"workload": args.workload, "restates": desc, "instances_per_gpu": n,
-                       "instances_total": n * world, "block": B, "sample_rate": args.sample_rate,
-                       "input_pool_blocks": pool_n, "parallelism": f"instance-shard x{world} (no data-path collective)"},
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-            "output_checksum": stats.checksum,
-            "output_nonfinite_rank0": nonfinite,
+            "data": "synthetic: per-(instance, channel) xorshift32 noise streams (SURVEY 8d seeds) in a device "
+                    "pool; per-instance params hashed from the global instance index",
+            "config": main_res["config"],
+            "roofline": main_res["roofline"],
+            "cpu_baseline": main_res["cpu_baseline"],
+            "output_checksum": main_res["output_checksum"],
+            "output_nonfinite_rank0": main_res["output_nonfinite_rank0"],
         }
+        if "mix" in main_res:
+            res["mix"] = main_res["mix"]
+        if world == 1 and args.cpu_seconds > 0 and args.workload == "chorus":
+            res["cpu_c1"] = cpu_c1(args.sample_rate, args.block)
+        if also_res:
+            res["also"] = also_res
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()

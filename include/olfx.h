@@ -242,6 +242,9 @@ uint32_t olfx_num_buses(const olfx_engine *e);          /* voice buses (olfx_mix
 /* Algorithmic ("compulsory") HBM bytes per instance-frame of the dominant kernel, the figure
    bench.py's roofline uses. */
 double   olfx_algorithmic_bytes_per_frame(const olfx_engine *e);
+/* The read share of the same figure: tap reads of data older than the block plus the input (the
+   north star's "HBM-read roofline", SURVEY.md section 8d "read-only variant"). */
+double   olfx_algorithmic_read_bytes_per_frame(const olfx_engine *e);
 const char *olfx_kernel_name(const olfx_engine *e);
 const char *olfx_last_error(const olfx_engine *e);   /* e may be NULL: last global error */
 

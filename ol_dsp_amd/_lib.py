@@ -103,6 +103,7 @@ SIGNATURES = {
     "olfx_kind": (ctypes.c_int, [_P]),
     "olfx_frames_processed": (ctypes.c_uint64, [_P]),
     "olfx_algorithmic_bytes_per_frame": (ctypes.c_double, [_P]),
+    "olfx_algorithmic_read_bytes_per_frame": (ctypes.c_double, [_P]),
     "olfx_kernel_name": (ctypes.c_char_p, [_P]),
     "olfx_last_error": (ctypes.c_char_p, [_P]),
     "olfx_mix_config": (ctypes.c_int, [_P, _U32, ctypes.POINTER(_U32), ctypes.POINTER(_U32)]),

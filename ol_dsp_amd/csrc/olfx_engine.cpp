@@ -1117,6 +1117,22 @@ double olfx_algorithmic_bytes_per_frame(const olfx_engine *e) {
     }
 }
 
+double olfx_algorithmic_read_bytes_per_frame(const olfx_engine *e) {
+    if (!e) return 0.0;
+    // the read share of the figures above (the north star's "HBM-read roofline"): every tap read
+    // of data older than the block, counted once, plus the input
+    switch (e->kind) {
+    case OLFX_KIND_DATTORRO: return 6445.0 * 4.0 / 256.0 + 8.0;   // 27 taps: sum min(d, 256) = 6,445 floats; + 8 in
+    case OLFX_KIND_CHORUS: return 32.0;        // 2 x (2 pitch taps + chorus tap) x 4 + 8 in
+    case OLFX_KIND_PITCHSHIFT: return 24.0;    // 2 x 2 taps x 4 + 8 in
+    case OLFX_KIND_VOICE: return 0.7;          // per-block state and coefficients
+    case OLFX_KIND_VOICE_MOOG: return 0.85;
+    case OLFX_KIND_CHAIN: return 8.0 + 24.0 + 16.0 + 6445.0 * 4.0 / 256.0;   // 148.7
+    case OLFX_KIND_FXRACK: return 16.0;        // ring read 8 + in 8
+    default: return 0.0;
+    }
+}
+
 const char *olfx_kernel_name(const olfx_engine *e) {
     if (!e) return "";
     switch (e->kind) {

@@ -126,8 +126,28 @@ class Engine:
         check(self.lib.olfx_set_params(self._h, int(first), int(cnt), self.field(field0), int(nf),
                                        arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float))), self._h)
 
-    def note_events(self, events: Iterable[Sequence[int]]) -> None:
-        """events: iterable of (inst, type, note[, velocity]); type 1 = NoteOn, 0 = NoteOff."""
+    @staticmethod
+    def make_events(inst, type_, note, velocity=100):
+        """A prebuilt event array (numpy-vectorised) for note_events: inst / note arrays (or
+        scalars broadcast against them), type 1 = NoteOn, 0 = NoteOff."""
+        inst = np.asarray(inst, np.uint32).ravel()
+        rec = np.zeros(len(inst), dtype=[("inst", "<u4"), ("type", "u1"), ("note", "u1"), ("velocity", "u1"),
+                                         ("pad", "u1")])
+        rec["inst"] = inst
+        rec["type"] = type_
+        rec["note"] = note
+        rec["velocity"] = velocity
+        assert ctypes.sizeof(_lib.Event) == rec.dtype.itemsize
+        return rec
+
+    def note_events(self, events) -> None:
+        """events: iterable of (inst, type, note[, velocity]) (type 1 = NoteOn, 0 = NoteOff), or an
+        array from make_events()."""
+        if isinstance(events, np.ndarray):
+            if len(events):
+                check(self.lib.olfx_note_events(self._h, events.ctypes.data_as(ctypes.POINTER(_lib.Event)),
+                                                len(events)), self._h)
+            return
         evs = list(events)
         if not evs:
             return
@@ -255,6 +275,10 @@ class Engine:
     @property
     def algorithmic_bytes_per_frame(self) -> float:
         return float(self.lib.olfx_algorithmic_bytes_per_frame(self._h))
+
+    @property
+    def algorithmic_read_bytes_per_frame(self) -> float:
+        return float(self.lib.olfx_algorithmic_read_bytes_per_frame(self._h))
 
     @property
     def kernel_name(self) -> str:

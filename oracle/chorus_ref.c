@@ -175,54 +175,91 @@ static float read_frac(const float *ring, uint32_t mask, uint32_t w, float d, fl
     return x0 + fr * (x1 - x0);
 }
 
+/* One frame of one instance (both channels): the per-sample operator body shared by the bank
+   (oracle_chorus_process) and the config-1 loop (oracle_chorus_c1). */
+static void chorus_frame(const oracle_chorus *o, const chcoef_t *k, chstate_t *s, uint32_t w,
+                         const float x[2], float y[2])
+{
+    const uint32_t pmask = o->psize - 1, cmask = o->csize - 1;
+    const float pmax = (float)(o->psize - 2), cmax = (float)(o->csize - 2);
+    const float lfo = oracle_cos2pi(unit24(s->lfo_acc + k->lfo_off));
+    s->lfo_acc += k->lfo_inc;
+    const float dch = lfo * k->D + k->D;
+    const float p0 = unit24(s->ps_acc);
+    const float p1 = unit24(s->ps_acc + 0x80000000u);
+    s->ps_acc += k->ps_inc;
+    const float g0 = oracle_cos2pi((p0 - 0.5f) * 0.5f);
+    const float g1 = oracle_cos2pi((p1 - 0.5f) * 0.5f);
+    const float d0 = p0 * k->W, d1 = p1 * k->W;
+    for (int c = 0; c < 2; c++) {
+        const float t0 = read_frac(s->pring[c], pmask, w, d0, 1.0f, pmax);
+        const float t1 = read_frac(s->pring[c], pmask, w, d1, 1.0f, pmax);
+        const float ps = t1 * g1 + t0 * g0;
+        s->pring[c][w & pmask] = x[c];
+        if (o->mode == 0) {
+            s->cring[c][w & cmask] = ps;
+            const float wet = read_frac(s->cring[c], cmask, w, dch, 0.0f, cmax);
+            const float lp = k->b0 * wet + s->z1[c];
+            s->z1[c] = (k->b1 * wet - k->a1 * lp) + s->z2[c];
+            s->z2[c] = k->b2 * wet - k->a2 * lp;
+            y[c] = x[c] * k->dry + lp * k->mix;
+        } else {
+            y[c] = ps;
+        }
+    }
+}
+
 /* in/out [2][n_frames][n] */
 int oracle_chorus_process(oracle_chorus *o, const float *in, float *out, int n_frames, int n_threads)
 {
     if (!o || n_frames < 0) return -1;
     const long n = o->n;
     const long plane = n * (long)n_frames;
-    const uint32_t pmask = o->psize - 1, cmask = o->csize - 1;
-    const float pmax = (float)(o->psize - 2), cmax = (float)(o->csize - 2);
     const uint32_t w0 = (uint32_t)o->w;
     (void)n_threads;
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static) num_threads(n_threads > 0 ? n_threads : 1)
 #endif
     for (long i = 0; i < n; i++) {
-        const chcoef_t *k = &o->k[i];
-        chstate_t *s = &o->s[i];
         for (int f = 0; f < n_frames; f++) {
-            const uint32_t w = w0 + (uint32_t)f;
-            const float lfo = oracle_cos2pi(unit24(s->lfo_acc + k->lfo_off));
-            s->lfo_acc += k->lfo_inc;
-            const float dch = lfo * k->D + k->D;
-            const float p0 = unit24(s->ps_acc);
-            const float p1 = unit24(s->ps_acc + 0x80000000u);
-            s->ps_acc += k->ps_inc;
-            const float g0 = oracle_cos2pi((p0 - 0.5f) * 0.5f);
-            const float g1 = oracle_cos2pi((p1 - 0.5f) * 0.5f);
-            const float d0 = p0 * k->W, d1 = p1 * k->W;
-            for (int c = 0; c < 2; c++) {
-                const float x = in[c * plane + (long)f * n + i];
-                const float t0 = read_frac(s->pring[c], pmask, w, d0, 1.0f, pmax);
-                const float t1 = read_frac(s->pring[c], pmask, w, d1, 1.0f, pmax);
-                const float ps = t1 * g1 + t0 * g0;
-                s->pring[c][w & pmask] = x;
-                float y;
-                if (o->mode == 0) {
-                    s->cring[c][w & cmask] = ps;
-                    const float wet = read_frac(s->cring[c], cmask, w, dch, 0.0f, cmax);
-                    const float lp = k->b0 * wet + s->z1[c];
-                    s->z1[c] = (k->b1 * wet - k->a1 * lp) + s->z2[c];
-                    s->z2[c] = k->b2 * wet - k->a2 * lp;
-                    y = x * k->dry + lp * k->mix;
-                } else {
-                    y = ps;
-                }
-                out[c * plane + (long)f * n + i] = y;
-            }
+            const float x[2] = {in[(long)f * n + i], in[plane + (long)f * n + i]};
+            float y[2];
+            chorus_frame(o, &o->k[i], &o->s[i], w0 + (uint32_t)f, x, y);
+            out[(long)f * n + i] = y[0];
+            out[plane + (long)f * n + i] = y[1];
         }
     }
     o->w += (uint64_t)n_frames;
     return 0;
+}
+
+/* BASELINE configs[0] / SURVEY 8d C1: ONE chorus instance on one core, in the shape of the
+   reference's fx_test.cpp:45-54 loop -- per block of `block` frames, per frame: next input
+   sample (xorshift32 noise of instance 0, SURVEY 8d seeds), process(), isnan check -- over
+   n_frames frames.  Returns the number of NaN outputs; *sum_abs = sum |y| (keeps the work live). */
+long oracle_chorus_c1(float sample_rate, const float *params, long n_frames, int block, double *sum_abs)
+{
+    oracle_chorus *o = oracle_chorus_create(1, sample_rate, 0);
+    if (!o || block <= 0) { oracle_chorus_destroy(o); return -1; }
+    for (int f = 0; f < OCH_NPARAMS; f++) oracle_chorus_set(o, 0, f, params[f]);
+    uint32_t s[2] = {(0x9E3779B9u ^ (1u * 0x85EBCA6Bu)) | 1u, (0x9E3779B9u ^ (2u * 0x85EBCA6Bu)) | 1u};
+    long nans = 0;
+    double acc = 0.0;
+    for (long f0 = 0; f0 < n_frames; f0 += block) {
+        const long C = n_frames - f0 < block ? n_frames - f0 : block;
+        for (long f = 0; f < C; f++) {
+            float x[2], y[2];
+            for (int c = 0; c < 2; c++) {
+                s[c] ^= s[c] << 13; s[c] ^= s[c] >> 17; s[c] ^= s[c] << 5;
+                x[c] = (float)(int32_t)s[c] / 2147483648.0f * 0.5f;
+            }
+            chorus_frame(o, &o->k[0], &o->s[0], (uint32_t)o->w, x, y);
+            o->w++;
+            nans += isnan(y[0]) + isnan(y[1]);
+            acc += fabs((double)y[0]) + fabs((double)y[1]);
+        }
+    }
+    oracle_chorus_destroy(o);
+    if (sum_abs) *sum_abs = acc;
+    return nans;
 }

@@ -50,6 +50,8 @@ oracle_chorus *oracle_chorus_create(int n_inst, float sample_rate, int mode);
 void oracle_chorus_destroy(oracle_chorus *o);
 int oracle_chorus_set(oracle_chorus *o, int inst, int field, float value);
 int oracle_chorus_process(oracle_chorus *o, const float *in, float *out, int n_frames, int n_threads);
+/* config 1: one instance, one core, per-frame calls in fx_test.cpp:45-54's shape */
+long oracle_chorus_c1(float sample_rate, const float *params, long n_frames, int block, double *sum_abs);
 
 /* ---- synthlib SynthVoice (DaisySP restatement, parity unpinned) ---- */
 enum {  /* Voice::Config order, modules/synthlib/Voice.h:14-31 */

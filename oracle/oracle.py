@@ -16,6 +16,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
+LIB_O0 = os.path.join(HERE, "liboracle_O0.so")      # the same sources at -O0 (reference CMake default)
 REF_LIB = os.path.join(HERE, "_ref", "libverb_ref.so")
 REF_LIB_O0 = os.path.join(HERE, "_ref", "libverb_ref_O0.so")
 
@@ -33,7 +34,7 @@ VOICE_DEFAULTS = [0.0, 0.0, 0.0, 1.0, 0.0, 1.0, 0.2, 0.0, 0.0, 0.8, 0.01, 1.0, 0
 
 _F = ctypes.c_float
 _PF = ctypes.POINTER(ctypes.c_float)
-_lib = None
+_libs = {}
 _ref = {}
 
 
@@ -41,12 +42,12 @@ def build() -> None:
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
 
-def lib() -> ctypes.CDLL:
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB):
+def lib(o0: bool = False) -> ctypes.CDLL:
+    path = LIB_O0 if o0 else LIB
+    if path not in _libs:
+        if not os.path.exists(path):
             build()
-        L = ctypes.CDLL(LIB)
+        L = ctypes.CDLL(path)
         L.oracle_dattorro_create.restype = ctypes.c_void_p
         L.oracle_dattorro_create.argtypes = [ctypes.c_int]
         L.oracle_dattorro_destroy.argtypes = [ctypes.c_void_p]
@@ -78,8 +79,10 @@ def lib() -> ctypes.CDLL:
         L.oracle_fxrack_destroy.argtypes = [ctypes.c_void_p]
         L.oracle_fxrack_set.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _F]
         L.oracle_fxrack_process.argtypes = [ctypes.c_void_p, _PF, _PF, ctypes.c_int, ctypes.c_int]
-        _lib = L
-    return _lib
+        L.oracle_chorus_c1.restype = ctypes.c_long
+        L.oracle_chorus_c1.argtypes = [_F, _PF, ctypes.c_long, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        _libs[path] = L
+    return _libs[path]
 
 
 def ref_available(o0: bool = False) -> bool:
@@ -143,7 +146,7 @@ class Dattorro(_Bank):
             self.L = ref_lib(o0)
             self.h = self.L.ref_verb_create(n)
         else:
-            self.L = lib()
+            self.L = lib(o0)
             self.h = self.L.oracle_dattorro_create(n)
         assert self.h
 
@@ -170,9 +173,9 @@ class Dattorro(_Bank):
 class Chorus(_Bank):
     """mode 0 = stereo chorus, 1 = pitch-shift stage (fields 'pitch' = shift Hz, 'window')."""
 
-    def __init__(self, n: int, sample_rate: float = 48000.0, mode: int = 0):
+    def __init__(self, n: int, sample_rate: float = 48000.0, mode: int = 0, o0: bool = False):
         self.n = n
-        self.L = lib()
+        self.L = lib(o0)
         self.h = self.L.oracle_chorus_create(n, sample_rate, mode)
         assert self.h
 
@@ -198,9 +201,9 @@ class Voice(_Bank):
     """SynthVoice bank.  moog=False: SvfFilter voice (SynthVoice default); moog=True: MoogFilter
     voice (daisysp::LadderFilter, the Daisy synth firmware's voice, main.cpp:49-52)."""
 
-    def __init__(self, n: int, sample_rate: float = 48000.0, moog: bool = False):
+    def __init__(self, n: int, sample_rate: float = 48000.0, moog: bool = False, o0: bool = False):
         self.n = n
-        self.L = lib()
+        self.L = lib(o0)
         self.h = self.L.oracle_voice_create_model(n, sample_rate, int(bool(moog)))
         assert self.h
 
@@ -223,6 +226,17 @@ class Voice(_Bank):
         return out
 
 
+def chorus_c1(params, n_frames: int, block: int = 256, sample_rate: float = 48000.0, o0: bool = False):
+    """BASELINE configs[0]: one chorus instance on one core, per-frame calls in fx_test.cpp:45-54's
+    loop shape (oracle_chorus_c1).  Returns (nan_count, sum |y|)."""
+    p = np.ascontiguousarray(np.asarray(params, dtype=np.float32))
+    assert p.shape == (len(CH_FIELDS),)
+    acc = ctypes.c_double()
+    nans = lib(o0).oracle_chorus_c1(sample_rate, _pf(p), int(n_frames), int(block), ctypes.byref(acc))
+    assert nans >= 0
+    return int(nans), acc.value
+
+
 def fxrack_defaults() -> np.ndarray:
     p = np.zeros(len(FR_FIELDS), np.float32)
     lib().oracle_fxrack_defaults(_pf(p))
@@ -232,9 +246,9 @@ def fxrack_defaults() -> np.ndarray:
 class FxRack(_Bank):
     """ol::fx::FxRack<2>: stereo in -> delay -> reverb (ReverbSc stub) -> filter (ch 0) -> master."""
 
-    def __init__(self, n: int, sample_rate: float = 48000.0):
+    def __init__(self, n: int, sample_rate: float = 48000.0, o0: bool = False):
         self.n = n
-        self.L = lib()
+        self.L = lib(o0)
         self.h = self.L.oracle_fxrack_create(n, sample_rate)
         assert self.h
 
