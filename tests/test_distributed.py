@@ -51,6 +51,58 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _shard_checksum(first, count):
+    """The chorus job's per-shard checksum: the oracle run on this shard's global instances (params
+    and inputs from the global index), summed as exact float64 over the output bit patterns."""
+    import numpy as np
+
+    import oracle as O
+    from ol_dsp_amd.workload import instance_params, noise_np
+    p = instance_params("chorus", first, count)
+    c = O.Chorus(count)
+    for i in range(count):
+        for f in range(8):
+            c.set(i, f, float(p[f, i]))
+    y = c.process(noise_np(first, count, 256, 2))
+    return float(y.view(np.uint32).astype(np.float64).sum())
+
+
+def _worker_job(rank, world, port, n_total, q):
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    first, count = shard(n_total, world, rank)
+    st = RunStats(elapsed_s=1.0, kernel_ms=1.0, frames=float(count * 256), checksum=_shard_checksum(first, count))
+    q.put((rank, reduce_stats(st)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_job_checksum_equals_single_rank(world):
+    """bench.py's multi-rank layout on CPU: each rank runs the oracle over its shard of a 96-instance
+    chorus job, the single all-reduce sums the shard checksums, and the sum equals the one-rank
+    job's checksum exactly."""
+    n_total = 96
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_job, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    whole = _shard_checksum(0, n_total)
+    for _, st in res:
+        assert st.checksum == whole
+        assert st.frames == n_total * 256
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_reduce_stats_gloo(world):
     ctx = mp.get_context("spawn")
