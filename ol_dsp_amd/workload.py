@@ -94,18 +94,19 @@ def noise_np(first: int, count: int, frames: int, ch: int = 2, skip: int = 0) ->
 
 def noise_torch(first: int, count: int, frames: int, ch: int, device, blocks: int = 1) -> List:
     """The same streams generated on the device, cut into `blocks` consecutive [ch][frames][count]
-    tensors (block b holds frames b*frames .. (b+1)*frames of every stream)."""
+    tensors (block b holds frames b*frames .. (b+1)*frames of every stream).  The streams are
+    stepped on the host (vectorised over instances) and each block is copied to the device once,
+    untimed: a handful of copies instead of thousands of tiny device launches, so profiler runs
+    see only the engine's kernels and a copy per block."""
     import torch
-    s = torch.from_numpy(seeds(first, count, ch).astype(np.int64)).to(device)
-    m = torch.tensor(M32, dtype=torch.int64, device=device)
+    s = seeds(first, count, ch).astype(np.uint32)
     out = []
+    host = np.empty((ch, frames, count), np.float32)
     for _ in range(blocks):
-        blk = torch.empty((ch, frames, count), dtype=torch.float32, device=device)
         for f in range(frames):
-            s = s ^ ((s << 13) & m)
-            s = s ^ (s >> 17)
-            s = s ^ ((s << 5) & m)
-            signed = s - ((s >> 31) << 32)
-            blk[:, f, :] = signed.to(torch.float32) * (2.0 ** -32)
-        out.append(blk)
+            s ^= s << np.uint32(13)
+            s ^= s >> np.uint32(17)
+            s ^= s << np.uint32(5)
+            host[:, f, :] = s.view(np.int32).astype(np.float32) * np.float32(2.0 ** -32)
+        out.append(torch.from_numpy(host).to(device, copy=True))
     return out

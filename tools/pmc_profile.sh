@@ -20,8 +20,8 @@ k=${PASS_BASE:-0}
 for p in "${passes[@]}"; do
   k=$((k+1))
   echo "== pass $k: $p"
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $p -d "$out/p$k" -o run --output-format csv -- \
-      python3 bench.py --workload "$wl" --steps "$steps" --warmup 2 --cpu-seconds 0 "$@" > "$out/p$k.log" 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --kernel-include-regex "_block_|voice_mix" --pmc $p -d "$out/p$k" -o run --output-format csv -- \
+      python3 bench.py --workload "$wl" --also "" --steps "$steps" --warmup 2 --cpu-seconds 0 "$@" > "$out/p$k.log" 2>&1
   rc=$?
   echo "   rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$out/p$k.log"; exit $rc; fi

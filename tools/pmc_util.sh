@@ -20,8 +20,8 @@ for wl in $wls; do
   for p in "${passes[@]}"; do
     k=$((k+1))
     echo "== $wl pass $k: $p"
-    timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $p -d "$out/p$k" -o run --output-format csv -- \
-        python3 bench.py --workload "$wl" --steps "$steps" --warmup 2 --cpu-seconds 0 > "$out/p$k.log" 2>&1
+    timeout -s KILL 120 rocprofv3 --kernel-trace --kernel-include-regex "_block_|voice_mix" --pmc $p -d "$out/p$k" -o run --output-format csv -- \
+        python3 bench.py --workload "$wl" --also "" --steps "$steps" --warmup 2 --cpu-seconds 0 > "$out/p$k.log" 2>&1
     rc=$?
     echo "   rc=$rc"
     if [ $rc -ne 0 ]; then tail -5 "$out/p$k.log"; exit $rc; fi
