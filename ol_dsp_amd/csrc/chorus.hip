@@ -1,56 +1,12 @@
 // ol_dsp_amd/csrc/chorus.hip -- RNBO stereo chorus and gen~ pitch-shifter kernel on gfx950.
-// The stage (spec, memory shape, software pipeline) is in chorus_stage.h.
-#include "chorus_stage.h"
+// The stage (spec, memory shape, line carry, software pipeline) is in chorus_stage_l.h, its
+// helpers in chorus_stage.h.
 #include "chorus_stage_l.h"
 
 namespace olfx {
 
-template <bool FULL>
-__global__ __launch_bounds__(ch::kThreads, 2) void chorus_block_v10(ChorusArgs a) {
-    using Stage = ch::ChStage<FULL>;
-    constexpr int kChunk = Stage::kChunk;
-    extern __shared__ __attribute__((aligned(16))) float lds[];   // [wave][3 taps][kSlots][kRow]
-    const uint32_t tid = threadIdx.x;
-    // wave index made provably wave-uniform (SGPR): the buffer descriptors and frame offsets
-    // derived from it stay scalar, so no waterfall loops around the buffer ops
-    const uint32_t wib = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
-    const uint32_t wave = blockIdx.x * (ch::kThreads / 64) + wib, lane = tid & 63u;
-    const uint32_t inst0 = wave * 32u;                  // first instance of this wave (uniform)
-    if (inst0 >= a.n) return;
-    Stage st;
-    st.init(a, lds + wib * Stage::kRegion, lane, inst0);
-
-    const uint32_t nf = a.n_frames, n = a.n;
-    const ch::Rsrc rIn = ch::rsrc(a.in, (a.plane + (uint64_t)nf * n) * 4);
-    const ch::Rsrc rOut = ch::rsrc(a.out, (a.plane + (uint64_t)nf * n) * 4);
-    const uint32_t io_v = st.ch * (uint32_t)a.plane * 4u + st.i * 4u, frame_b = n * 4u;
-    const uint32_t out_v = st.valid ? io_v : 0xFFFFFFF0u;   // invalid lanes: range check drops
-
-    float x[kChunk], xn[kChunk];
-    int C = (int)min((uint32_t)kChunk, nf);
-#pragma unroll
-    for (int k = 0; k < kChunk; ++k) x[k] = k < C ? ch::ld1<ch::kStreamAux>(rIn, io_v, (uint32_t)k * frame_b) : 0.f;
-    st.begin(x, C);
-    for (uint32_t f0 = 0; f0 < nf; f0 += kChunk) {
-        C = (int)min((uint32_t)kChunk, nf - f0);
-        const int Cn = f0 + kChunk < nf ? (int)min((uint32_t)kChunk, nf - f0 - kChunk) : 0;
-        // the next chunk's input, in flight while this one computes (unconditional loads, the
-        // frame clamped into the block; lanes past Cn get 0)
-#pragma unroll
-        for (int k = 0; k < kChunk; ++k) {
-            const float v = ch::ld1<ch::kStreamAux>(rIn, io_v, min(f0 + kChunk + (uint32_t)k, nf - 1u) * frame_b);
-            xn[k] = k < Cn ? v : 0.f;
-        }
-        st.chunk(x, C, Cn, [&](int k, float v) { ch::st1<ch::kStreamAux>(rOut, out_v, (f0 + (uint32_t)k) * frame_b, v); });
-#pragma unroll
-        for (int k = 0; k < kChunk; ++k) x[k] = xn[k];
-    }
-    st.finish(a);
-}
-
-
-// v11: the same kernel over the line-carry stage (chorus_stage_l.h); chunks alternate the line set
-// (PAR), so the chunk loop is unrolled by two.
+// chorus_block_v11: one wave = 32 instances x 2 channels over the line-carry stage
+// (chorus_stage_l.h); chunks alternate the line set (PAR), so the chunk loop is unrolled by two.
 template <bool FULL>
 __global__ __launch_bounds__(ch::kThreads, 2) void chorus_block_v11(ChorusArgs a) {
     using Stage = ch::ChStageL<FULL>;
@@ -110,14 +66,9 @@ hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s) {
         return hipErrorInvalidValue;
     const uint32_t waves = (a.n + 31) / 32;              // 32 instances x 2 channels per wave
     const uint32_t blocks = (waves + ch::kThreads / 64 - 1) / (ch::kThreads / 64);
-    const size_t lds = (size_t)(ch::kThreads / 64) * ch::ChStage<true>::kRegion * sizeof(float);
-    if (OLFX_CHORUS_V == 11) {
-        if (a.mode == 0) hipLaunchKernelGGL(chorus_block_v11<true>, dim3(blocks), dim3(ch::kThreads), lds, s, a);
-        else hipLaunchKernelGGL(chorus_block_v11<false>, dim3(blocks), dim3(ch::kThreads), lds, s, a);
-    } else {
-        if (a.mode == 0) hipLaunchKernelGGL(chorus_block_v10<true>, dim3(blocks), dim3(ch::kThreads), lds, s, a);
-        else hipLaunchKernelGGL(chorus_block_v10<false>, dim3(blocks), dim3(ch::kThreads), lds, s, a);
-    }
+    const size_t lds = (size_t)(ch::kThreads / 64) * ch::ChStageL<true>::kRegion * sizeof(float);
+    if (a.mode == 0) hipLaunchKernelGGL(chorus_block_v11<true>, dim3(blocks), dim3(ch::kThreads), lds, s, a);
+    else hipLaunchKernelGGL(chorus_block_v11<false>, dim3(blocks), dim3(ch::kThreads), lds, s, a);
     return hipGetLastError();
 }
 

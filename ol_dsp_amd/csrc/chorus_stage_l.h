@@ -174,11 +174,7 @@ struct ChStageL {
 #pragma unroll
         for (int t = 0; t < kTaps; ++t) {
             const uint32_t lnext = (w + (uint32_t)s[t]) >> 4;
-#ifdef OLFX_V11_FRESH
-            const bool carry = ((OLFX_V11_FRESH >> t) & 1) == 0 && !first && lnext == lcur[t] + 1u;   // debug: reload taps in mask
-#else
             const bool carry = !first && lnext == lcur[t] + 1u;
-#endif
             lcur[t] = lnext;
             pk[t] = (int)((uint32_t)s[t] << 1) | (carry ? 0 : 1);
         }

@@ -9,83 +9,65 @@
 // voice samples.
 //
 // HBM-bound and small beside the voice kernel: one 4-B read per voice sample, one 4-B read and one
-// 4-B write per bus sample.  One lane = (bus, frame), buses fastest: the lanes of a wave read the
-// voices of neighbouring buses in one frame row, so the lines one add step touches are the lines
-// the next step reuses (from the L1).
+// 4-B write per bus sample.  Buses run fastest across lanes: the lanes of a wave read the voices of
+// neighbouring buses in one frame row, so the lines one add step touches are the lines the next
+// step reuses (from the L1).
 #include "olfx_internal.h"
 
 namespace olfx {
 
-__global__ __launch_bounds__(256) void voice_mix_v1(MixArgs a) {
-    const uint32_t b = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t f = blockIdx.y;
-    if (b >= a.n_buses) return;
-    const float *row = a.in + (size_t)f * a.n;
-    float *dst = a.out + (size_t)f * a.n_buses + b;
-    const uint32_t k1 = a.off[b + 1];
-    uint32_t k = a.off[b];
-    float acc = *dst;
-    // four loads in flight per step; the adds stay in order
-    for (; k + 4 <= k1; k += 4) {
-        const float v0 = row[a.order[k]], v1 = row[a.order[k + 1]];
-        const float v2 = row[a.order[k + 2]], v3 = row[a.order[k + 3]];
-        acc = acc + v0;
-        acc = acc + v1;
-        acc = acc + v2;
-        acc = acc + v3;
-    }
-    for (; k < k1; ++k) acc = acc + row[a.order[k]];
-    *dst = acc;
-}
-
-// v2: one lane = (bus, four frames).  A bus's voice indices are read once per four frames instead
-// of once per frame, and the four frames' loads of one voice are independent, so eight loads are
-// in flight per unrolled step.  Every frame's adds still run voice by voice in list order.
+// One lane = (bus, four frames).  A bus's voice indices are read once per four frames instead of
+// once per frame, and the four frames' loads of one voice are independent, so eight loads are in
+// flight per unrolled step.  Every frame's adds still run voice by voice in list order.  A block
+// row loops over frame tiles (grid.y is capped), so any frame count launches.
 constexpr uint32_t kMixFr = 4;
+constexpr uint32_t kMixMaxRows = 4096;
 
 __global__ __launch_bounds__(256) void voice_mix_v2(MixArgs a) {
     const uint32_t b = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t f0 = blockIdx.y * kMixFr;
     if (b >= a.n_buses) return;
-    const uint32_t nfr = a.n_frames - f0 < kMixFr ? a.n_frames - f0 : kMixFr;   // uniform per block
-    const float *row = a.in + (size_t)f0 * a.n;
-    float *dst = a.out + (size_t)f0 * a.n_buses + b;
-    const uint32_t k1 = a.off[b + 1];
-    uint32_t k = a.off[b];
-    if (nfr == kMixFr) {
-        float acc[kMixFr];
+    for (uint32_t f0 = blockIdx.y * kMixFr; f0 < a.n_frames; f0 += gridDim.y * kMixFr) {
+        const uint32_t nfr = a.n_frames - f0 < kMixFr ? a.n_frames - f0 : kMixFr;   // uniform per block
+        const float *row = a.in + (size_t)f0 * a.n;
+        float *dst = a.out + (size_t)f0 * a.n_buses + b;
+        const uint32_t k1 = a.off[b + 1];
+        uint32_t k = a.off[b];
+        if (nfr == kMixFr) {
+            float acc[kMixFr];
 #pragma unroll
-        for (uint32_t j = 0; j < kMixFr; ++j) acc[j] = dst[(size_t)j * a.n_buses];
-        for (; k + 2 <= k1; k += 2) {
-            const uint32_t i0 = a.order[k], i1 = a.order[k + 1];
-            float v0[kMixFr], v1[kMixFr];
+            for (uint32_t j = 0; j < kMixFr; ++j) acc[j] = dst[(size_t)j * a.n_buses];
+            for (; k + 2 <= k1; k += 2) {
+                const uint32_t i0 = a.order[k], i1 = a.order[k + 1];
+                float v0[kMixFr], v1[kMixFr];
 #pragma unroll
-            for (uint32_t j = 0; j < kMixFr; ++j) {
-                v0[j] = row[(size_t)j * a.n + i0];
-                v1[j] = row[(size_t)j * a.n + i1];
+                for (uint32_t j = 0; j < kMixFr; ++j) {
+                    v0[j] = row[(size_t)j * a.n + i0];
+                    v1[j] = row[(size_t)j * a.n + i1];
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < kMixFr; ++j) acc[j] = (acc[j] + v0[j]) + v1[j];
+            }
+            if (k < k1) {
+                const uint32_t i0 = a.order[k];
+#pragma unroll
+                for (uint32_t j = 0; j < kMixFr; ++j) acc[j] = acc[j] + row[(size_t)j * a.n + i0];
             }
 #pragma unroll
-            for (uint32_t j = 0; j < kMixFr; ++j) acc[j] = (acc[j] + v0[j]) + v1[j];
-        }
-        if (k < k1) {
-            const uint32_t i0 = a.order[k];
-#pragma unroll
-            for (uint32_t j = 0; j < kMixFr; ++j) acc[j] = acc[j] + row[(size_t)j * a.n + i0];
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kMixFr; ++j) dst[(size_t)j * a.n_buses] = acc[j];
-    } else {
-        for (uint32_t j = 0; j < nfr; ++j) {
-            float acc = dst[(size_t)j * a.n_buses];
-            for (uint32_t q = k; q < k1; ++q) acc = acc + row[(size_t)j * a.n + a.order[q]];
-            dst[(size_t)j * a.n_buses] = acc;
+            for (uint32_t j = 0; j < kMixFr; ++j) dst[(size_t)j * a.n_buses] = acc[j];
+        } else {
+            for (uint32_t j = 0; j < nfr; ++j) {
+                float acc = dst[(size_t)j * a.n_buses];
+                for (uint32_t q = k; q < k1; ++q) acc = acc + row[(size_t)j * a.n + a.order[q]];
+                dst[(size_t)j * a.n_buses] = acc;
+            }
         }
     }
 }
 
 hipError_t launch_mix(const MixArgs &a, hipStream_t s) {
     if (a.n_buses == 0 || a.n_frames == 0) return hipSuccess;
-    const dim3 grid((a.n_buses + 255) / 256, (a.n_frames + kMixFr - 1) / kMixFr);
+    const uint32_t rows = (a.n_frames + kMixFr - 1) / kMixFr;
+    const dim3 grid((a.n_buses + 255) / 256, rows < kMixMaxRows ? rows : kMixMaxRows);
     hipLaunchKernelGGL(voice_mix_v2, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }

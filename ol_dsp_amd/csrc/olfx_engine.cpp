@@ -167,9 +167,11 @@ void default_params(int kind, float *p) {
 // Coefficient derivation (control rate, host).  These restate the reference setters.
 // ---------------------------------------------------------------------------------------------
 uint32_t dattorro_predelay_samples(float v) {
-    // verb.cpp:137-139: uint16(value * 4800.f); the engine accepts [0, 1]
+    // verb.cpp:137-139: uint16(value * 4800.f) into DelayBuffer_setDelay, whose read offset
+    // mask + 1 - delay (verb.cpp:59-61) on the 8192-sample pre-delay ring makes the effective delay
+    // uint16(value * 4800) mod 8192 (olfx_set_params accepts value * 4800 in [0, 65536))
     float d = v * 4800.0f;
-    return d <= 0.0f ? 0u : (uint32_t)(uint16_t)d;
+    return d <= 0.0f ? 0u : ((uint32_t)(uint16_t)d & (kDtSize[DT_PRE] - 1u));
 }
 
 void derive_dattorro(const float *p, float *c) {
@@ -379,6 +381,7 @@ struct olfx_engine {
     std::vector<olfx_event> events;
     // voice buses (olfx_mix_config): [n_buses + 1] offsets, then the voice lists
     uint32_t *mix_dev = nullptr;
+    hipEvent_t mix_done = nullptr;          // recorded after every olfx_mix launch
     uint32_t n_buses = 0;
     std::vector<float> h_vstate;                         // host copy for event application
 
@@ -832,6 +835,7 @@ int olfx_destroy(olfx_engine *e) {
     if (e->d_in) (void)hipFree(e->d_in);
     if (e->d_out) (void)hipFree(e->d_out);
     if (e->mix_dev) (void)hipFree(e->mix_dev);
+    if (e->mix_done) (void)hipEventDestroy(e->mix_done);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return OLFX_OK;
@@ -849,19 +853,23 @@ int olfx_set_params(olfx_engine *e, uint32_t first, uint32_t count, uint32_t fie
     if (!e) return OLFX_E_ARG;
     if (!values || (uint64_t)first + count > e->n || (uint64_t)field0 + n_fields > e->n_params)
         return e->fail(OLFX_E_ARG, "olfx_set_params: range out of bounds");
+    // validate everything first: a rejected call changes nothing
     for (uint32_t f = 0; f < n_fields; ++f) {
         const uint32_t field = field0 + f;
         const bool predelay = (e->kind == OLFX_KIND_DATTORRO && field == OLFX_DT_PREDELAY) ||
                               (e->kind == OLFX_KIND_CHAIN && field == OLFX_CN_VERB0 + OLFX_DT_PREDELAY);
         for (uint32_t k = 0; k < count; ++k) {
-            float v = values[(size_t)f * count + k];
+            const float v = values[(size_t)f * count + k];
             if (!std::isfinite(v)) return e->fail(OLFX_E_ARG, "olfx_set_params: non-finite value");
-            // the pre-delay ring holds MAX_PREDELAY = 4800 samples (verb.cpp:137-139, :177)
-            if (predelay && (v < 0.f || v > 1.f))
-                return e->fail(OLFX_E_ARG, "olfx_set_params: pre-delay outside [0,1]");
-            e->params[(size_t)field * e->n + first + k] = v;
+            // the reference converts value * MAX_PREDELAY (4800) to uint16 (verb.cpp:137-139): values
+            // whose product leaves [0, 65536) have no defined meaning there
+            if (predelay && !(v >= 0.f && v * 4800.0f < 65536.0f))
+                return e->fail(OLFX_E_ARG, "olfx_set_params: pre-delay outside [0, 65536/4800)");
         }
     }
+    for (uint32_t f = 0; f < n_fields; ++f)
+        for (uint32_t k = 0; k < count; ++k)
+            e->params[(size_t)(field0 + f) * e->n + first + k] = values[(size_t)f * count + k];
     if (is_voice_kind(e->kind))
         for (uint32_t k = 0; k < count; ++k) e->configured[first + k] = 1;
     e->dirty = true;
@@ -1037,15 +1045,21 @@ int olfx_mix_config(olfx_engine *e, uint32_t n_buses, const uint32_t *offsets, c
         h.insert(h.end(), order, order + len);
     }
     HIPCHK(e, hipSetDevice(e->device));
-    if (e->mix_dev) {                       // a mix still in flight may read the old lists
-        HIPCHK(e, hipDeviceSynchronize());
-        HIPCHK(e, hipFree(e->mix_dev));
-        e->mix_dev = nullptr;
+    // the new lists first: a failed allocation leaves the current configuration in place
+    uint32_t *fresh = nullptr;
+    if (n_buses) {
+        HIPCHK(e, hipMalloc((void **)&fresh, h.size() * 4));
+        const hipError_t r = hipMemcpy(fresh, h.data(), h.size() * 4, hipMemcpyHostToDevice);
+        if (r != hipSuccess) {
+            (void)hipFree(fresh);
+            return e->hip_fail(r, "olfx_mix_config upload");
+        }
     }
-    e->n_buses = 0;
-    if (!n_buses) return OLFX_OK;
-    HIPCHK(e, hipMalloc((void **)&e->mix_dev, h.size() * 4));
-    HIPCHK(e, hipMemcpy(e->mix_dev, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    if (e->mix_dev) {   // the last mix launched (on any stream) may still read the old lists
+        if (e->mix_done) HIPCHK(e, hipEventSynchronize(e->mix_done));
+        HIPCHK(e, hipFree(e->mix_dev));
+    }
+    e->mix_dev = fresh;
     e->n_buses = n_buses;
     return OLFX_OK;
 }
@@ -1057,6 +1071,7 @@ int olfx_mix(olfx_engine *e, const float *voice_out, float *bus_out, uint32_t n_
     if (!voice_out || !bus_out) return e->fail(OLFX_E_ARG, "olfx_mix: null buffer");
     if (io_flags != OLFX_IO_DEVICE && io_flags != OLFX_IO_HOST) return e->fail(OLFX_E_ARG, "olfx_mix: bad io_flags");
     HIPCHK(e, hipSetDevice(e->device));
+    if (!e->mix_done) HIPCHK(e, hipEventCreateWithFlags(&e->mix_done, hipEventDisableTiming));
     hipStream_t s = (hipStream_t)stream;
     MixArgs a{};
     a.off = e->mix_dev;
@@ -1076,6 +1091,7 @@ int olfx_mix(olfx_engine *e, const float *voice_out, float *bus_out, uint32_t n_
         a.in = e->d_in;
         a.out = e->d_out;
         if ((r = launch_mix(a, s)) != hipSuccess) return e->hip_fail(r, "mix launch");
+        HIPCHK(e, hipEventRecord(e->mix_done, s));
         HIPCHK(e, hipMemcpyAsync(e->h_out, e->d_out, fout * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(e, hipStreamSynchronize(s));
         std::memcpy(bus_out, e->h_out, fout * 4);
@@ -1084,6 +1100,7 @@ int olfx_mix(olfx_engine *e, const float *voice_out, float *bus_out, uint32_t n_
     a.in = voice_out;
     a.out = bus_out;
     if ((r = launch_mix(a, s)) != hipSuccess) return e->hip_fail(r, "mix launch");
+    HIPCHK(e, hipEventRecord(e->mix_done, s));
     return OLFX_OK;
 }
 
@@ -1138,9 +1155,9 @@ const char *olfx_kernel_name(const olfx_engine *e) {
     switch (e->kind) {
     case OLFX_KIND_DATTORRO: return "dattorro_block_v4";
     case OLFX_KIND_CHORUS:
-    case OLFX_KIND_PITCHSHIFT: return OLFX_CHORUS_V == 11 ? "chorus_block_v11" : "chorus_block_v10";
-    case OLFX_KIND_VOICE: return OLFX_VOICE_V == 5 ? "voice_block_v5" : "voice_block_v4";
-    case OLFX_KIND_VOICE_MOOG: return "voice_block_v4<true>";
+    case OLFX_KIND_PITCHSHIFT: return "chorus_block_v11";
+    case OLFX_KIND_VOICE: return "voice_block_v5";
+    case OLFX_KIND_VOICE_MOOG: return "voice_block_v4";
     case OLFX_KIND_CHAIN: return "chain_block_v1";
     case OLFX_KIND_FXRACK: return "fxrack_block_v2";
     default: return "";

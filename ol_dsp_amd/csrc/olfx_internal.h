@@ -11,17 +11,6 @@
 
 #define OLFX_HD __host__ __device__ __forceinline__
 
-// chorus / pitch-shift kernel generation: 11 = line carry (chorus_stage_l.h), 10 = per-chunk
-// windows (chorus_stage.h).  A build knob for A/B timing (tools/ab.sh).
-#ifndef OLFX_CHORUS_V
-#define OLFX_CHORUS_V 11
-#endif
-// Svf voice kernel generation: 5 = four balanced role waves (voice_block_v5), 4 = three role
-// waves (voice_block_v4).  A build knob for A/B timing.
-#ifndef OLFX_VOICE_V
-#define OLFX_VOICE_V 5
-#endif
-
 namespace olfx {
 
 // ----------------------------------------------------------------------------------------------

@@ -135,18 +135,16 @@ __device__ __forceinline__ void for_chunk(uint32_t m, F &&f) {
     }
 }
 
-// One workgroup = 64 voices, the voice pipelined over waves that hand each sample's values on
-// through an LDS double buffer (one barrier per 16-sample chunk):
-//   amp role    : amp envelope, portamento, oscillator          -> (src, amp)
-//   cutoff role : filter envelope, cutoff, Svf::SetFreq         -> (fq, damp)
-//                 (ladder: LadderFilter::SetFreq -> SetAlpha     -> (alpha, Qadjust))
-//   filter role : Svf passes / LadderFilter::Process, output store
-// Svf voices run the three roles on three waves (96 of them per 32 CUs' worth of voices, so
-// 32,768 voices occupy 1,536 waves); the ladder's serial recurrence dominates its voice, so the
-// amp and cutoff roles share one wave there (two waves per workgroup).
-template <bool MOOG>
-__global__ __launch_bounds__(MOOG ? 128 : 192) void voice_block_v4(VoiceArgs a) {
-    constexpr uint32_t kRoles = MOOG ? 2u : 3u;
+// voice_block_v4: the MoogFilter voice.  One workgroup = 64 voices, the voice pipelined over two
+// waves that hand each sample's values on through an LDS double buffer (one barrier per 16-sample
+// chunk):
+//   feed wave   : amp envelope, portamento, oscillator, filter envelope, cutoff,
+//                 LadderFilter::SetFreq -> SetAlpha          -> (src * drive, amp, alpha, Qadjust)
+//   filter wave : LadderFilter::Process, output store
+// The ladder's serial recurrence dominates the voice, so the feed roles share one wave.  (The Svf
+// voice runs voice_block_v5 below, over four role waves.)
+__global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
+    constexpr uint32_t kRoles = 2u;
     __shared__ float4 q[2][kVcChunk][64];
     __shared__ uint32_t fflags[64];
     const uint32_t n = a.n;
@@ -170,9 +168,9 @@ __global__ __launch_bounds__(MOOG ? 128 : 192) void voice_block_v4(VoiceArgs a) 
         const float amp_amt = c[VCC_AMP_AMT * n + i], port_c = c[VCC_PORT_COEF * n + i];
         const float inv_sr = c[VCC_INV_SR * n + i], freq = s[VCS_FREQ * n + i];
         const float cutoff = c[VCC_CUTOFF * n + i], fenv_amt = c[VCC_FENV_AMT * n + i];
-        // Svf: damp_res, fc_max, 1/(2 sr); ladder: drive_scaled (VCC_DRIVE), 1/(4 sr) (VCC_FC_MAX)
-        const float damp_res = c[VCC_DAMP_RES * n + i], drive = c[VCC_DRIVE * n + i];
-        const float fc_max = c[VCC_FC_MAX * n + i], inv_2sr = 1.0f / (c[VCC_SR * n + i] * 2.0f);
+        // ladder: drive_scaled (VCC_DRIVE), 1/(4 sr) (VCC_FC_MAX)
+        const float drive = c[VCC_DRIVE * n + i];
+        const float fc_max = c[VCC_FC_MAX * n + i];
         float phase = s[VCS_PHASE * n + i];
         float port_z = s[VCS_PORT_Z * n + i];
         bool gprev_a = (flags0 >> 6) & 1u, gprev_f = (flags0 >> 7) & 1u;
@@ -203,29 +201,16 @@ __global__ __launch_bounds__(MOOG ? 128 : 192) void voice_block_v4(VoiceArgs a) 
                         phase += inc;
                         phase = phase > 1.0f ? phase - 1.0f : phase;
                         const float src = o * 0.5f;
-                        ab = make_float2(MOOG ? src * drive : src, amp);   // ladder: Process's input scaling
+                        ab = make_float2(src * drive, amp);   // ladder: Process's input scaling
                     }
                     if constexpr (CUT) {
                         const float fe = ef.step();
                         const float fc_in = cutoff + ((fe * 20000.0f) * fenv_amt);
-                        if (MOOG) {
-                            // LadderFilter::SetFreq (unclamped) -> SetAlpha
-                            const float wc = fc_in * 2.0f * 3.1415927410125732f * fc_max;
-                            const float wc2 = wc * wc;
-                            cd.x = 0.9892f * wc - 0.4324f * wc2 + 0.1381f * wc * wc2 - 0.0202f * wc2 * wc2;
-                            cd.y = 1.006f + 0.0536f * wc - 0.095f * wc2 - 0.05f * wc2 * wc2;
-                        } else {
-                            // Svf::SetFreq; its divisions use the hardware reciprocal (~1 ulp, within
-                            // the voice tolerance, like sin_quarter)
-                            const float fc = fminf(fmaxf(fc_in, 1.0e-6f), fc_max);
-                            const float fcn = fc * inv_2sr;
-                            const float arg = 0.25f < fcn ? 0.25f : fcn;
-                            const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
-                            const float lim = 2.0f * __builtin_amdgcn_rcpf(fq) - fq * 0.5f;
-                            const float dlim = 2.0f < lim ? 2.0f : lim;
-                            cd.x = fq;
-                            cd.y = damp_res < dlim ? damp_res : dlim;
-                        }
+                        // LadderFilter::SetFreq (unclamped) -> SetAlpha
+                        const float wc = fc_in * 2.0f * 3.1415927410125732f * fc_max;
+                        const float wc2 = wc * wc;
+                        cd.x = 0.9892f * wc - 0.4324f * wc2 + 0.1381f * wc * wc2 - 0.0202f * wc2 * wc2;
+                        cd.y = 1.006f + 0.0536f * wc - 0.095f * wc2 - 0.05f * wc2 * wc2;
                     }
                     if constexpr (AMP && CUT) {
                         qb[j * 64] = make_float4(ab.x, ab.y, cd.x, cd.y);
@@ -251,26 +236,17 @@ __global__ __launch_bounds__(MOOG ? 128 : 192) void voice_block_v4(VoiceArgs a) 
         if constexpr (CUT) s[VCS_ENVF_X * n + i] = ef.x;
     };
     if (!filt_role) {
-        if (MOOG) feed(std::true_type{}, std::true_type{});
-        else if (wave == 0) feed(std::true_type{}, std::false_type{});
-        else feed(std::false_type{}, std::true_type{});
+        feed(std::true_type{}, std::true_type{});
     } else {
-        // ---------------- filter role: Svf passes or LadderFilter::Process ----------------
+        // ---------------- filter role: LadderFilter::Process ----------------
         const float k_or_unused = c[VCC_DAMP_RES * n + i];     // ladder: K (VCC_LADDER_K)
-        const float drive = c[VCC_DRIVE * n + i];              // Svf drive
-        float low = 0.f, band = 0.f;
         Ladder L;
-        if (MOOG) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                L.z0[k] = s[(VCS_LZ0 + k) * n + i];
-                L.z1[k] = s[(VCS_LZ1 + k) * n + i];
-            }
-            L.old = s[VCS_LOLD * n + i];
-        } else {
-            low = s[VCS_LOW * n + i];
-            band = s[VCS_BAND * n + i];
+        for (int k = 0; k < 4; ++k) {
+            L.z0[k] = s[(VCS_LZ0 + k) * n + i];
+            L.z1[k] = s[(VCS_LZ1 + k) * n + i];
         }
+        L.old = s[VCS_LOLD * n + i];
         float *out = a.out + i;
         for (uint32_t k = 0; k <= nchunks; ++k) {
             if (k > 0) {
@@ -280,7 +256,7 @@ __global__ __launch_bounds__(MOOG ? 128 : 192) void voice_block_v4(VoiceArgs a) 
                 for_chunk(m, [&](uint32_t j) {
                     const float4 v = qb[j * 64];
                     float y;
-                    if (MOOG) {
+                    {
                         // LadderFilter::Process, LP24
                         const float input = v.x, alpha = v.z, qadj = v.w;
                         float total = 0.0f, interp = 0.0f;
@@ -298,20 +274,6 @@ __global__ __launch_bounds__(MOOG ? 128 : 192) void voice_block_v4(VoiceArgs a) 
                         }
                         L.old = input;
                         y = total * v.y;
-                    } else {
-                        // Svf::Process: two passes, Low() = average of the two low outputs
-                        const float src = v.x, fq = v.z, damp = v.w;
-                        float notch = src - damp * band;
-                        low = low + fq * band;
-                        float high = notch - low;
-                        band = fq * high + band - drive * band * band * band;
-                        float out_low = 0.5f * low;
-                        notch = src - damp * band;
-                        low = low + fq * band;
-                        high = notch - low;
-                        band = fq * high + band - drive * band * band * band;
-                        out_low += 0.5f * low;
-                        y = out_low * v.y;
                     }
                     out[(size_t)(f0 + j) * n] = y;
                 });
@@ -319,22 +281,17 @@ __global__ __launch_bounds__(MOOG ? 128 : 192) void voice_block_v4(VoiceArgs a) 
             __syncthreads();
         }
         __syncthreads();                                      // the flags hand-off barrier
-        if (MOOG) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                s[(VCS_LZ0 + k) * n + i] = L.z0[k];
-                s[(VCS_LZ1 + k) * n + i] = L.z1[k];
-            }
-            s[VCS_LOLD * n + i] = L.old;
-        } else {
-            s[VCS_LOW * n + i] = low;
-            s[VCS_BAND * n + i] = band;
+        for (int k = 0; k < 4; ++k) {
+            s[(VCS_LZ0 + k) * n + i] = L.z0[k];
+            s[(VCS_LZ1 + k) * n + i] = L.z1[k];
         }
+        s[VCS_LOLD * n + i] = L.old;
     }
 }
 
 // ---------------------------------------------------------------------------------------------
-// voice_block_v5 (SvfFilter voices, OLFX_VOICE_V 5): v4's arithmetic, operation for operation, over
+// voice_block_v5 (SvfFilter voices): v4's arithmetic, operation for operation, over
 // FOUR role waves per workgroup of 64 voices, balanced across the SIMDs of a CU.
 //   v4's roles cost about 40 / 34 / 30 VALU instructions per sample (amp / cutoff / filter; with
 //   -ffp-contract=off every a*b+c is two).  Two workgroups share a CU: six waves on four SIMDs, so
@@ -344,16 +301,12 @@ __global__ __launch_bounds__(MOOG ? 128 : 192) void voice_block_v4(VoiceArgs a) 
 //     OSC  : the polyBLEP saw from (t, inc)                                     -> (src, amp)
 //     FREQ : Svf::SetFreq(fc_in)                                                -> (fq, damp)
 //     FILT : the two Svf passes, Low() * amp, the output store
-//   about 22 / 23 / 30 / 29 instructions: eight waves per CU, two per SIMD.  Two co-resident
-//   workgroups whose roles differ by two on every SIMD pair ENV with FREQ and OSC with FILT; the
-//   rotation is taken from the workgroup's slot on its CU (OLFX_VC_ROT).
+//   about 22 / 23 / 30 / 29 instructions: eight waves per CU, two per SIMD.  Role = wave: rotating
+//   the roles of co-resident workgroups (to pair ENV with FREQ and OSC with FILT on every SIMD) was
+//   measured slower (0.0441 vs 0.0422 ms) and is not built.
 // A three-stage pipeline over 16-sample chunks: at step k ENV makes chunk k, OSC and FREQ chunk
 // k-1, FILT chunk k-2; one barrier per step; 64 KB of LDS per workgroup.
 // ---------------------------------------------------------------------------------------------
-#ifndef OLFX_VC_ROT
-#define OLFX_VC_ROT 0   // 0: role = wave (measured fastest: 0.0422 vs 0.0441 ms); 1: rotated by HW_ID.TG_ID parity; 2: by (blockIdx >> 8)
-#endif                  // parity; 3: roles follow the SIMDs (HW_ID.SIMD_ID), rotated as 1
-
 __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     __shared__ float4 eq[2][kVcChunk][64];      // ENV -> OSC, FREQ: (t, inc, amp, fc_in)
     __shared__ float2 sq[2][kVcChunk][64];      // OSC -> FILT: (src, amp)
@@ -367,27 +320,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     const uint32_t nsteps = (nf + kVcChunk - 1) / kVcChunk + 2;
     const float *c = a.coef;
     float *s = a.state;
-#if OLFX_VC_ROT == 0
-    const uint32_t role = wave;
-#else
-    // every wave publishes its HW_ID (one word per wave of chunk buffer 1, first written at step 1)
-    uint32_t *ids = reinterpret_cast<uint32_t *>(&eq[1][0][0]);
-    if (lane == 0) ids[wave] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
-    __syncthreads();
-#if OLFX_VC_ROT == 2
-    const uint32_t rot = ((blockIdx.x >> 8) & 1u) << 1;
-#else
-    const uint32_t rot = ((ids[0] >> 16) & 1u) << 1;          // TG_ID parity: the slot on the CU
-#endif
-#if OLFX_VC_ROT == 3
-    uint32_t seen = 0;
-    for (uint32_t w = 0; w < 4; ++w) seen |= 1u << ((ids[w] >> 4) & 3u);
-    const uint32_t base = seen == 15u ? (ids[wave] >> 4) & 3u : wave;
-#else
-    const uint32_t base = wave;
-#endif
-    const uint32_t role = (uint32_t)__builtin_amdgcn_readfirstlane((int)((base + rot) & 3u));
-#endif
+    const uint32_t role = wave;                  // role = wave
     auto len = [&](uint32_t k) {             // frames of chunk k (the last may be short)
         const uint32_t f0 = k * kVcChunk;
         return nf - f0 < (uint32_t)kVcChunk ? nf - f0 : (uint32_t)kVcChunk;
@@ -501,9 +434,8 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
 hipError_t launch_voice(const VoiceArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
     const dim3 grid((a.n + 63) / 64);     // 64 voices per workgroup, one wave per role
-    if (a.moog) hipLaunchKernelGGL(voice_block_v4<true>, grid, dim3(128), 0, s, a);
-    else if (OLFX_VOICE_V == 5) hipLaunchKernelGGL(voice_block_v5, grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(voice_block_v4<false>, grid, dim3(192), 0, s, a);
+    if (a.moog) hipLaunchKernelGGL(voice_block_v4, grid, dim3(128), 0, s, a);
+    else hipLaunchKernelGGL(voice_block_v5, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

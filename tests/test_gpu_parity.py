@@ -109,6 +109,34 @@ def test_dattorro_per_instance_predelay(cuda):
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
 
+def test_dattorro_predelay_beyond_max(cuda):
+    """Pre-delays past MAX_PREDELAY: the reference accepts any value whose product with 4800 fits
+    uint16 (verb.cpp:137-139); DelayBuffer_setDelay's offset mask + 1 - delay (verb.cpp:59-61) on
+    the 8192-sample ring makes the effective delay that product mod 8192 (8192 acts as 0, 8193 as
+    1).  Values outside [0, 65536/4800) are rejected, not clamped."""
+    ks = np.array([4801, 6000, 8190, 8191, 8192, 8193, 8196, 8200, 12000, 16384, 16389, 65535], np.float64)
+    n = 64
+    rng = np.random.default_rng(78)
+    p = dt_params(rng, n, 0.0)
+    p[0, :] = (rng.integers(4801, 65536, n) / 4800).astype(np.float32)
+    p[0, :len(ks)] = (ks / 4800).astype(np.float32)
+    x = fast_noise(n, 12800, seed=78)
+    e = engine("dattorro", n)
+    e.set_params(0, p)
+    y = run_gpu(e, x, [256] * 40 + [2560], cuda)
+    ref = O.Dattorro(n)
+    for i in range(n):
+        for f in range(7):
+            ref.set(i, f, float(p[f, i]))
+    yr = ref.process(x, threads=8)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+    for bad in (-0.01, 65536 / 4800, 20.0):
+        q = p.copy()
+        q[0, 3] = bad
+        with pytest.raises(Exception):
+            e.set_params(0, q)
+
+
 def test_dattorro_long_run_wraps(cuda):
     """70,000 frames: the modulation turn at t = 32768 and the uint16 wrap of t at 65536."""
     n = 64
