@@ -129,15 +129,31 @@ enum {
 #define OLFX_CN_VERB0     (OLFX_CH_NPARAMS + OLFX_PS_NPARAMS)
 #define OLFX_CN_NPARAMS   (OLFX_CH_NPARAMS + OLFX_PS_NPARAMS + OLFX_DT_NPARAMS)
 
-/* ---- note events (voices) ---- */
-enum { OLFX_EV_NOTE_OFF = 0, OLFX_EV_NOTE_ON = 1 };
+/* ---- note events (voices) ----
+   The ol::synth::Voice calls that change a voice's gate or pitch (Voice.h:33-57), as SynthVoice
+   implements them (SynthVoice.h:231-268):
+     NOTE_ON        NoteOn(note, vel)  = GateOn + freq_ = mtof(note) + Retrigger(true) on both envelopes
+     NOTE_OFF       NoteOff(note, vel) = GateOff
+     GATE_ON        GateOn()           = gate = true (the envelopes see the rising edge, no retrigger)
+     GATE_OFF       GateOff()          = gate = false
+     SET_FREQUENCY  SetFrequency(hz)   = freq_ = hz (olfx_voice_event.value; olfx_voice_events only) */
+enum { OLFX_EV_NOTE_OFF = 0, OLFX_EV_NOTE_ON = 1, OLFX_EV_GATE_ON = 2, OLFX_EV_GATE_OFF = 3,
+       OLFX_EV_SET_FREQUENCY = 4 };
 typedef struct olfx_event {
     uint32_t inst;      /* instance index */
-    uint8_t  type;      /* OLFX_EV_* */
+    uint8_t  type;      /* OLFX_EV_* (not SET_FREQUENCY) */
     uint8_t  note;      /* MIDI note (NoteOn: freq = mtof(note)) */
     uint8_t  velocity;  /* unused by SynthVoice (SynthVoice.h:245) */
     uint8_t  pad;
 } olfx_event;
+typedef struct olfx_voice_event {
+    uint32_t inst;      /* instance index */
+    uint8_t  type;      /* OLFX_EV_* */
+    uint8_t  note;      /* NOTE_ON: MIDI note */
+    uint8_t  velocity;  /* unused by SynthVoice */
+    uint8_t  pad;
+    float    value;     /* SET_FREQUENCY: Hz (finite); else unused */
+} olfx_voice_event;
 
 /* ---- control changes (MIDI CC / hardware controls; corelib/cc_map.h numbers) ----
    The reference's UpdateMidiControl(control, 0..127) / UpdateHardwareControl(control, float)
@@ -206,6 +222,13 @@ int olfx_control(olfx_engine *e, const olfx_control_event *ev, uint32_t n);
 
 /* Queue note events (voices); applied in order at the start of the next olfx_process. */
 int olfx_note_events(olfx_engine *e, const olfx_event *ev, uint32_t n);
+/* The same queue with SET_FREQUENCY (Voice::SetFrequency, SynthVoice.h:264-267) as well. */
+int olfx_voice_events(olfx_engine *e, const olfx_voice_event *ev, uint32_t n);
+
+/* Update() of instances [first, first + count) with their current parameters (SynthVoice.h:66-98,
+   Fx.h Update()): for voices, the first Update() ends SynthVoice::Init's component defaults
+   (olfx_set_params and olfx_control imply it).  Applied at the next olfx_process. */
+int olfx_update(olfx_engine *e, uint32_t first, uint32_t count);
 
 /* Process n_frames (multiple of 4) for all instances.  `stream` is a hipStream_t; NULL is the
    HIP default (null) stream, as everywhere in HIP; olfx_stream(e) is the engine's own stream.

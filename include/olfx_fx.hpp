@@ -260,6 +260,11 @@ protected:
     void control(uint8_t cc, int source, float value) {
         check(olfx_sample_control(need(), cc, source, value), nullptr, "olfx_sample_control");
     }
+    void voice_event(uint8_t type, uint8_t midi_note, uint8_t velocity, float value) {
+        check(olfx_sample_voice_event(need(), type, midi_note, velocity, value), nullptr, "olfx_sample_voice_event");
+    }
+    void update() { check(olfx_sample_update(need()), nullptr, "olfx_sample_update"); }
+    bool live() const { return s_ != nullptr; }
 
 private:
     olfx_sample *need() const {

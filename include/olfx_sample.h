@@ -48,6 +48,9 @@ int olfx_sample_destroy(olfx_sample *s);
    olfx_set_param), note event (voices) and control change (as olfx_control). */
 int olfx_sample_set_param(olfx_sample *s, uint32_t field, float value);
 int olfx_sample_note(olfx_sample *s, uint8_t type, uint8_t note, uint8_t velocity);
+/* Any voice event (olfx_voice_event: GateOn / GateOff / SetFrequency as well) and Update(). */
+int olfx_sample_voice_event(olfx_sample *s, uint8_t type, uint8_t note, uint8_t velocity, float value);
+int olfx_sample_update(olfx_sample *s);
 int olfx_sample_control(olfx_sample *s, uint8_t control, int source, float value);
 
 /* One frame: in[in_channels] (NULL for voices) -> out[out_channels] (olfx_kind_info_get). */

@@ -64,6 +64,20 @@ class Event(ctypes.Structure):
     ]
 
 
+class VoiceEvent(ctypes.Structure):
+    _fields_ = [
+        ("inst", ctypes.c_uint32),
+        ("type", ctypes.c_uint8),
+        ("note", ctypes.c_uint8),
+        ("velocity", ctypes.c_uint8),
+        ("pad", ctypes.c_uint8),
+        ("value", ctypes.c_float),
+    ]
+
+
+EV_NOTE_OFF, EV_NOTE_ON, EV_GATE_ON, EV_GATE_OFF, EV_SET_FREQUENCY = 0, 1, 2, 3, 4
+
+
 class ControlEvent(ctypes.Structure):
     _fields_ = [
         ("inst", ctypes.c_uint32),
@@ -93,6 +107,8 @@ SIGNATURES = {
     "olfx_set_param": (ctypes.c_int, [_P, _U32, _U32, _F]),
     "olfx_get_param": (ctypes.c_int, [_P, _U32, _U32, ctypes.POINTER(_F)]),
     "olfx_note_events": (ctypes.c_int, [_P, ctypes.POINTER(Event), _U32]),
+    "olfx_voice_events": (ctypes.c_int, [_P, ctypes.POINTER(VoiceEvent), _U32]),
+    "olfx_update": (ctypes.c_int, [_P, _U32, _U32]),
     "olfx_control_map": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint8, ctypes.c_int, _F, ctypes.POINTER(_U32),
                                         ctypes.POINTER(_F)]),
     "olfx_control": (ctypes.c_int, [_P, ctypes.POINTER(ControlEvent), _U32]),
@@ -115,6 +131,8 @@ SIGNATURES = {
     "olfx_sample_destroy": (ctypes.c_int, [_P]),
     "olfx_sample_set_param": (ctypes.c_int, [_P, _U32, _F]),
     "olfx_sample_note": (ctypes.c_int, [_P, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
+    "olfx_sample_voice_event": (ctypes.c_int, [_P, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, _F]),
+    "olfx_sample_update": (ctypes.c_int, [_P]),
     "olfx_sample_control": (ctypes.c_int, [_P, ctypes.c_uint8, ctypes.c_int, _F]),
     "olfx_sample_process": (ctypes.c_int, [_P, ctypes.POINTER(_F), ctypes.POINTER(_F)]),
     "olfx_sample_latency": (_U32, [_P]),

@@ -378,7 +378,7 @@ struct olfx_engine {
 
     // voice
     float *vc_state = nullptr, *vc_coef = nullptr;
-    std::vector<olfx_event> events;
+    std::vector<olfx_voice_event> events;
     // voice buses (olfx_mix_config): [n_buses + 1] offsets, then the voice lists
     uint32_t *mix_dev = nullptr;
     hipEvent_t mix_done = nullptr;          // recorded after every olfx_mix launch
@@ -522,19 +522,22 @@ int apply_events(olfx_engine *e, hipStream_t s) {
     std::vector<float> st((size_t)VCS_N * n);
     HIPCHK(e, hipMemcpyAsync(st.data(), e->vc_state, st.size() * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(e, hipStreamSynchronize(s));
-    for (const olfx_event &ev : e->events) {
+    for (const olfx_voice_event &ev : e->events) {
         const uint32_t i = ev.inst;
         uint32_t flags;
         std::memcpy(&flags, &st[(size_t)VCS_FLAGS * n + i], 4);
-        if (ev.type == OLFX_EV_NOTE_ON) {
+        switch (ev.type) {
+        case OLFX_EV_NOTE_ON:
             flags |= 1u << 8;                                   // gate = true
             // Retrigger(true): mode = ATTACK (1), x = 0, for amp (bits 0-2) and filter (3-5)
             flags = (flags & ~0x3Fu) | 1u | (1u << 3);
             st[(size_t)VCS_ENVA_X * n + i] = 0.f;
             st[(size_t)VCS_ENVF_X * n + i] = 0.f;
             st[(size_t)VCS_FREQ * n + i] = powf(2.f, (ev.note - 69.0f) / 12.0f) * 440.0f;  // daisysp::mtof
-        } else {
-            flags &= ~(1u << 8);
+            break;
+        case OLFX_EV_GATE_ON: flags |= 1u << 8; break;         // SynthVoice::GateOn (:231-234)
+        case OLFX_EV_SET_FREQUENCY: st[(size_t)VCS_FREQ * n + i] = ev.value; break;   // :264-267
+        default: flags &= ~(1u << 8); break;                    // NoteOff / GateOff (:236-239)
         }
         std::memcpy(&st[(size_t)VCS_FLAGS * n + i], &flags, 4);
     }
@@ -976,10 +979,33 @@ int olfx_note_events(olfx_engine *e, const olfx_event *ev, uint32_t n) {
     if (!is_voice_kind(e->kind)) return e->fail(OLFX_E_STATE, "olfx_note_events: not a voice engine");
     if (n && !ev) return e->fail(OLFX_E_ARG, "olfx_note_events: null events");
     for (uint32_t k = 0; k < n; ++k) {
-        if (ev[k].inst >= e->n || ev[k].note > 127 || ev[k].type > 1)
+        if (ev[k].inst >= e->n || ev[k].note > 127 || ev[k].type > OLFX_EV_GATE_OFF)
             return e->fail(OLFX_E_ARG, "olfx_note_events: bad event %u", k);
     }
+    for (uint32_t k = 0; k < n; ++k)
+        e->events.push_back(olfx_voice_event{ev[k].inst, ev[k].type, ev[k].note, ev[k].velocity, 0, 0.f});
+    return OLFX_OK;
+}
+
+int olfx_voice_events(olfx_engine *e, const olfx_voice_event *ev, uint32_t n) {
+    if (!e) return OLFX_E_ARG;
+    if (!is_voice_kind(e->kind)) return e->fail(OLFX_E_STATE, "olfx_voice_events: not a voice engine");
+    if (n && !ev) return e->fail(OLFX_E_ARG, "olfx_voice_events: null events");
+    for (uint32_t k = 0; k < n; ++k) {
+        if (ev[k].inst >= e->n || ev[k].note > 127 || ev[k].type > OLFX_EV_SET_FREQUENCY ||
+            (ev[k].type == OLFX_EV_SET_FREQUENCY && !std::isfinite(ev[k].value)))
+            return e->fail(OLFX_E_ARG, "olfx_voice_events: bad event %u", k);
+    }
     e->events.insert(e->events.end(), ev, ev + n);
+    return OLFX_OK;
+}
+
+int olfx_update(olfx_engine *e, uint32_t first, uint32_t count) {
+    if (!e) return OLFX_E_ARG;
+    if ((uint64_t)first + count > e->n) return e->fail(OLFX_E_ARG, "olfx_update: range out of bounds");
+    if (is_voice_kind(e->kind))
+        for (uint32_t k = 0; k < count; ++k) e->configured[first + k] = 1;
+    e->dirty = true;
     return OLFX_OK;
 }
 

@@ -159,6 +159,27 @@ class Engine:
             arr[k].velocity = int(e[3]) if len(e) > 3 else 100
         check(self.lib.olfx_note_events(self._h, arr, len(evs)), self._h)
 
+    def voice_events(self, events: Iterable[Sequence]) -> None:
+        """Voice events in order: iterable of (inst, type[, note[, value]]) with type one of
+        _lib.EV_* (NoteOn/NoteOff/GateOn/GateOff/SetFrequency, Voice.h:33-57); value = Hz for
+        SetFrequency."""
+        evs = list(events)
+        if not evs:
+            return
+        arr = (_lib.VoiceEvent * len(evs))()
+        for k, e in enumerate(evs):
+            arr[k].inst = int(e[0])
+            arr[k].type = int(e[1])
+            arr[k].note = int(e[2]) if len(e) > 2 else 0
+            arr[k].velocity = 100
+            arr[k].value = float(e[3]) if len(e) > 3 else 0.0
+        check(self.lib.olfx_voice_events(self._h, arr, len(evs)), self._h)
+
+    def update(self, first: int = 0, count: int = -1) -> None:
+        """Update() of instances first..first+count with their current parameters."""
+        count = self.n - first if count < 0 else count
+        check(self.lib.olfx_update(self._h, int(first), int(count)), self._h)
+
     def control(self, events: Iterable[Sequence]) -> None:
         """Control changes, applied in order: iterable of (inst, cc, value[, source]); source
         "midi" (value 0..127, the default) or "hw" (UpdateHardwareControl value)."""

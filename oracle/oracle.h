@@ -68,6 +68,8 @@ oracle_voice *oracle_voice_create_model(int n_inst, float sample_rate, int model
 void oracle_voice_destroy(oracle_voice *o);
 int oracle_voice_config(oracle_voice *o, int inst, const float *values);
 int oracle_voice_note(oracle_voice *o, int inst, int on, int note);
+/* 0 NoteOff, 1 NoteOn, 2 GateOn, 3 GateOff, 4 SetFrequency(value Hz) (Voice.h:33-57) */
+int oracle_voice_event(oracle_voice *o, int inst, int type, int note, float value);
 int oracle_voice_process(oracle_voice *o, float *out, int n_frames, int n_threads);
 
 /* ---- fxlib effect rack ol::fx::FxRack<2> (spec oracle for the DaisySP parts, parity unpinned) ---- */

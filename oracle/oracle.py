@@ -72,6 +72,7 @@ def lib(o0: bool = False) -> ctypes.CDLL:
         L.oracle_voice_destroy.argtypes = [ctypes.c_void_p]
         L.oracle_voice_config.argtypes = [ctypes.c_void_p, ctypes.c_int, _PF]
         L.oracle_voice_note.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oracle_voice_event.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _F]
         L.oracle_voice_process.argtypes = [ctypes.c_void_p, _PF, ctypes.c_int, ctypes.c_int]
         L.oracle_fxrack_defaults.argtypes = [_PF]
         L.oracle_fxrack_create.restype = ctypes.c_void_p
@@ -219,6 +220,10 @@ class Voice(_Bank):
 
     def note(self, inst: int, on: bool, note: int = 60) -> None:
         assert self.L.oracle_voice_note(self.h, inst, int(bool(on)), int(note)) == 0
+
+    def event(self, inst: int, type_: int, note: int = 0, value: float = 0.0) -> None:
+        """Voice.h:33-57: 0 NoteOff, 1 NoteOn, 2 GateOn, 3 GateOff, 4 SetFrequency(value)."""
+        assert self.L.oracle_voice_event(self.h, inst, int(type_), int(note), float(value)) == 0
 
     def process(self, frames: int, threads: int = 1) -> np.ndarray:
         out = np.empty((1, frames, self.n), dtype=np.float32)

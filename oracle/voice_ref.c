@@ -311,6 +311,21 @@ int oracle_voice_note(oracle_voice *o, int inst, int on, int note)
     return 0;
 }
 
+/* Voice.h:33-57 gate / pitch calls (types as include/olfx.h OLFX_EV_*): 0 NoteOff, 1 NoteOn,
+   2 GateOn (SynthVoice.h:231-234), 3 GateOff (:236-239), 4 SetFrequency(value) (:264-267) */
+int oracle_voice_event(oracle_voice *o, int inst, int type, int note, float value)
+{
+    if (!o || inst < 0 || inst >= o->n) return -1;
+    voice_t *v = &o->v[inst];
+    switch (type) {
+    case 0: case 1: return oracle_voice_note(o, inst, type, note);
+    case 2: v->gate = 1; return 0;
+    case 3: v->gate = 0; return 0;
+    case 4: v->freq = value; return 0;
+    default: return -1;
+    }
+}
+
 /* out [n_frames][n] */
 int oracle_voice_process(oracle_voice *o, float *out, int n_frames, int n_threads)
 {

@@ -10,6 +10,7 @@
  * gtest is not in the image, so a small TEST/EXPECT harness stands in. The binary exits non-zero
  * on any failure. It needs a GPU; run it through tests/test_cpp_operators.py (-m gpu).
  */
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -20,58 +21,8 @@
 
 #include "olfx_adapter.hpp"
 #include "olfx_fx.hpp"
-#include "../../oracle/oracle.h"
+#include "harness.h"
 
-namespace {
-struct Case { const char *suite, *name; std::function<void()> fn; };
-std::vector<Case> &cases() { static std::vector<Case> c; return c; }
-int g_failures = 0;
-struct Reg { Reg(const char *s, const char *n, std::function<void()> f) { cases().push_back({s, n, std::move(f)}); } };
-#define TEST(S, N) static void S##_##N(); static Reg reg_##S##_##N(#S, #N, S##_##N); static void S##_##N()
-#define EXPECT_TRUE(c) do { if (!(c)) { ++g_failures; std::printf("  FAILED %s:%d: %s\n", __FILE__, __LINE__, #c); } } while (0)
-#define EXPECT_EQ(a, b) EXPECT_TRUE((a) == (b))
-
-/* xorshift32 white noise in [-1,1): the SURVEY section 8c KAT generator, one seed per instance */
-std::vector<float> noise(uint32_t ch, uint32_t frames, uint32_t n, uint32_t seed) {
-    std::vector<float> x((size_t)ch * frames * n);
-    for (uint32_t c = 0; c < ch; ++c)
-        for (uint32_t i = 0; i < n; ++i)
-            oracle_xorshift_noise(seed + 7919u * i + 104729u * c, x.data() + (size_t)c * frames * n + i,
-                                  frames, n);
-    return x;
-}
-
-struct Lcg {   /* deterministic parameter draws */
-    uint64_t s;
-    explicit Lcg(uint64_t seed) : s(seed) {}
-    float uni(float lo, float hi) {
-        s = s * 6364136223846793005ull + 1442695040888963407ull;
-        return lo + (hi - lo) * (float)((s >> 40) * (1.0 / 16777216.0));
-    }
-};
-
-size_t first_bit_mismatch(const std::vector<float> &a, const std::vector<float> &b) {
-    for (size_t k = 0; k < a.size(); ++k)
-        if (std::memcmp(&a[k], &b[k], 4) != 0) return k;
-    return (size_t)-1;
-}
-
-/* Process `frames` frames through `op` in blocks of `block` frames; layout [ch][frames][n]. */
-template <class F>
-std::vector<float> run_blocks(F &&proc, const std::vector<float> &x, uint32_t ich, uint32_t och,
-                              uint32_t frames, uint32_t n, uint32_t block) {
-    std::vector<float> y((size_t)och * frames * n), xin((size_t)ich * block * n), yb((size_t)och * block * n);
-    for (uint32_t f0 = 0; f0 < frames; f0 += block) {
-        uint32_t b = std::min(block, frames - f0);
-        for (uint32_t c = 0; c < ich; ++c)
-            std::memcpy(&xin[(size_t)c * b * n], &x[((size_t)c * frames + f0) * n], (size_t)b * n * 4);
-        proc(xin.data(), yb.data(), b);
-        for (uint32_t c = 0; c < och; ++c)
-            std::memcpy(&y[((size_t)c * frames + f0) * n], &yb[(size_t)c * b * n], (size_t)b * n * 4);
-    }
-    return y;
-}
-}  // namespace
 
 /* ol::fx::Reverb surface over N plates vs the bit-exact Dattorro oracle. */
 TEST(Reverb, BankMatchesOracleBitExact) {
@@ -472,13 +423,24 @@ TEST(PerSample, PolyvoiceEqualsBankBuses) {
     EXPECT_TRUE(bo[(size_t)100 * 2] != 0.f && bo[(size_t)100 * 2 + 1] != 0.f);
 }
 
-int main() {
-    for (auto &c : cases()) {
-        int before = g_failures;
-        std::printf("[ RUN      ] %s.%s\n", c.suite, c.name);
-        try { c.fn(); } catch (const std::exception &e) { ++g_failures; std::printf("  exception: %s\n", e.what()); }
-        std::printf("[ %s ] %s.%s\n", g_failures == before ? "      OK" : " FAILED ", c.suite, c.name);
-    }
-    std::printf("%zu tests, %d failures\n", cases().size(), g_failures);
-    return g_failures ? 1 : 0;
+/* Per-sample call rate of the pool (include/olfx_sample.h): N ChorusEffect objects called frame-major
+   from one host thread, as a reference per-frame callback calls its operators.  The per-frame call
+   takes no lock; the instance completing a block runs the generation on the GPU (host I/O). */
+TEST(PerSample, CallsPerSecond) {
+    const uint32_t n = 4096, blocks = 8;
+    std::vector<olfx::ChorusEffect> fx(n);
+    for (auto &f : fx) f.init(48000.f);
+    const uint32_t B = fx[0].latency();
+    float acc = 0.f;
+    for (uint32_t i = 0; i < n; ++i) acc += fx[i].process(0.f);           /* first run: engine creation */
+    const auto t0 = std::chrono::steady_clock::now();
+    uint64_t calls = 0;
+    for (uint32_t t = 1; t < blocks * B; ++t)
+        for (uint32_t i = 0; i < n; ++i, ++calls) acc += fx[i].process(((t * 31 + i) & 255) * (1.f / 512.f) - 0.25f);
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("  per-sample calls/s: %.4g (%u instances x %u frames, %.3f s, %u-frame blocks)\n",
+                calls / s, n, blocks * B - 1, s, B);
+    EXPECT_TRUE(std::isfinite(acc));
 }
+
+int main() { return run_all_tests(); }

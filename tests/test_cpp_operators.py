@@ -47,4 +47,41 @@ def test_cpp_operators_on_gpu():
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=600)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "14 tests, 0 failures" in r.stdout
+    assert "15 tests, 0 failures" in r.stdout
+
+
+REF_BIN = os.path.join(CPP, "test_ref_surface")
+REF_HDR = "/root/reference/modules/synthlib/Polyvoice.h"
+
+
+def _build_ref():
+    """tests/cpp/Makefile `test_ref_surface`: include/olfx_ref.hpp under the reference's own,
+    unmodified Polyvoice.h / VoiceMap.h / Voice.h / corelib (built here only; prebuilt on the box)."""
+    if os.path.exists(REF_HDR):
+        r = subprocess.run(["make", "-s", "-C", CPP, "test_ref_surface"], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+    if not os.path.exists(REF_BIN):
+        pytest.skip("test_ref_surface not built (needs /root/reference at build time)")
+    return REF_BIN
+
+
+def test_ref_surface_compiles_against_reference_headers_and_fails_loudly_without_gpu():
+    """The reference's Polyvoice / VoiceMap compile unmodified over ol::synth::SynthVoice and
+    ol::fx::FxRack<2>; off-GPU the first Process throws OLFX_E_NODEVICE (no CPU path)."""
+    _build_ref()
+    if os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK | os.W_OK):
+        pytest.skip("GPU visible: covered by the -m gpu run")
+    r = subprocess.run([REF_BIN], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1
+    assert "no HIP device" in r.stdout and "(code -4)" in r.stdout
+
+
+@pytest.mark.gpu
+def test_ref_surface_on_gpu():
+    """Reference-typed classes on the GPU: Polyvoice / VoiceMap sums, Voice gate / pitch calls,
+    FxRack<2>(DelayFx&, ReverbFx&, FilterFx&) controls, ChorusFx<1|2>, vs the oracle one block late."""
+    _build_ref()
+    r = subprocess.run([REF_BIN], capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "5 tests, 0 failures" in r.stdout

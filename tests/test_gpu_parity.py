@@ -405,6 +405,57 @@ def test_voice_unconfigured_defaults(cuda, kind):
     assert rel_err(y[0].T, yr[0].T) <= VOICE_TOL
 
 
+@pytest.mark.parametrize("kind", ["voice", "voice_moog"])
+def test_voice_gate_frequency_update_events(cuda, kind):
+    """Voice.h:33-57 calls beyond NoteOn/NoteOff through olfx_voice_events / olfx_update:
+    GateOff then GateOn without retrigger (SynthVoice.h:231-239), SetFrequency (:264-267) under
+    portamento, and Update() alone (member defaults, SynthVoice.h:285-311) on voices never
+    configured; each lands at the next block, in order, against the oracle."""
+    from ol_dsp_amd import _lib
+    n = 64
+    rng = np.random.default_rng(33)
+    cfg = voice_configs(rng, n)
+    cfg[15, :] = rng.uniform(0.0, 0.01, n).astype(np.float32)     # portamento: SetFrequency glides
+    notes = [int(v) for v in rng.integers(36, 97, n)]
+    e, ref = _voice_pair(n, cfg, notes, kind=kind)
+    half = n // 2
+    # a second bank never configured: Update() only (the engine's default params == the members')
+    e2, ref2 = _voice_pair(n, None, notes, kind=kind)
+    e2.update(0, n)
+    defaults = np.asarray([[0.0, 0.0, 0.0, 1.0, 0.0, 1.0, 0.2, 0.0, 0.0, 0.8, 0.01, 1.0, 0.0, 1.0, 0.01, 0.0]],
+                          np.float32).T.repeat(n, 1)
+    for i in range(n):
+        ref2.config(i, defaults[:, i])
+    ys, yrs, y2, yr2 = [], [], [], []
+    for blk in range(8):
+        if blk == 2:
+            e.voice_events([(i, _lib.EV_SET_FREQUENCY, 0, 110.0 * (1 + i % 7)) for i in range(half)])
+            for i in range(half):
+                ref.event(i, 4, 0, 110.0 * (1 + i % 7))
+        if blk == 3:
+            e.voice_events([(i, _lib.EV_GATE_OFF) for i in range(n)])
+            for i in range(n):
+                ref.event(i, 3)
+        if blk == 5:
+            e.voice_events([(i, _lib.EV_GATE_ON) for i in range(0, n, 2)] +
+                           [(i, _lib.EV_NOTE_ON, 60) for i in range(1, n, 2)])
+            for i in range(n):
+                ref.event(i, 2 if i % 2 == 0 else 1, 60)
+            e2.voice_events([(i, _lib.EV_GATE_OFF) for i in range(n)])
+            for i in range(n):
+                ref2.event(i, 3)
+        ys.append(_voice_run(e, 256, cuda))
+        yrs.append(ref.process(256))
+        y2.append(_voice_run(e2, 256, cuda))
+        yr2.append(ref2.process(256))
+    y, yr = np.concatenate(ys, 1), np.concatenate(yrs, 1)
+    assert np.all(np.isfinite(y))
+    assert rel_err(y[0].T, yr[0].T) <= VOICE_TOL
+    y2, yr2 = np.concatenate(y2, 1), np.concatenate(yr2, 1)
+    assert np.any(yr2 != 0)
+    assert rel_err(y2[0].T, yr2[0].T) <= VOICE_TOL
+
+
 def test_voice_moog_golden_and_state_carry(cuda, golden):
     """MoogFilter voices against the frozen fixture, in ragged blocks (the LadderFilter state and
     oldinput_ carry across launches), plus the synth_test.cpp:102-148 first-sample pin."""
