@@ -1,29 +1,56 @@
 // ol_dsp_amd/csrc/chain.hip -- chorus -> pitch-shift -> dattorro in one launch (BASELINE
-// configs[4]: 16,384 chains per GPU).
+// configs[4]: 16,384 chains per GPU; north_star: >= 64k chorus+reverb instances).
 //
-// A workgroup owns 64 instances and runs the three stages as a pipeline of waves:
-//   waves 0, 1 ("CP"): 32 instances x 2 channels each; every lane runs the chorus stage and then
-//                      the pitch-shift stage on the chorus output, chunk by chunk (16 frames);
-//   wave 2     ("DT"): the 64 reverbs, lane = instance, fed through LDS.
-// Step s: the CP waves produce chunk s into queue buffer s & 1 while the DT wave consumes chunk
-// s-1 from the other buffer; one workgroup barrier per step.  Every stage still processes each
-// instance's frames in order, so the output is the plain composition of the three stages
-// (bit-exact with the oracle's chorus -> pitch-shift -> dattorro, tests/test_gpu_parity.py).
-// The intermediates never touch HBM, and the three stages run concurrently on different SIMDs,
-// where three separate launches each filled only part of the chip at 16,384 instances.
-#include "chorus_stage.h"
+// A workgroup owns 64 instances and runs the three stages as a pipeline of four single-role waves,
+// one per SIMD:
+//   waves 0, 1 ("C"):  the chorus stage, 32 instances x 2 channels each, input from HBM;
+//   wave 2     ("P"):  the pitch-shift stage for all 64 instances, as two 32-instance groups;
+//   wave 3     ("DT"): the 64 reverbs, lane = instance, output to HBM.
+// Stage outputs go through LDS queues (double-buffered, [ch][16 frames][64 instances]).  Barrier
+// b ends step b: the C waves produce chunk b, P runs chunk b-1, DT runs chunk b-2; nchunks + 2
+// steps.  Every stage still processes each instance's frames in order, so the output is the plain
+// composition of the three stages (bit-exact with the oracle's chorus -> pitch-shift -> dattorro,
+// tests/test_gpu_parity.py), and the intermediates never touch HBM.
+//
+// The chorus and pitch stages are the line-carry stage of chorus_block_v11 (chorus_stage_l.h):
+// per tap and instance the two aligned 128-B lines of the window live in registers and a chunk
+// loads only the new line, so every ring byte is read about once (v1 re-fetched a fresh window
+// per tap per chunk: 296 B/frame of HBM traffic against 228.6 algorithmic; v3: 245).  The pitch
+// stage's next input (the chorus output of the next chunk) does not exist while it runs a chunk,
+// so it uses the XPREV form (stores its own input, patches the previous one from registers).
+// Why four roles (history in DESIGN.md section 4): every wave of the kernel gets the reverb's
+// register allocation (256 VGPR + AGPRs), so a CU holds four waves; v2 ran chorus and pitch
+// in the same two waves (12.6 us per step against the reverb's 8.1) and left one SIMD idle.
+#include "chorus_stage_l.h"
 #include "dattorro_stage.h"
 
 namespace olfx {
 
 namespace {
-constexpr int kChainThreads = 192;            // 3 waves
+constexpr int kChainThreads = 256;            // 4 waves
 constexpr int kQCh = 16 * 64 + 32;            // floats per channel of one queue buffer (padded)
 constexpr int kQBuf = 2 * kQCh;               // one buffer: [ch][16 frames][64 instances]
-constexpr int kChainLds = 4 * ch::ChStage<true>::kRegion + 2 * kQBuf;   // 2 CP waves x 2 regions
+constexpr int kDepth = 3;                     // buffers per queue: a role may run 2 chunks ahead
+constexpr int kChainRegion = ch::ChStageL<true>::kRegion;
+constexpr int kFlags = 8;                     // LDS progress counters
+constexpr int kChainLds = 4 * kChainRegion + 2 * kDepth * kQBuf + kFlags;
+enum { F_C0 = 0, F_C1, F_PIN, F_POUT, F_DIN };   // chunks published by C0 / C1, taken by P, published by P, taken by DT
+
+__device__ __forceinline__ uint32_t flag_get(const uint32_t *f) {
+    return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void flag_put(uint32_t *f, uint32_t v) {
+    __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// spin (with s_sleep) until cond(); the counters only grow, and every role's wait targets a
+// counter another role advances without waiting on this one first, so the pipeline cannot lock
+template <class Cond>
+__device__ __forceinline__ void wait_for(Cond &&cond) {
+    while (!cond()) __builtin_amdgcn_s_sleep(1);
+}
 }  // namespace
 
-__global__ __launch_bounds__(kChainThreads, 1) void chain_block_v1(ChainArgs a) {
+__global__ __launch_bounds__(kChainThreads, 1) void chain_block_v4(ChainArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int kChunk = 16;
     const uint32_t tid = threadIdx.x;
@@ -32,59 +59,92 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v1(ChainArgs a) 
     const uint32_t base = blockIdx.x * 64u;               // first instance of the workgroup
     const uint32_t n = a.n, nf = a.n_frames;
     const uint32_t nchunks = (nf + kChunk - 1) / kChunk;
-    float *queue = lds + 4 * ch::ChStage<true>::kRegion;   // [2 bufs][2 ch][16][64]
+    float *q1 = lds + 4 * kChainRegion;                    // chorus -> pitch   [kDepth][2 ch][16][64]
+    float *q2 = q1 + kDepth * kQBuf;                       // pitch -> reverb
+    uint32_t *flags = (uint32_t *)(q2 + kDepth * kQBuf);
+    if (tid < kFlags) flags[tid] = 0;
+    __syncthreads();                                       // the only barrier
 
     if (wib < 2) {
-        // ---------------- CP: chorus then pitch-shift, per (instance, channel) lane ----------------
-        ch::ChStage<true> s1;
-        ch::ChStage<false> s2;
-        s1.init(a.c1, lds + (2 * wib) * ch::ChStage<true>::kRegion, lane, base + 32u * wib);
-        s2.init(a.c2, lds + (2 * wib + 1) * ch::ChStage<true>::kRegion, lane, base + 32u * wib);
+        // ---------------- C: the chorus, per (instance, channel) lane ----------------
+        ch::ChStageL<true> s1;
+        s1.init(a.c1, lds + wib * kChainRegion, lane, base + 32u * wib);
         const ch::Rsrc rIn = ch::rsrc(a.in, (a.plane + (uint64_t)nf * n) * 4);
         const uint32_t io_v = s1.ch * (uint32_t)a.plane * 4u + s1.i * 4u, frame_b = n * 4u;
-        const uint32_t qcol = s1.ch * kQCh + 32u * wib + s1.j;   // this lane's queue column
+        const uint32_t qcol = s1.ch * kQCh + 32u * wib + s1.j;
 
-        float x[kChunk], xn[kChunk], y1[kChunk];
+        float x[kChunk], xn[kChunk];
         int C = (int)min((uint32_t)kChunk, nf);
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) x[k] = k < C ? ch::ld1(rIn, io_v, (uint32_t)k * frame_b) : 0.f;
         s1.begin(x, C);
-        // chunk c: stage 1 on x, stage 2 on stage 1's output, published into queue buffer c & 1.
-        // Chunk 0 is peeled: stage 2's begin() needs stage 1's first output (a begin() inside the
-        // loop kept stage 2's state in scratch memory).
-        auto step = [&](uint32_t c, auto first_tag) {
-            constexpr bool FIRST = decltype(first_tag)::value;
-            const uint32_t f0 = c * kChunk;
+        auto step = [&](auto par, uint32_t f0, uint32_t c) {
             C = (int)min((uint32_t)kChunk, nf - f0);
             const int Cn = f0 + kChunk < nf ? (int)min((uint32_t)kChunk, nf - f0 - kChunk) : 0;
+            auto prefetch = [&]() {                           // next chunk's input, clamped, unconditional
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) {   // next chunk's input in flight (clamped, unconditional)
-                const float v = ch::ld1(rIn, io_v, min(f0 + kChunk + (uint32_t)k, nf - 1u) * frame_b);
-                xn[k] = k < Cn ? v : 0.f;
-            }
+                for (int k = 0; k < kChunk; ++k) {
+                    const float v = ch::ld1(rIn, io_v, min(f0 + kChunk + (uint32_t)k, nf - 1u) * frame_b);
+                    xn[k] = k < Cn ? v : 0.f;
+                }
+            };
+            // outputs to registers first, then to the queue: a store through a generic pointer
+            // inside the stage's sink may alias the stage object, which then stays in scratch
+            float y[kChunk];
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) y1[k] = 0.f;
-            s1.chunk(x, C, Cn, [&](int k, float v) { y1[k] = v; });
-            if (FIRST) s2.begin(y1, C);
-            float *q = queue + (c & 1u) * kQBuf + qcol;
-            // stage 2's output goes to registers first and then to the queue: a store through a
-            // generic pointer inside the stage's sink may alias the stage object, which then
-            // stays in scratch memory
-            float y2[kChunk];
+            for (int k = 0; k < kChunk; ++k) y[k] = 0.f;
+            s1.template chunk<decltype(par)::value>(x, xn, C, Cn, [&](int k, float v) { y[k] = v; }, prefetch);
+            wait_for([&] { return flag_get(flags + F_PIN) + kDepth > c; });   // buffer c % kDepth free
+            float *q = q1 + (c % kDepth) * kQBuf + qcol;
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) y2[k] = 0.f;
-            s2.chunk(y1, C, Cn, [&](int k, float v) { y2[k] = v; });
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) q[k * 64] = y2[k];
-            __syncthreads();                                  // chunk c published to the DT wave
+            for (int k = 0; k < kChunk; ++k) q[k * 64] = y[k];
+            flag_put(flags + F_C0 + wib, c + 1);
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) x[k] = xn[k];
         };
-        step(0, std::true_type{});
-        for (uint32_t c = 1; c < nchunks; ++c) step(c, std::false_type{});
-        __syncthreads();                                      // the DT wave's last step
+        for (uint32_t f0 = 0, c = 0; f0 < nf; f0 += 2 * kChunk, c += 2) {
+            step(std::integral_constant<int, 0>{}, f0, c);
+            if (f0 + kChunk < nf) step(std::integral_constant<int, 1>{}, f0 + kChunk, c + 1);
+        }
         s1.finish(a.c1);
-        s2.finish(a.c2);
+    } else if (wib == 2) {
+        // ---------------- P: the pitch-shifter, two 32-instance groups per lane ----------------
+        ch::ChStageL<false, true> sa, sb;
+        sa.init(a.c2, lds + 2 * kChainRegion, lane, base);
+        sb.init(a.c2, lds + 3 * kChainRegion, lane, base + 32u);
+        const uint32_t qa = sa.ch * kQCh + sa.j, qb = qa + 32u;
+        float xa[kChunk], xb[kChunk];
+        int C = (int)min((uint32_t)kChunk, nf);
+        sa.begin(xa, C);                                      // XPREV: lines only, x unused
+        sb.begin(xb, C);
+        auto step = [&](auto par, uint32_t f0, uint32_t c) {
+            constexpr int P = decltype(par)::value;
+            C = (int)min((uint32_t)kChunk, nf - f0);
+            const int Cn = f0 + kChunk < nf ? (int)min((uint32_t)kChunk, nf - f0 - kChunk) : 0;
+            wait_for([&] { return flag_get(flags + F_C0) > c && flag_get(flags + F_C1) > c; });
+            const float *qi = q1 + (c % kDepth) * kQBuf;
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) { xa[k] = qi[qa + k * 64]; xb[k] = qi[qb + k * 64]; }
+            flag_put(flags + F_PIN, c + 1);                   // (the release waits for these reads)
+            float y[kChunk];
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) y[k] = 0.f;
+            sa.template chunk<P>(xa, xa, C, Cn, [&](int k, float v) { y[k] = v; }, []() {});
+            wait_for([&] { return flag_get(flags + F_DIN) + kDepth > c; });
+            float *qo = q2 + (c % kDepth) * kQBuf;
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) { qo[qa + k * 64] = y[k]; y[k] = 0.f; }
+            sb.template chunk<P>(xb, xb, C, Cn, [&](int k, float v) { y[k] = v; }, []() {});
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) qo[qb + k * 64] = y[k];
+            flag_put(flags + F_POUT, c + 1);
+        };
+        for (uint32_t f0 = 0, c = 0; f0 < nf; f0 += 2 * kChunk, c += 2) {
+            step(std::integral_constant<int, 0>{}, f0, c);
+            if (f0 + kChunk < nf) step(std::integral_constant<int, 1>{}, f0 + kChunk, c + 1);
+        }
+        sa.finish(a.c2);
+        sb.finish(a.c2);
     } else {
         // ---------------- DT: the reverb, lane = instance, input from the queue ----------------
         const uint32_t i = base + lane;                       // < d.n (padded to 64)
@@ -92,15 +152,19 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v1(ChainArgs a) 
         const uint32_t t0 = a.d.t0;
         dt_prime(t0);
         const bool valid = i < n;
-        __syncthreads();                                      // chunk 0 published
         for (uint32_t c = 0; c < nchunks; ++c) {
             const uint32_t f0 = c * kChunk;
             const uint32_t C = min((uint32_t)kChunk, nf - f0);
-            const float *q = queue + (c & 1u) * kQBuf + lane;
+            wait_for([&] { return flag_get(flags + F_POUT) > c; });
+            const float *q = q2 + (c % kDepth) * kQBuf + lane;
+            float xm[kChunk];                                 // the chunk's mono input, (l + r) / 2
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) xm[k] = (q[k * 64] + q[kQCh + k * 64]) / 2;
+            flag_put(flags + F_DIN, c + 1);
             for (uint32_t s = 0; s < C; s += 4) {
                 float xin[4], o_l[4], o_r[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) xin[k] = (q[(s + k) * 64] + q[kQCh + (s + k) * 64]) / 2;
+                for (int k = 0; k < 4; ++k) xin[k] = xm[s + k];
                 dt_step(t0 + f0 + s, f0 + s + 4 < nf, xin, o_l, o_r);
                 if (valid) {
 #pragma unroll
@@ -110,7 +174,6 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v1(ChainArgs a) 
                     }
                 }
             }
-            __syncthreads();                                  // chunk c consumed; c + 1 published
         }
         dt_finish();
     }
@@ -122,7 +185,7 @@ hipError_t launch_chain(const ChainArgs &a, hipStream_t s) {
     if ((uint64_t)a.n * 2 * a.c1.csize * 4 >= (1ull << 32) || (a.plane + (uint64_t)a.n_frames * a.n) * 4 >= (1ull << 32))
         return hipErrorInvalidValue;
     const uint32_t blocks = (a.n + 63u) / 64u;
-    hipLaunchKernelGGL(chain_block_v1, dim3(blocks), dim3(kChainThreads), (size_t)kChainLds * sizeof(float), s, a);
+    hipLaunchKernelGGL(chain_block_v4, dim3(blocks), dim3(kChainThreads), (size_t)kChainLds * sizeof(float), s, a);
     return hipGetLastError();
 }
 

@@ -24,6 +24,11 @@
 // that did not advance by exactly one line (or the first chunk of a launch) is FRESH: it also
 // reloads L' (the "lo" load, exec-masked, so a carried line is never clobbered).
 //
+// XPREV variant (the fused chain's second stage, whose next input is not known while a chunk runs):
+// each chunk stores its OWN input x_c before the next chunk's line loads, and keeps it in registers
+// (xp) for one more chunk.  A line loaded during chunk c then holds everything up to x_c; at chunk
+// c+1 a carried line lacks x_c (patched from xp) and x_{c+1} (patched from x, as always).
+//
 // The chorus tap can span 18 positions (its delay may fall by one inside a chunk); when such a
 // window starts at the last position of a line, its highest position lies in line L'+2: that one
 // position per lane ("straggler") is loaded directly (4 B, own channel, exec-masked) and staged.
@@ -77,7 +82,7 @@ __device__ __forceinline__ PlanL plan_chunk_l(uint32_t lfo_acc, uint32_t lfo_inc
     return p;
 }
 
-template <bool FULL>
+template <bool FULL, bool XPREV = false>
 struct ChStageL {
     static constexpr int kChunk = 16, kWin = 24, kSlots = kWin + 1;
     static constexpr int kRegion = 3 * kSlots * kRow;   // floats of LDS per wave (4,800), as v10
@@ -104,6 +109,7 @@ struct ChStageL {
     PlanL pl;
     uint32_t wpos;
     bool started;
+    float xp[XPREV ? kChunk : 1];   // XPREV: the previous chunk's input
 
     __device__ __forceinline__ void init(const ChorusArgs &a, float *lds_region, uint32_t lane_, uint32_t inst0_) {
         lane = lane_; j = lane >> 1; ch = lane & 1u; inst0 = inst0_; n = a.n;
@@ -253,10 +259,13 @@ struct ChStageL {
         }
     }
 
-    // first chunk of the launch: store its inputs, then load both lines of every window (fresh)
+    // first chunk of the launch: store its inputs, then load both lines of every window (fresh).
+    // XPREV: no store (chunk 0 stores its own input), x is unused
     __device__ __forceinline__ void begin(const float (&x)[kChunk], int C) {
-        stage_run(x, 0);
-        coop_store(true, 0, wpos, C);
+        if (!XPREV) {
+            stage_run(x, 0);
+            coop_store(true, 0, wpos, C);
+        }
         pl = plan_chunk_l<kWin>(lfo_acc, lfo_inc, lfo_off, ps_acc, ps_inc, C, D, W, pmax, cmax, FULL);
         load_lines<0>(pl, wpos, true);
     }
@@ -265,13 +274,17 @@ struct ChStageL {
     // psv_c and x_{c+1} into the rings (the pitch windows are dead: their LDS is staging), then
     // chunk c+1's plan and line loads
     template <int PAR>
-    __device__ __forceinline__ void stores_and_next(const float (&psv)[kChunk], const float (&xn)[kChunk], uint32_t w0,
-                                                    int C, int Cn, uint32_t lfo0, uint32_t ps0) {
+    __device__ __forceinline__ void stores_and_next(const float (&psv)[kChunk], const float (&x)[kChunk],
+                                                    const float (&xn)[kChunk], uint32_t w0, int C, int Cn,
+                                                    uint32_t lfo0, uint32_t ps0) {
         if (FULL) {
             stage_run(psv, kPsvBase);
             coop_store(false, kPsvBase, w0, C);
         }
-        if (Cn > 0) {
+        if (XPREV) {                                    // this chunk's own input
+            stage_run(x, 0);
+            coop_store(true, 0, w0, C);
+        } else if (Cn > 0) {
             stage_run(xn, 0);
             coop_store(true, 0, w0 + (uint32_t)C, Cn);
         }
@@ -323,6 +336,23 @@ struct ChStageL {
         }
         stage_tap<PAR, 0>();
         stage_tap<PAR, 1>();
+        // XPREV: x_{c-1} is not in a carried line (stored during chunk c-1, after its loads)
+        if (XPREV && started) {
+            if (cur.sA > -kWin - kChunk) {
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) {
+                    const int jw = k - kChunk - cur.sA;
+                    if (jw >= 0 && jw < kWin) wP0[jw * kRow] = xp[k];
+                }
+            }
+            if (cur.sB > -kWin - kChunk) {
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) {
+                    const int jw = k - kChunk - cur.sB;
+                    if (jw >= 0 && jw < kWin) wP1[jw * kRow] = xp[k];
+                }
+            }
+        }
         // x_c is not in a carried line either
         if (cur.sA > -kWin) {
 #pragma unroll
@@ -436,7 +466,7 @@ struct ChStageL {
         }
         // one call site: line registers loaded on two paths meet in a phi, and the copies it needs
         // pushed the kernel from 211 VGPRs to 256 + spills
-        stores_and_next<PAR>(psv, xn, w0, C, Cn, lfo0, ps0);
+        stores_and_next<PAR>(psv, x, xn, w0, C, Cn, lfo0, ps0);
         if (fast) {
             // C. the chorus tap + lores~ (reads independent of each other; only the biquad is serial),
             //    the cover for chunk c+1's line loads
@@ -466,6 +496,10 @@ struct ChStageL {
             }
         }
         wpos = w0 + (uint32_t)C;
+        if (XPREV) {
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) xp[k] = x[k];
+        }
     }
 
     __device__ __forceinline__ void finish(const ChorusArgs &a) const {
