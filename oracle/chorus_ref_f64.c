@@ -1,0 +1,163 @@
+/*
+ * oracle/chorus_ref_f64.c -- the RNBO stereo chorus / gen~ pitch-shifter restated in DOUBLE
+ * precision, as gen~ and RNBO compute (TEST INFRASTRUCTURE ONLY: tests/ and nothing else).
+ *
+ * Purpose: the build's spec (oracle/chorus_ref.c) declares fp32 arithmetic
+ * and fixed-point phasors where gen~/RNBO use double.  This restatement removes exactly those two
+ * choices and keeps every other one, so tests/test_oracle.py can MEASURE the fp32 spec's
+ * deviation from double-precision arithmetic on the same inputs instead of asserting it.
+ * Parity stays UNPINNED: RNBO/genlib are absent, and the other spec choices (cycle~ as an exact
+ * cosine instead of RNBODefaultSinus, lores~ as an RBJ biquad) are shared by both restatements.
+ *
+ * Graph (same citations as chorus_ref.c): mono-chorus.rnbopat
+ *   y = (1-mix) x + mix * lores~( delay~( pitchshift(x, pitch), D cycle~(rate_hz, phase) + D ) )
+ * pitchshift gencode (mono-chorus.rnbopat:962, pitchshift.gendsp:19-305), in double:
+ *   ph = phasor(shift): output, then ph += shift / sr, wrapped to [0, 1);  p0 = ph, p1 = (ph + .5) % 1
+ *   out = read(p1 W) cos((p1 - .5) pi) + read(p0 W) cos((p0 - .5) pi);  write(x) after the reads
+ *   (gen Delay.read: linear, delay clamped to >= 1; delay~: write before read, linear, >= 0)
+ * cycle~(rate_hz, phase): cos(2 pi (ph_lfo + phase)), ph_lfo a double phasor.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include "oracle.h"
+
+static uint32_t pow2ge64(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; return p; }
+static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+typedef struct {
+    double lfo_ph, ps_ph, z1[2], z2[2];
+    double lfo_inc, lfo_off, ps_inc, D, W, b0, b1, b2, a1, a2, mix;
+    double *pring[2], *cring[2];
+} ch64_t;
+
+struct oracle_chorus64 {
+    int n, mode, quantize;
+    double sr;
+    uint32_t psize, csize;
+    uint64_t w;
+    double *pool;
+    ch64_t *v;
+    double *params;            /* [n][OCH_NPARAMS] */
+};
+
+/* quantize = 1: phasor increments rounded to the fp32 spec's 32-bit fixed point (chorus_ref.c
+   fix_inc), so the remaining deviation is the fp32 arithmetic alone */
+static double q32(double inc) { return floor(inc * 4294967296.0 + 0.5) / 4294967296.0; }
+
+static void derive64(const double *p, double sr, int quantize, ch64_t *c)
+{
+    const double pitch = clampd(p[OCH_PITCH], 0.0, 3.0);
+    const double q = clampd(p[OCH_Q], 0.0, 1.0);
+    const double cutoff = clampd(p[OCH_CUTOFF], 0.0, 1.0);
+    const double depth = clampd(p[OCH_DEPTH], 0.08, 1.0);
+    const double rate = clampd(p[OCH_RATE], 0.01, 1.0);
+    const double window = clampd(p[OCH_WINDOW], 4.0, 10.0);
+    c->mix = clampd(p[OCH_MIX], 0.0, 1.0);
+    c->lfo_off = clampd(p[OCH_PHASE], 0.0, 1.0);
+    c->lfo_inc = (0.01 + rate * (0.5 - 0.01)) / sr;          /* scale 0 1 0.01 0.5, :3935 */
+    c->ps_inc = pitch / sr;
+    if (quantize) { c->lfo_inc = q32(c->lfo_inc); c->ps_inc = q32(c->ps_inc); }
+    c->D = (1.0 + depth * (12.0 - 1.0)) * sr / 1000.0;       /* mstosamps(scale 0 1 1 12), :3436 */
+    c->W = window * sr / 1000.0;
+    const double fc = 300.0 + cutoff * (15000.0 - 300.0);    /* :2242 */
+    const double Q = 0.70710678118654752 + 20.0 * q * q * q;
+    const double w0 = 2.0 * 3.14159265358979323846 * fc / sr;
+    const double cw = cos(w0), sw = sin(w0);
+    const double alpha = sw / (2.0 * Q), a0 = 1.0 + alpha;
+    c->b0 = (1.0 - cw) * 0.5 / a0;
+    c->b1 = (1.0 - cw) / a0;
+    c->b2 = (1.0 - cw) * 0.5 / a0;
+    c->a1 = -2.0 * cw / a0;
+    c->a2 = (1.0 - alpha) / a0;
+}
+
+oracle_chorus64 *oracle_chorus64_create(int n_inst, double sample_rate, int mode)
+{
+    if (n_inst <= 0 || (mode & ~3)) return NULL;
+    oracle_chorus64 *o = (oracle_chorus64 *)calloc(1, sizeof(*o));
+    if (!o) return NULL;
+    o->n = n_inst; o->mode = mode & 1; o->quantize = mode >> 1; o->sr = sample_rate;
+    o->psize = pow2ge64((uint32_t)ceil(10.0 * sample_rate / 1000.0) + 2);
+    o->csize = pow2ge64(2u * (uint32_t)ceil(12.0 * sample_rate / 1000.0) + 2);
+    const size_t per = 2u * (o->psize + o->csize);
+    o->pool = (double *)calloc(per * (size_t)n_inst, sizeof(double));
+    o->v = (ch64_t *)calloc((size_t)n_inst, sizeof(ch64_t));
+    o->params = (double *)calloc((size_t)n_inst * OCH_NPARAMS, sizeof(double));
+    if (!o->pool || !o->v || !o->params) { oracle_chorus64_destroy(o); return NULL; }
+    for (int i = 0; i < n_inst; i++) {
+        double *base = o->pool + per * (size_t)i, *p = o->params + (size_t)i * OCH_NPARAMS;
+        o->v[i].pring[0] = base;
+        o->v[i].pring[1] = base + o->psize;
+        o->v[i].cring[0] = base + 2 * o->psize;
+        o->v[i].cring[1] = base + 2 * o->psize + o->csize;
+        p[OCH_PITCH] = 0.0; p[OCH_MIX] = 0.5; p[OCH_Q] = 0.5; p[OCH_CUTOFF] = 0.3;   /* RNBO defaults */
+        p[OCH_PHASE] = 1.0; p[OCH_DEPTH] = 0.5; p[OCH_RATE] = 0.2; p[OCH_WINDOW] = 10.0;
+        derive64(p, o->sr, o->quantize, &o->v[i]);
+    }
+    return o;
+}
+
+void oracle_chorus64_destroy(oracle_chorus64 *o)
+{
+    if (!o) return;
+    free(o->pool); free(o->v); free(o->params); free(o);
+}
+
+int oracle_chorus64_set(oracle_chorus64 *o, int inst, int field, double value)
+{
+    if (!o || inst < 0 || inst >= o->n || field < 0 || field >= OCH_NPARAMS) return -1;
+    o->params[(size_t)inst * OCH_NPARAMS + field] = value;
+    derive64(o->params + (size_t)inst * OCH_NPARAMS, o->sr, o->quantize, &o->v[inst]);
+    return 0;
+}
+
+static double read64(const double *ring, uint32_t mask, uint64_t w, double d, double dmin)
+{
+    d = d < dmin ? dmin : d;
+    const uint64_t di = (uint64_t)d;
+    const double fr = d - (double)di;
+    const double x0 = ring[(w - di) & mask], x1 = ring[(w - di - 1u) & mask];
+    return x0 + fr * (x1 - x0);
+}
+
+static double wrap1(double x) { return x - floor(x); }
+
+/* in: float [2][n_frames][n] (the same inputs as the fp32 oracle); out: double [2][n_frames][n] */
+int oracle_chorus64_process(oracle_chorus64 *o, const float *in, double *out, int n_frames)
+{
+    if (!o || n_frames < 0) return -1;
+    const long n = o->n, plane = n * (long)n_frames;
+    const uint32_t pmask = o->psize - 1, cmask = o->csize - 1;
+    const double pi = 3.14159265358979323846;
+    for (long i = 0; i < n; i++) {
+        ch64_t *s = &o->v[i];
+        for (int f = 0; f < n_frames; f++) {
+            const uint64_t w = o->w + (uint64_t)f;
+            const double lfo = cos(2.0 * pi * wrap1(s->lfo_ph + s->lfo_off));
+            s->lfo_ph = wrap1(s->lfo_ph + s->lfo_inc);
+            const double dch = lfo * s->D + s->D;
+            const double p0 = s->ps_ph, p1 = wrap1(s->ps_ph + 0.5);
+            s->ps_ph = wrap1(s->ps_ph + s->ps_inc);
+            const double g0 = cos((p0 - 0.5) * pi), g1 = cos((p1 - 0.5) * pi);
+            for (int c = 0; c < 2; c++) {
+                const double x = in[c * plane + (long)f * n + i];
+                const double ps = read64(s->pring[c], pmask, w, p1 * s->W, 1.0) * g1 +
+                                  read64(s->pring[c], pmask, w, p0 * s->W, 1.0) * g0;
+                s->pring[c][w & pmask] = x;
+                double y = ps;
+                if (o->mode == 0) {
+                    s->cring[c][w & cmask] = ps;
+                    const double wet = read64(s->cring[c], cmask, w, dch, 0.0);
+                    const double lp = s->b0 * wet + s->z1[c];
+                    s->z1[c] = (s->b1 * wet - s->a1 * lp) + s->z2[c];
+                    s->z2[c] = s->b2 * wet - s->a2 * lp;
+                    y = x * (1.0 - s->mix) + lp * s->mix;
+                }
+                out[c * plane + (long)f * n + i] = y;
+            }
+        }
+    }
+    o->w += (uint64_t)n_frames;
+    return 0;
+}

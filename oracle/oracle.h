@@ -53,6 +53,16 @@ int oracle_chorus_process(oracle_chorus *o, const float *in, float *out, int n_f
 /* config 1: one instance, one core, per-frame calls in fx_test.cpp:45-54's shape */
 long oracle_chorus_c1(float sample_rate, const float *params, long n_frames, int block, double *sum_abs);
 
+/* The same chorus / pitch-shift in double precision with double phasors (gen~ / RNBO arithmetic;
+   oracle/chorus_ref_f64.c): measures the fp32 spec's arithmetic deviation.  out is double.
+   mode: bit 0 as oracle_chorus_create; bit 1 = phasor increments rounded to the spec's 32-bit
+   fixed point (isolates the fp32 arithmetic from the increment rounding). */
+typedef struct oracle_chorus64 oracle_chorus64;
+oracle_chorus64 *oracle_chorus64_create(int n_inst, double sample_rate, int mode);
+void oracle_chorus64_destroy(oracle_chorus64 *o);
+int oracle_chorus64_set(oracle_chorus64 *o, int inst, int field, double value);
+int oracle_chorus64_process(oracle_chorus64 *o, const float *in, double *out, int n_frames);
+
 /* ---- synthlib SynthVoice (DaisySP restatement, parity unpinned) ---- */
 enum {  /* Voice::Config order, modules/synthlib/Voice.h:14-31 */
     OVC_FILTER_CUTOFF = 0, OVC_FILTER_RESONANCE, OVC_FILTER_DRIVE, OVC_FILTER_ENV_AMOUNT,

@@ -71,6 +71,11 @@ def lib(o0: bool = False) -> ctypes.CDLL:
         L.oracle_voice_create_model.argtypes = [ctypes.c_int, _F, ctypes.c_int]
         L.oracle_voice_destroy.argtypes = [ctypes.c_void_p]
         L.oracle_voice_config.argtypes = [ctypes.c_void_p, ctypes.c_int, _PF]
+        L.oracle_chorus64_create.restype = ctypes.c_void_p
+        L.oracle_chorus64_create.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_int]
+        L.oracle_chorus64_destroy.argtypes = [ctypes.c_void_p]
+        L.oracle_chorus64_set.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_double]
+        L.oracle_chorus64_process.argtypes = [ctypes.c_void_p, _PF, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.oracle_voice_note.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.oracle_voice_event.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _F]
         L.oracle_voice_process.argtypes = [ctypes.c_void_p, _PF, ctypes.c_int, ctypes.c_int]
@@ -195,6 +200,35 @@ class Chorus(_Bank):
         assert ch == 2 and n == self.n
         out = np.empty_like(x)
         assert self.L.oracle_chorus_process(self.h, _pf(x), _pf(out), frames, threads) == 0
+        return out
+
+
+class Chorus64(_Bank):
+    """The chorus / pitch-shift in double precision with double phasors (gen~ / RNBO arithmetic,
+    oracle/chorus_ref_f64.c): the yardstick for the fp32 spec's arithmetic deviation."""
+
+    def __init__(self, n: int, sample_rate: float = 48000.0, mode: int = 0):
+        self.n = n
+        self.L = lib()
+        self.h = self.L.oracle_chorus64_create(n, sample_rate, mode)
+        assert self.h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.oracle_chorus64_destroy(self.h)
+            self.h = None
+
+    def set(self, inst: int, field, value: float) -> None:
+        f = CH_FIELDS.index(field) if isinstance(field, str) else int(field)
+        assert self.L.oracle_chorus64_set(self.h, inst, f, float(value)) == 0
+
+    def process(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        ch, frames, n = x.shape
+        assert ch == 2 and n == self.n
+        out = np.empty(x.shape, np.float64)
+        assert self.L.oracle_chorus64_process(
+            self.h, _pf(x), out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), frames) == 0
         return out
 
 

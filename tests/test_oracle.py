@@ -143,6 +143,37 @@ def test_chorus_frozen_golden(golden, key, mode):
     assert [f"{O.fnv1a64_lr(y[0, :, i], y[1, :, i]):016x}" for i in range(g["n"])] == g["fnv1a64"]
 
 
+@pytest.mark.parametrize("key,mode", [("chorus", 0), ("pitchshift", 1)])
+def test_chorus_fp32_deviation_from_double(golden, key, mode):
+    """The spec's declared deviation (fp32 arithmetic, 32-bit fixed-point phasors) MEASURED against
+    the same graph in double precision with double phasors (gen~ / RNBO arithmetic,
+    oracle/chorus_ref_f64.c) on the golden inputs (6 instances x 6,000 frames of white noise).
+    Measured: chorus max |d| / max(|ref|, rms) 1.51e-3 (SNR 77.5 dB), pitch-shift 4.2e-4 (82.3 dB);
+    with the double restatement's increments rounded to the spec's fixed point, 1.8e-4 / 1.4e-4
+    (93.7 / 93.4 dB): the increment rounding (LFO phase drift over time) dominates.  Parity stays
+    unpinned (RNBO / genlib absent); this bounds only the arithmetic."""
+    g = golden[key]
+    p = np.asarray(g["params"], np.float32)
+    x = noise_block(g["n"], g["frames"], g["input_base"])
+    out = {}
+    for q in (0, 2):
+        a, b = O.Chorus(g["n"], 48000.0, mode), O.Chorus64(g["n"], 48000.0, mode | q)
+        for i in range(g["n"]):
+            for f in range(8):
+                a.set(i, f, float(p[f, i]))
+                b.set(i, f, float(p[f, i]))
+        ya, yb = a.process(x).astype(np.float64), b.process(x)
+        d = np.abs(ya - yb)
+        rms = np.sqrt(np.mean(yb ** 2, axis=1, keepdims=True))
+        rel = float(np.max(d / np.maximum(np.abs(yb), rms)))
+        snr = float(10 * np.log10(np.sum(yb ** 2) / np.sum(d ** 2)))
+        out[q] = (rel, snr)
+        print(f"{key} {'fixed-point increments' if q else 'double increments'}: rel {rel:.3g}, SNR {snr:.1f} dB")
+    assert out[0][0] <= 2e-3 and out[0][1] >= 75.0
+    assert out[2][0] <= 2.5e-4 and out[2][1] >= 90.0
+    assert out[2][0] < out[0][0]
+
+
 def test_cos2pi_accuracy():
     xs = np.linspace(-3, 3, 20001).astype(np.float32)
     got = np.array([O.lib().oracle_cos2pi(float(v)) for v in xs], np.float64)
