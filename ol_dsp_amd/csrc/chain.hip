@@ -23,6 +23,7 @@
 // in the same two waves (12.6 us per step against the reverb's 8.1) and left one SIMD idle.
 #include "chorus_stage_l.h"
 #include "dattorro_stage.h"
+#include "lds_flags.h"
 
 namespace olfx {
 
@@ -36,18 +37,6 @@ constexpr int kFlags = 8;                     // LDS progress counters
 constexpr int kChainLds = 4 * kChainRegion + 2 * kDepth * kQBuf + kFlags;
 enum { F_C0 = 0, F_C1, F_PIN, F_POUT, F_DIN };   // chunks published by C0 / C1, taken by P, published by P, taken by DT
 
-__device__ __forceinline__ uint32_t flag_get(const uint32_t *f) {
-    return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void flag_put(uint32_t *f, uint32_t v) {
-    __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// spin (with s_sleep) until cond(); the counters only grow, and every role's wait targets a
-// counter another role advances without waiting on this one first, so the pipeline cannot lock
-template <class Cond>
-__device__ __forceinline__ void wait_for(Cond &&cond) {
-    while (!cond()) __builtin_amdgcn_s_sleep(1);
-}
 }  // namespace
 
 __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v4(ChainArgs a) {

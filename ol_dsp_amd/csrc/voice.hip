@@ -102,6 +102,14 @@ struct Env {
         sus = s;
         set_segment(m, atk_d0, atk_tgt, rel_d0);
     }
+    // the same update with no segment switch, for a chunk computed speculatively: returns the
+    // sample and records in `ended` whether the segment ended (then the chunk is redone by step())
+    __device__ __forceinline__ float step_spec(bool &ended) {
+        const float xn = x + d0 * (tgt - x);
+        ended = ended || xn > hi || xn < lo;
+        x = xn;                                          // == v_med3(xn, lo, hi) while inside
+        return x;
+    }
     __device__ __forceinline__ float step() {
         const float xn = x + d0 * (tgt - x);
         const bool ends = xn > hi || xn < lo;
@@ -292,23 +300,21 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // voice_block_v5 (SvfFilter voices): v4's arithmetic, operation for operation, over
-// FOUR role waves per workgroup of 64 voices, balanced across the SIMDs of a CU.
-//   v4's roles cost about 40 / 34 / 30 VALU instructions per sample (amp / cutoff / filter; with
-//   -ffp-contract=off every a*b+c is two).  Two workgroups share a CU: six waves on four SIMDs, so
-//   two SIMDs carry two roles each and the per-chunk barrier holds every wave to the busiest.
-//   v5's roles:
-//     ENV  : both envelopes, portamento, the phase accumulator, the cutoff sum -> (t, inc, amp, fc_in)
-//     OSC  : the polyBLEP saw from (t, inc)                                     -> (src, amp)
-//     FREQ : Svf::SetFreq(fc_in)                                                -> (fq, damp)
-//     FILT : the two Svf passes, Low() * amp, the output store
-//   about 22 / 23 / 30 / 29 instructions: eight waves per CU, two per SIMD.  Role = wave: rotating
-//   the roles of co-resident workgroups (to pair ENV with FREQ and OSC with FILT on every SIMD) was
-//   measured slower (0.0441 vs 0.0422 ms) and is not built.
+// FOUR role waves per workgroup of 64 voices (two workgroups per CU, two waves per SIMD):
+//   ENV  : the amp and filter Adsr, the cutoff sum                            -> (amp, fc_in)
+//   OSC  : Port, the oscillator's phase, the polyBLEP saw                     -> (src, amp)
+//   FREQ : Svf::SetFreq(fc_in)                                                -> (fq, damp)
+//   FILT : the two Svf passes, Low() * amp, the output store
 // A three-stage pipeline over 16-sample chunks: at step k ENV makes chunk k, OSC and FREQ chunk
-// k-1, FILT chunk k-2; one barrier per step; 64 KB of LDS per workgroup.
+// k-1, FILT chunk k-2; one barrier per step; 48 KB of LDS per workgroup.  Measured per role
+// alone (the others skipping their arithmetic): the skeleton (launch, state,
+// 18 barriers) 9.7 us, FREQ 10.0, FILT 15, OSC 20, ENV 26 of the kernel's 43.6 us.  The envelopes
+// of a full chunk run speculatively (Env::step_spec, no per-sample lane vote and branch) and the
+// chunk is redone exactly when a lane's segment ended in it.  Role = wave: rotating the roles of
+// co-resident workgroups was measured slower and is not built.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
-    __shared__ float4 eq[2][kVcChunk][64];      // ENV -> OSC, FREQ: (t, inc, amp, fc_in)
+    __shared__ float2 eq[2][kVcChunk][64];      // ENV -> OSC, FREQ: (amp, fc_in)
     __shared__ float2 sq[2][kVcChunk][64];      // OSC -> FILT: (src, amp)
     __shared__ float2 fdq[2][kVcChunk][64];     // FREQ -> FILT: (fq, damp)
     const uint32_t n = a.n;
@@ -327,14 +333,12 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     };
 
     if (role == 0) {
-        // ---- ENV (SynthVoice.h:42-48): Adsr x2, Port, the oscillator's phase, the cutoff sum ----
+        // ---- ENV (SynthVoice.h:42,46-47): the amp and filter Adsr, the cutoff sum ----
         const uint32_t flags0 = __float_as_uint(s[VCS_FLAGS * n + i]);
         const bool gate = (flags0 >> 8) & 1u;
         bool gprev_a = (flags0 >> 6) & 1u, gprev_f = (flags0 >> 7) & 1u;
-        const float amp_amt = c[VCC_AMP_AMT * n + i], port_c = c[VCC_PORT_COEF * n + i];
-        const float inv_sr = c[VCC_INV_SR * n + i], freq = s[VCS_FREQ * n + i];
+        const float amp_amt = c[VCC_AMP_AMT * n + i];
         const float cutoff = c[VCC_CUTOFF * n + i], fenv_amt = c[VCC_FENV_AMT * n + i];
-        float phase = s[VCS_PHASE * n + i], port_z = s[VCS_PORT_Z * n + i];
         Env ea, ef;
         ea.begin(gate, gprev_a, flags0 & 7u, s[VCS_ENVA_X * n + i], c[VCC_ATK_D0A * n + i],
                  c[VCC_ATK_TGT_A * n + i], c[VCC_DEC_D0A * n + i], c[VCC_REL_D0A * n + i], c[VCC_SUS_A * n + i]);
@@ -342,52 +346,79 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                  c[VCC_ATK_TGT_F * n + i], c[VCC_DEC_D0F * n + i], c[VCC_REL_D0F * n + i], c[VCC_SUS_F * n + i]);
         for (uint32_t k = 0; k < nsteps; ++k) {
             if (k + 2 < nsteps) {
-                float4 *qo = &eq[k & 1][0][lane];
-                for_chunk(len(k), [&](uint32_t j) {
-                    const float amp = ea.step() * amp_amt;
+                float2 *qo = &eq[k & 1][0][lane];
+                if (len(k) == (uint32_t)kVcChunk) {
+                    // Full chunk: the envelopes run speculatively with no per-sample segment test
+                    // (a branch on a lane vote per sample serialised the chunk); if any lane's
+                    // segment ended inside the chunk -- a few chunks per note -- the chunk is
+                    // redone sample by sample from its start with the exact segment machine.
+                    const float xa0 = ea.x, xf0 = ef.x;
+                    bool ended = false;
+#pragma unroll
+                    for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) {
+                        const float amp = ea.step_spec(ended) * amp_amt;
+                        const float fe = ef.step_spec(ended);
+                        qo[j * 64] = make_float2(amp, cutoff + ((fe * 20000.0f) * fenv_amt));
+                    }
+                    if (__builtin_amdgcn_ballot_w64(ended)) {
+                        ea.x = xa0;
+                        ef.x = xf0;
+                        for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) {
+                            const float amp = ea.step() * amp_amt;
+                            const float fe = ef.step();
+                            qo[j * 64] = make_float2(amp, cutoff + ((fe * 20000.0f) * fenv_amt));
+                        }
+                    }
+                } else {
+                    for_chunk(len(k), [&](uint32_t j) {
+                        const float amp = ea.step() * amp_amt;
+                        const float fe = ef.step();
+                        qo[j * 64] = make_float2(amp, cutoff + ((fe * 20000.0f) * fenv_amt));
+                    });
+                }
+            }
+            __syncthreads();
+        }
+        s[VCS_ENVA_X * n + i] = ea.x;
+        s[VCS_ENVF_X * n + i] = ef.x;
+        s[VCS_FLAGS * n + i] = __uint_as_float(ea.mode | ef.mode << 3 | (uint32_t)gprev_a << 6 |
+                                               (uint32_t)gprev_f << 7 | (uint32_t)gate << 8);
+    } else if (role == 1) {
+        // ---- OSC (SynthVoice.h:44-45): Port::Process, Oscillator::SetFreq / Process, WAVE_POLYBLEP_SAW,
+        //      amp 0.5 ----
+        const float port_c = c[VCC_PORT_COEF * n + i];
+        const float inv_sr = c[VCC_INV_SR * n + i], freq = s[VCS_FREQ * n + i];
+        float phase = s[VCS_PHASE * n + i], port_z = s[VCS_PORT_Z * n + i];
+        for (uint32_t k = 0; k < nsteps; ++k) {
+            if (k >= 1 && k + 1 < nsteps) {
+                const float2 *qi = &eq[(k - 1) & 1][0][lane];
+                float2 *qo = &sq[(k - 1) & 1][0][lane];
+                for_chunk(len(k - 1), [&](uint32_t j) {
                     port_z = freq + port_c * (port_z - freq);     // Port::Process (Portamento.h:218-221)
                     const float inc = port_z * inv_sr;             // Oscillator::SetFreq
                     const float t = phase;                         // Oscillator::Process reads, then advances
                     phase += inc;
                     phase = phase > 1.0f ? phase - 1.0f : phase;
-                    const float fe = ef.step();
-                    qo[j * 64] = make_float4(t, inc, amp, cutoff + ((fe * 20000.0f) * fenv_amt));
+                    float o = (2.0f * t) - 1.0f;
+                    o -= polyblep(inc, t);
+                    o *= -1.0f;
+                    qo[j * 64] = make_float2(o * 0.5f, qi[j * 64].x);
                 });
             }
             __syncthreads();
         }
         s[VCS_PHASE * n + i] = phase;
         s[VCS_PORT_Z * n + i] = port_z;
-        s[VCS_ENVA_X * n + i] = ea.x;
-        s[VCS_ENVF_X * n + i] = ef.x;
-        s[VCS_FLAGS * n + i] = __uint_as_float(ea.mode | ef.mode << 3 | (uint32_t)gprev_a << 6 |
-                                               (uint32_t)gprev_f << 7 | (uint32_t)gate << 8);
-    } else if (role == 1) {
-        // ---- OSC: Oscillator::Process, WAVE_POLYBLEP_SAW, amp 0.5 ----
-        for (uint32_t k = 0; k < nsteps; ++k) {
-            if (k >= 1 && k + 1 < nsteps) {
-                const float4 *qi = &eq[(k - 1) & 1][0][lane];
-                float2 *qo = &sq[(k - 1) & 1][0][lane];
-                for_chunk(len(k - 1), [&](uint32_t j) {
-                    const float4 v = qi[j * 64];
-                    float o = (2.0f * v.x) - 1.0f;
-                    o -= polyblep(v.y, v.x);
-                    o *= -1.0f;
-                    qo[j * 64] = make_float2(o * 0.5f, v.z);
-                });
-            }
-            __syncthreads();
-        }
     } else if (role == 2) {
         // ---- FREQ: Svf::SetFreq (its divisions use the hardware reciprocal, as in v4) ----
         const float damp_res = c[VCC_DAMP_RES * n + i], fc_max = c[VCC_FC_MAX * n + i];
         const float inv_2sr = 1.0f / (c[VCC_SR * n + i] * 2.0f);
         for (uint32_t k = 0; k < nsteps; ++k) {
             if (k >= 1 && k + 1 < nsteps) {
-                const float4 *qi = &eq[(k - 1) & 1][0][lane];
+                const float2 *qi = &eq[(k - 1) & 1][0][lane];
                 float2 *qo = &fdq[(k - 1) & 1][0][lane];
                 for_chunk(len(k - 1), [&](uint32_t j) {
-                    const float fc = fminf(fmaxf(qi[j * 64].w, 1.0e-6f), fc_max);
+                    const float fc = fminf(fmaxf(qi[j * 64].y, 1.0e-6f), fc_max);
                     const float fcn = fc * inv_2sr;
                     const float arg = 0.25f < fcn ? 0.25f : fcn;
                     const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
