@@ -85,3 +85,16 @@ def test_ref_surface_on_gpu():
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "5 tests, 0 failures" in r.stdout
+
+
+def test_ref_header_standalone_without_gpu():
+    """include/olfx_ref.hpp alone (its restated Voice / SoundSource): the reference's constructors
+    compile, the filter component picks the kernel, a foreign SoundSource is refused with
+    OLFX_E_KIND, and without a GPU the first Process throws OLFX_E_NODEVICE."""
+    _build()
+    if os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK | os.W_OK):
+        pytest.skip("GPU visible: the GPU suites cover the run path")
+    r = subprocess.run([os.path.join(CPP, "test_ref_standalone")], capture_output=True, text=True, timeout=60)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "no HIP device" in r.stdout and "0 problems" in r.stdout
