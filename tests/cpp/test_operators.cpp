@@ -10,7 +10,9 @@
  * gtest is not in the image, so a small TEST/EXPECT harness stands in. The binary exits non-zero
  * on any failure. It needs a GPU; run it through tests/test_cpp_operators.py (-m gpu).
  */
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -441,6 +443,55 @@ TEST(PerSample, CallsPerSecond) {
     std::printf("  per-sample calls/s: %.4g (%u instances x %u frames, %.3f s, %u-frame blocks)\n",
                 calls / s, n, blocks * B - 1, s, B);
     EXPECT_TRUE(std::isfinite(acc));
+}
+
+/* The per-frame call from several host threads: each thread owns some of a generation's objects
+   and the threads meet once per frame (frame-major across the generation, as the contract asks).
+   No call takes a process-wide lock; the object that completes a block runs it.  The outputs must
+   equal the oracle one block late, bit for bit. */
+TEST(PerSample, ThreadedFrameMajorBitExact) {
+    const uint32_t n = 8, nt = 4, B = 256, F = 3 * B;
+    std::vector<olfx::ChorusEffect> fx(n);
+    oracle_chorus *ref = oracle_chorus_create((int)n, 48000.f, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        fx[i].init(48000.f);
+        fx[i].setDepth(0.1f + 0.1f * i);
+        oracle_chorus_set(ref, (int)i, OCH_DEPTH, 0.1f + 0.1f * i);
+    }
+    std::vector<float> x = noise(1, F, n, 55), y((size_t)F * n, -1.f);
+    std::atomic<uint32_t> arrived{0}, generation{0};
+    std::atomic<int> errors{0};
+    auto meet = [&]() {                               /* a spin barrier over nt threads */
+        const uint32_t g = generation.load();
+        if (arrived.fetch_add(1) + 1 == nt) { arrived.store(0); generation.fetch_add(1); }
+        else while (generation.load() == g) std::this_thread::yield();
+    };
+    std::vector<std::thread> th;
+    for (uint32_t w = 0; w < nt; ++w)
+        th.emplace_back([&, w]() {
+            for (uint32_t t = 0; t < F; ++t) {
+                for (uint32_t i = w; i < n; i += nt) {
+                    try { y[(size_t)t * n + i] = fx[i].process(x[(size_t)t * n + i]); }
+                    catch (const olfx::Error &) { errors.fetch_add(1); }
+                }
+                meet();
+            }
+        });
+    for (auto &t : th) t.join();
+    EXPECT_EQ(errors.load(), 0);
+    std::vector<float> x2(2 * (size_t)F * n), yr(x2.size());
+    std::memcpy(x2.data(), x.data(), x.size() * 4);
+    std::memcpy(x2.data() + x.size(), x.data(), x.size() * 4);
+    oracle_chorus_process(ref, x2.data(), yr.data(), (int)F, 1);
+    bool ok = true;
+    for (uint32_t t = 0; t < F && ok; ++t)
+        for (uint32_t i = 0; i < n && ok; ++i) {
+            const float want = t < B ? 0.f : yr[(size_t)(t - B) * n + i];
+            ok = std::memcmp(&y[(size_t)t * n + i], &want, 4) == 0;
+            if (!ok) std::printf("  first mismatch t=%u i=%u: %.9g vs %.9g\n", t, i, y[(size_t)t * n + i], want);
+        }
+    EXPECT_TRUE(ok);
+    oracle_chorus_destroy(ref);
 }
 
 int main() { return run_all_tests(); }
