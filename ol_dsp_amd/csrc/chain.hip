@@ -39,132 +39,145 @@ enum { F_C0 = 0, F_C1, F_PIN, F_POUT, F_DIN };   // chunks published by C0 / C1,
 
 }  // namespace
 
-__global__ __launch_bounds__(kChainThreads, 1) void chain_block_v4(ChainArgs a) {
+__global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int kChunk = 16;
     const uint32_t tid = threadIdx.x;
     const uint32_t wib = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
     const uint32_t lane = tid & 63u;
-    const uint32_t base = blockIdx.x * 64u;               // first instance of the workgroup
     const uint32_t n = a.n, nf = a.n_frames;
     const uint32_t nchunks = (nf + kChunk - 1) / kChunk;
+    const uint32_t ngroups = (n + 63u) / 64u;              // 64 instances per group
     float *q1 = lds + 4 * kChainRegion;                    // chorus -> pitch   [kDepth][2 ch][16][64]
     float *q2 = q1 + kDepth * kQBuf;                       // pitch -> reverb
     uint32_t *flags = (uint32_t *)(q2 + kDepth * kQBuf);
     if (tid < kFlags) flags[tid] = 0;
     __syncthreads();                                       // the only barrier
+    // A workgroup runs the groups blockIdx.x, + gridDim.x, ... back to back; its queues and
+    // counters run on across them (chunk number gc = group index in the workgroup x nchunks + c),
+    // so the pipeline fills and drains once per launch, not once per group.
 
     if (wib < 2) {
         // ---------------- C: the chorus, per (instance, channel) lane ----------------
         ch::ChStageL<true> s1;
-        s1.init(a.c1, lds + wib * kChainRegion, lane, base + 32u * wib);
         const ch::Rsrc rIn = ch::rsrc(a.in, (a.plane + (uint64_t)nf * n) * 4);
-        const uint32_t io_v = s1.ch * (uint32_t)a.plane * 4u + s1.i * 4u, frame_b = n * 4u;
-        const uint32_t qcol = s1.ch * kQCh + 32u * wib + s1.j;
-
-        float x[kChunk], xn[kChunk];
-        int C = (int)min((uint32_t)kChunk, nf);
+        const uint32_t frame_b = n * 4u;
+        for (uint32_t g = blockIdx.x, gi = 0; g < ngroups; g += gridDim.x, ++gi) {
+            const uint32_t base = g * 64u, gc0 = gi * nchunks;
+            s1.init(a.c1, lds + wib * kChainRegion, lane, base + 32u * wib);
+            const uint32_t io_v = s1.ch * (uint32_t)a.plane * 4u + s1.i * 4u;
+            const uint32_t qcol = s1.ch * kQCh + 32u * wib + s1.j;
+            float x[kChunk], xn[kChunk];
+            int C = (int)min((uint32_t)kChunk, nf);
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k) x[k] = k < C ? ch::ld1(rIn, io_v, (uint32_t)k * frame_b) : 0.f;
-        s1.begin(x, C);
-        auto step = [&](auto par, uint32_t f0, uint32_t c) {
-            C = (int)min((uint32_t)kChunk, nf - f0);
-            const int Cn = f0 + kChunk < nf ? (int)min((uint32_t)kChunk, nf - f0 - kChunk) : 0;
-            auto prefetch = [&]() {                           // next chunk's input, clamped, unconditional
+            for (int k = 0; k < kChunk; ++k) x[k] = k < C ? ch::ld1(rIn, io_v, (uint32_t)k * frame_b) : 0.f;
+            s1.begin(x, C);
+            auto step = [&](auto par, uint32_t f0, uint32_t c) {
+                C = (int)min((uint32_t)kChunk, nf - f0);
+                const int Cn = f0 + kChunk < nf ? (int)min((uint32_t)kChunk, nf - f0 - kChunk) : 0;
+                auto prefetch = [&]() {                       // next chunk's input, clamped, unconditional
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) {
-                    const float v = ch::ld1(rIn, io_v, min(f0 + kChunk + (uint32_t)k, nf - 1u) * frame_b);
-                    xn[k] = k < Cn ? v : 0.f;
-                }
+                    for (int k = 0; k < kChunk; ++k) {
+                        const float v = ch::ld1(rIn, io_v, min(f0 + kChunk + (uint32_t)k, nf - 1u) * frame_b);
+                        xn[k] = k < Cn ? v : 0.f;
+                    }
+                };
+                // outputs to registers first, then to the queue: a store through a generic
+                // pointer inside the stage's sink may alias the stage object (scratch)
+                float y[kChunk];
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) y[k] = 0.f;
+                s1.template chunk<decltype(par)::value>(x, xn, C, Cn, [&](int k, float v) { y[k] = v; }, prefetch);
+                const uint32_t gc = gc0 + c;
+                wait_for([&] { return flag_get(flags + F_PIN) + kDepth > gc; });   // buffer gc % kDepth free
+                float *q = q1 + (gc % kDepth) * kQBuf + qcol;
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) q[k * 64] = y[k];
+                flag_put(flags + F_C0 + wib, gc + 1);
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) x[k] = xn[k];
             };
-            // outputs to registers first, then to the queue: a store through a generic pointer
-            // inside the stage's sink may alias the stage object, which then stays in scratch
-            float y[kChunk];
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) y[k] = 0.f;
-            s1.template chunk<decltype(par)::value>(x, xn, C, Cn, [&](int k, float v) { y[k] = v; }, prefetch);
-            wait_for([&] { return flag_get(flags + F_PIN) + kDepth > c; });   // buffer c % kDepth free
-            float *q = q1 + (c % kDepth) * kQBuf + qcol;
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) q[k * 64] = y[k];
-            flag_put(flags + F_C0 + wib, c + 1);
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) x[k] = xn[k];
-        };
-        for (uint32_t f0 = 0, c = 0; f0 < nf; f0 += 2 * kChunk, c += 2) {
-            step(std::integral_constant<int, 0>{}, f0, c);
-            if (f0 + kChunk < nf) step(std::integral_constant<int, 1>{}, f0 + kChunk, c + 1);
+            for (uint32_t f0 = 0, c = 0; f0 < nf; f0 += 2 * kChunk, c += 2) {
+                step(std::integral_constant<int, 0>{}, f0, c);
+                if (f0 + kChunk < nf) step(std::integral_constant<int, 1>{}, f0 + kChunk, c + 1);
+            }
+            s1.finish(a.c1);
         }
-        s1.finish(a.c1);
     } else if (wib == 2) {
         // ---------------- P: the pitch-shifter, two 32-instance groups per lane ----------------
         ch::ChStageL<false, true> sa, sb;
-        sa.init(a.c2, lds + 2 * kChainRegion, lane, base);
-        sb.init(a.c2, lds + 3 * kChainRegion, lane, base + 32u);
-        const uint32_t qa = sa.ch * kQCh + sa.j, qb = qa + 32u;
-        float xa[kChunk], xb[kChunk];
-        int C = (int)min((uint32_t)kChunk, nf);
-        sa.begin(xa, C);                                      // XPREV: lines only, x unused
-        sb.begin(xb, C);
-        auto step = [&](auto par, uint32_t f0, uint32_t c) {
-            constexpr int P = decltype(par)::value;
-            C = (int)min((uint32_t)kChunk, nf - f0);
-            const int Cn = f0 + kChunk < nf ? (int)min((uint32_t)kChunk, nf - f0 - kChunk) : 0;
-            wait_for([&] { return flag_get(flags + F_C0) > c && flag_get(flags + F_C1) > c; });
-            const float *qi = q1 + (c % kDepth) * kQBuf;
+        for (uint32_t g = blockIdx.x, gi = 0; g < ngroups; g += gridDim.x, ++gi) {
+            const uint32_t base = g * 64u, gc0 = gi * nchunks;
+            sa.init(a.c2, lds + 2 * kChainRegion, lane, base);
+            sb.init(a.c2, lds + 3 * kChainRegion, lane, base + 32u);
+            const uint32_t qa = sa.ch * kQCh + sa.j, qb = qa + 32u;
+            float xa[kChunk], xb[kChunk];
+            int C = (int)min((uint32_t)kChunk, nf);
+            sa.begin(xa, C);                                  // XPREV: lines only, x unused
+            sb.begin(xb, C);
+            auto step = [&](auto par, uint32_t f0, uint32_t c) {
+                constexpr int P = decltype(par)::value;
+                C = (int)min((uint32_t)kChunk, nf - f0);
+                const int Cn = f0 + kChunk < nf ? (int)min((uint32_t)kChunk, nf - f0 - kChunk) : 0;
+                const uint32_t gc = gc0 + c;
+                wait_for([&] { return flag_get(flags + F_C0) > gc && flag_get(flags + F_C1) > gc; });
+                const float *qi = q1 + (gc % kDepth) * kQBuf;
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) { xa[k] = qi[qa + k * 64]; xb[k] = qi[qb + k * 64]; }
-            flag_put(flags + F_PIN, c + 1);                   // (the release waits for these reads)
-            float y[kChunk];
+                for (int k = 0; k < kChunk; ++k) { xa[k] = qi[qa + k * 64]; xb[k] = qi[qb + k * 64]; }
+                flag_put(flags + F_PIN, gc + 1);              // (the release waits for these reads)
+                float y[kChunk];
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) y[k] = 0.f;
-            sa.template chunk<P>(xa, xa, C, Cn, [&](int k, float v) { y[k] = v; }, []() {});
-            wait_for([&] { return flag_get(flags + F_DIN) + kDepth > c; });
-            float *qo = q2 + (c % kDepth) * kQBuf;
+                for (int k = 0; k < kChunk; ++k) y[k] = 0.f;
+                sa.template chunk<P>(xa, xa, C, Cn, [&](int k, float v) { y[k] = v; }, []() {});
+                wait_for([&] { return flag_get(flags + F_DIN) + kDepth > gc; });
+                float *qo = q2 + (gc % kDepth) * kQBuf;
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) { qo[qa + k * 64] = y[k]; y[k] = 0.f; }
-            sb.template chunk<P>(xb, xb, C, Cn, [&](int k, float v) { y[k] = v; }, []() {});
+                for (int k = 0; k < kChunk; ++k) { qo[qa + k * 64] = y[k]; y[k] = 0.f; }
+                sb.template chunk<P>(xb, xb, C, Cn, [&](int k, float v) { y[k] = v; }, []() {});
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) qo[qb + k * 64] = y[k];
-            flag_put(flags + F_POUT, c + 1);
-        };
-        for (uint32_t f0 = 0, c = 0; f0 < nf; f0 += 2 * kChunk, c += 2) {
-            step(std::integral_constant<int, 0>{}, f0, c);
-            if (f0 + kChunk < nf) step(std::integral_constant<int, 1>{}, f0 + kChunk, c + 1);
+                for (int k = 0; k < kChunk; ++k) qo[qb + k * 64] = y[k];
+                flag_put(flags + F_POUT, gc + 1);
+            };
+            for (uint32_t f0 = 0, c = 0; f0 < nf; f0 += 2 * kChunk, c += 2) {
+                step(std::integral_constant<int, 0>{}, f0, c);
+                if (f0 + kChunk < nf) step(std::integral_constant<int, 1>{}, f0 + kChunk, c + 1);
+            }
+            sa.finish(a.c2);
+            sb.finish(a.c2);
         }
-        sa.finish(a.c2);
-        sb.finish(a.c2);
     } else {
         // ---------------- DT: the reverb, lane = instance, input from the queue ----------------
-        const uint32_t i = base + lane;                       // < d.n (padded to 64)
-        DT_STAGE(a.d, i);
-        const uint32_t t0 = a.d.t0;
-        dt_prime(t0);
-        const bool valid = i < n;
-        for (uint32_t c = 0; c < nchunks; ++c) {
-            const uint32_t f0 = c * kChunk;
-            const uint32_t C = min((uint32_t)kChunk, nf - f0);
-            wait_for([&] { return flag_get(flags + F_POUT) > c; });
-            const float *q = q2 + (c % kDepth) * kQBuf + lane;
-            float xm[kChunk];                                 // the chunk's mono input, (l + r) / 2
+        for (uint32_t g = blockIdx.x, gi = 0; g < ngroups; g += gridDim.x, ++gi) {
+            const uint32_t i = g * 64u + lane, gc0 = gi * nchunks;   // < d.n (padded to 64)
+            DT_STAGE(a.d, i);
+            const uint32_t t0 = a.d.t0;
+            dt_prime(t0);
+            const bool valid = i < n;
+            for (uint32_t c = 0; c < nchunks; ++c) {
+                const uint32_t f0 = c * kChunk, gc = gc0 + c;
+                const uint32_t C = min((uint32_t)kChunk, nf - f0);
+                wait_for([&] { return flag_get(flags + F_POUT) > gc; });
+                const float *q = q2 + (gc % kDepth) * kQBuf + lane;
+                float xm[kChunk];                             // the chunk's mono input, (l + r) / 2
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) xm[k] = (q[k * 64] + q[kQCh + k * 64]) / 2;
-            flag_put(flags + F_DIN, c + 1);
-            for (uint32_t s = 0; s < C; s += 4) {
-                float xin[4], o_l[4], o_r[4];
+                for (int k = 0; k < kChunk; ++k) xm[k] = (q[k * 64] + q[kQCh + k * 64]) / 2;
+                flag_put(flags + F_DIN, gc + 1);
+                for (uint32_t s = 0; s < C; s += 4) {
+                    float xin[4], o_l[4], o_r[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) xin[k] = xm[s + k];
-                dt_step(t0 + f0 + s, f0 + s + 4 < nf, xin, o_l, o_r);
-                if (valid) {
+                    for (int k = 0; k < 4; ++k) xin[k] = xm[s + k];
+                    dt_step(t0 + f0 + s, f0 + s + 4 < nf, xin, o_l, o_r);
+                    if (valid) {
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        a.out[(size_t)(f0 + s + k) * n + i] = o_l[k];
-                        a.out[a.plane + (size_t)(f0 + s + k) * n + i] = o_r[k];
+                        for (int k = 0; k < 4; ++k) {
+                            a.out[(size_t)(f0 + s + k) * n + i] = o_l[k];
+                            a.out[a.plane + (size_t)(f0 + s + k) * n + i] = o_r[k];
+                        }
                     }
                 }
             }
+            dt_finish();
         }
-        dt_finish();
     }
 }
 
@@ -173,8 +186,15 @@ hipError_t launch_chain(const ChainArgs &a, hipStream_t s) {
     if ((a.n_frames & 3u) || (a.c1.t0 & 3u) || (a.d.t0 & 3u) || a.d.n < ((a.n + 63u) & ~63u)) return hipErrorInvalidValue;
     if ((uint64_t)a.n * 2 * a.c1.csize * 4 >= (1ull << 32) || (a.plane + (uint64_t)a.n_frames * a.n) * 4 >= (1ull << 32))
         return hipErrorInvalidValue;
-    const uint32_t blocks = (a.n + 63u) / 64u;
-    hipLaunchKernelGGL(chain_block_v4, dim3(blocks), dim3(kChainThreads), (size_t)kChainLds * sizeof(float), s, a);
+    // one workgroup per CU (LDS and registers allow no more), each running its groups back to back
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return hipErrorInvalidDevice;
+    const uint32_t groups = (a.n + 63u) / 64u;
+    const uint32_t blocks = groups < (uint32_t)cus[dev] ? groups : (uint32_t)cus[dev];
+    hipLaunchKernelGGL(chain_block_v5, dim3(blocks), dim3(kChainThreads), (size_t)kChainLds * sizeof(float), s, a);
     return hipGetLastError();
 }
 
