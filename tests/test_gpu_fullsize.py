@@ -119,6 +119,29 @@ def test_full_size_stream_kinds(cuda, kind, n):
     e.close()
 
 
+def test_chain_persistent_groups_ragged(cuda):
+    """chain_block_v5 runs one workgroup per CU over 64-instance groups back to back, its queues and
+    counters running on across groups.  n = CUs x 64 x 2 + 37 instances: every workgroup runs two
+    or three groups, the last one ragged (37 of 64); sampled instances in first, middle and last
+    groups of several workgroups, over two blocks, bit-exact against the composed oracle."""
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n = cus * 64 * 2 + 37
+    p = _params("chain", 0, n, clone=False)
+    xs = _inputs(0, n, 2, cuda, clone=False)
+    e = _engine("chain", n)
+    e.set_params(0, p)
+    y = _run(e, xs)
+    assert torch.isfinite(y).all()
+    idx = np.array(sorted({0, 63, 64, cus * 64 - 1, cus * 64, cus * 64 + 65, 2 * cus * 64 - 1,
+                           2 * cus * 64, 2 * cus * 64 + 17, n - 1}), np.int64)
+    x = torch.cat(xs, 1)[:, :, idx].cpu().numpy()
+    yr = _oracle("chain", p, idx, np.ascontiguousarray(x))
+    yg = y[:, :, idx].cpu().numpy()
+    assert bits_equal(yg, yr), first_mismatch(yg, yr)
+    e.close()
+
+
 @pytest.mark.parametrize("kind", ["voice", "voice_moog"])
 def test_full_size_voices(cuda, kind):
     """configs[3]'s per-GPU shard: 32,768 voices, NoteOn at block 0 and NoteOff at block 2 of 4 (SURVEY
