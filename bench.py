@@ -221,7 +221,7 @@ def _traffic(name: str, n: int, B: int, override: str = ""):
                 with open(tj) as f:
                     tr = json.load(f)
                 if tr.get("instances") == n and tr.get("block") == B:
-                    return tr.get("hbm_bytes_per_launch")
+                    return tr
             except Exception:
                 pass
     return None
@@ -314,7 +314,17 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
     per_launch = n * B
     achieved = bpf * per_launch / (kern_ms * 1e-3) / 1e9
     achieved_r = rbpf * per_launch / (kern_ms * 1e-3) / 1e9
-    traffic = _traffic(name, n, B, args.traffic_json if name == args.workload else "")
+    tr = _traffic(name, n, B, args.traffic_json if name == args.workload else "")
+    traffic = tr.get("hbm_bytes_per_launch") if tr else None
+    # the PMC-measured HBM bytes of the same kernel (profiles/traffic_<workload>.json, separate
+    # --pmc passes) over this run's kernel time: what HBM actually moved, against the peak
+    measured = {}
+    if tr and traffic:
+        measured["hbm_gbs_measured"] = traffic / (kern_ms * 1e-3) / 1e9
+        rd = tr.get("read_bytes_by_request_size")
+        if rd:
+            measured.update({"traffic_read": rd, "hbm_read_gbs_measured": rd / (kern_ms * 1e-3) / 1e9,
+                             "frac_read_measured": rd / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS})
     if voice:
         fps = VOICE_MOOG_FLOPS_PER_SAMPLE if kind == "voice_moog" else VOICE_FLOPS_PER_SAMPLE
         tflops = fps * per_launch / (kern_ms * 1e-3) / 1e12
@@ -328,7 +338,7 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
                     "achieved_read": achieved_r, "frac_read": achieved_r / HBM_PEAK_GBS,
                     "kernel": kname, "kernel_ms": kern_ms,
                     "algorithmic_bytes_per_frame": bpf, "algorithmic_read_bytes_per_frame": rbpf,
-                    "frames_per_launch": per_launch}
+                    "frames_per_launch": per_launch, **measured}
     res = {"metric": METRIC, "value": frames / elapsed,
            "unit": "voice samples/s" if voice else "stereo samples/s",
            "ms_per_step": elapsed / K * 1e3,
