@@ -145,6 +145,10 @@ struct ChStageL {
         strag_slot = kWin;
     }
 
+    // a window slot, or the junk slot kWin when the position lies outside the window: patches
+    // write unconditionally (a select, no exec-masked block and branch per position)
+    __device__ __forceinline__ static int junk_or(int jw) { return (uint32_t)jw < (uint32_t)kWin ? jw : kWin; }
+
     // this lane's samples in its rings, recomputed where used.  The empty asm makes the lane index
     // look loop-variant: otherwise the loop-invariant products are hoisted, spilled under the
     // register pressure of the carried lines, and every reload (a scratch load) costs a
@@ -328,10 +332,7 @@ struct ChStageL {
             if (started && cur.sC > -kWin - kChunk) {
                 const float *prev = region + kPsvBase + j * kStride + ch;
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) {
-                    const int jw = k - kChunk - cur.sC;
-                    if (jw >= 0 && jw < kWin) wC[jw * kRow] = prev[2 * k];
-                }
+                for (int k = 0; k < kChunk; ++k) wC[junk_or(k - kChunk - cur.sC) * kRow] = prev[2 * k];
             }
         }
         stage_tap<PAR, 0>();
@@ -340,29 +341,21 @@ struct ChStageL {
         if (XPREV && started) {
             if (cur.sA > -kWin - kChunk) {
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) {
-                    const int jw = k - kChunk - cur.sA;
-                    if (jw >= 0 && jw < kWin) wP0[jw * kRow] = xp[k];
-                }
+                for (int k = 0; k < kChunk; ++k) wP0[junk_or(k - kChunk - cur.sA) * kRow] = xp[k];
             }
             if (cur.sB > -kWin - kChunk) {
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) {
-                    const int jw = k - kChunk - cur.sB;
-                    if (jw >= 0 && jw < kWin) wP1[jw * kRow] = xp[k];
-                }
+                for (int k = 0; k < kChunk; ++k) wP1[junk_or(k - kChunk - cur.sB) * kRow] = xp[k];
             }
         }
         // x_c is not in a carried line either
         if (cur.sA > -kWin) {
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k)
-                if (k < C && k - cur.sA < kWin) wP0[(k - cur.sA) * kRow] = x[k];
+            for (int k = 0; k < kChunk; ++k) wP0[junk_or(k < C ? k - cur.sA : kWin) * kRow] = x[k];
         }
         if (cur.sB > -kWin) {
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k)
-                if (k < C && k - cur.sB < kWin) wP1[(k - cur.sB) * kRow] = x[k];
+            for (int k = 0; k < kChunk; ++k) wP1[junk_or(k < C ? k - cur.sB : kWin) * kRow] = x[k];
         }
         started = true;
         prefetch();

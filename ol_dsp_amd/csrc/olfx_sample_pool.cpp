@@ -59,7 +59,7 @@ struct Generation {
     std::vector<float> in;                // [ich][block][n]
     std::vector<float> out[2];            // [och][block][n], by block parity
     std::atomic<uint32_t> live{0}, complete{0};
-    std::atomic<uint64_t> given{0};       // frames given for the block being filled (all instances)
+    std::atomic<bool> filling{false};     // some instance has given a frame of the block being filled
     std::atomic<uint64_t> blocks{0};      // blocks run so far
 };
 
@@ -142,7 +142,7 @@ int run_block(Generation *g) {
     const int rc = olfx_process(g->e.load(), g->ich ? g->in.data() : nullptr, o.data(), g->block, OLFX_IO_HOST, nullptr);
     if (rc) return engine_fail(g, rc, "olfx_process");
     g->complete.store(0, std::memory_order_relaxed);
-    g->given.store(0, std::memory_order_relaxed);
+    g->filling.store(false, std::memory_order_relaxed);
     for (olfx_sample *m : g->members)
         if (m) m->pos.store(0, std::memory_order_relaxed);
     g->blocks.store(b + 1, std::memory_order_release);
@@ -152,7 +152,7 @@ int run_block(Generation *g) {
 int queue_or_apply(olfx_sample *s, const PendingOp &op) {
     Generation *g = s->g;
     std::lock_guard<std::mutex> lk(g->mu);
-    if (!g->e.load() || g->given.load()) {   // before the engine exists, or mid-block: at the next boundary
+    if (!g->e.load() || g->filling.load()) {   // before the engine exists, or mid-block: at the next boundary
         g->pending.push_back(op);
         return OLFX_OK;
     }
@@ -298,7 +298,7 @@ int olfx_sample_process(olfx_sample *s, const float *in, float *out) {
         const float *o = g->out[(blocks - 1) & 1].data();
         for (uint32_t c = 0; c < g->och; ++c) out[c] = o[c * plane + at];
     }
-    g->given.fetch_add(1, std::memory_order_relaxed);
+    if (pos == 0) g->filling.store(true, std::memory_order_relaxed);   // once per instance per block
     s->pos.store(pos + 1, std::memory_order_relaxed);
     if (pos + 1 == g->block && g->complete.fetch_add(1, std::memory_order_acq_rel) + 1 == g->live.load()) {
         std::lock_guard<std::mutex> gl(g->mu);
