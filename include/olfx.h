@@ -121,6 +121,12 @@ enum {
     OLFX_FR_FILTER_DRIVE,        /* [0] */
     OLFX_FR_FILTER_TYPE,         /* 0 low, 1 band, 2 high, 3 notch, 4 peak      [0]     Fx.h:67-73 */
     OLFX_FR_MASTER_VOLUME,       /* [0.8] Fx.h:405 */
+    OLFX_FR_TOPOLOGY,            /* [0] 0: FxRack<2>::Process (Fx.h:432-440): delay -> reverb -> filter1 into the
+                                    zeroed buf_c -> x master (output channel 1 is 0).
+                                    1: the Daisy synth firmware's audio callback (ol_daisy/app/synth/main.cpp:
+                                    78-86): DelayFx<1> on channel 0 -> stereo[0] = stereo[1] -> ReverbFx<2>
+                                    -> FilterFx<2> in place (channel 1 keeps the reverb's output), no master
+                                    volume (MASTER_VOLUME ignored).  Input: the mono signal in channel 0. */
     OLFX_FR_NPARAMS
 };
 /* Chain: chorus params, then pitch-shift params, then dattorro params */

@@ -185,6 +185,11 @@ public:
                  int io = OLFX_IO_HOST, void *stream = nullptr) {
         process(frame_in, frame_out, n_frames, io, stream);
     }
+    /* OLFX_FR_TOPOLOGY: FxRack<2>::Process (Fx.h:432-440), or the Daisy synth firmware's callback
+       chain (ol_daisy/app/synth/main.cpp:78-86: mono in channel 0, delay, stereo copy, reverb,
+       filter in place, no master) */
+    enum class Topology { Rack = 0, DaisyFirmware = 1 };
+    void SetTopology(uint32_t i, Topology t) { set(i, OLFX_FR_TOPOLOGY, static_cast<float>(t)); }
 };
 
 /* ol::synth::SynthVoice over N voices (SynthVoice.h). The config array is in Voice::Config field

@@ -7,6 +7,10 @@
 //   FilterFx<2>  filter1 (Svf, selected output) on channel 0 only; channel 1 is never written
 //                and FxRack's buf_c starts at 0 (Fx.h:408), so output 1 is 0   Fx.h:88-108
 //   out = buf_c * master_volume
+// Topology 1 (OLFX_FR_TOPOLOGY, the Daisy synth firmware's callback, ol_daisy/app/synth/main.cpp:
+// 78-86): DelayFx<1> is the rack's channel-0 delay with its filter; stereo[0] = stereo[1] makes the
+// reverb's two outputs equal, FilterFx<2> in place leaves channel 1 at the reverb output, and there
+// is no master volume (x 1.0f).
 // DelayLine<float, 48000> (DaisySP, restated): read at delay D and D + 1, linear interpolation,
 // read before write.  Here the ring is time-forward (position = t mod 48000) and stereo-
 // interleaved [n][48000][2]: both channels share the delay, so one window load serves both.
@@ -102,6 +106,9 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v2(FxRackArgs a) {
     const float fdrive = __uint_as_float(a.coef[FRC_FDRIVE * n + i]);
     const uint32_t ftype = a.coef[FRC_FTYPE * n + i];
     const float master = __uint_as_float(a.coef[FRC_MASTER * n + i]);
+    // topology 1 (the synth firmware's callback): lane D's output is channel 1 = the reverb
+    // output of the mono delay's stereo copy, which equals channel 0's reverb output b0
+    const bool fw = a.coef[FRC_TOPO * n + i] != 0u;
     // Lane roles (v2): both filters act on channel 0 only (Fx.h:88-108, DelayFx filter_), so the
     // lane pair of an instance splits them: lane ch 0 ("D") runs DelayFx's filter_, lane ch 1 ("F")
     // runs FxRack's filter1 one tick behind, on D's reverb output of the previous frame (a DPP
@@ -222,7 +229,8 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v2(FxRackArgs a) {
             const bool commit = ch ? k >= 1 : frame_k;
             slow = commit ? lo : slow;
             sband = commit ? ba : sband;
-            if constexpr (k >= 1) o[k - 1] = (ch ? so : 0.0f) * master;   // F: channel 0 of frame k-1
+            // F: channel 0 of frame k-1; D: channel 1 (0, or in topology 1 frame k-1's b0)
+            if constexpr (k >= 1) o[k - 1] = (ch ? so : (fw ? b0p : 0.0f)) * master;
             if (frame_k) {
                 // DelayFx: a = filtered * balance + in * (1 - balance) (D lane: channel 0)
                 const float a0 = (so * dbal) + (x[kk] * (1 - dbal));

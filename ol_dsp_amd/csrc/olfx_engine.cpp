@@ -158,6 +158,7 @@ void default_params(int kind, float *p) {
         p[OLFX_FR_FILTER_DRIVE] = 0.f;
         p[OLFX_FR_FILTER_TYPE] = 0.f;
         p[OLFX_FR_MASTER_VOLUME] = 0.8f;
+        p[OLFX_FR_TOPOLOGY] = 0.f;
         break;
     default: break;
     }
@@ -279,7 +280,9 @@ void derive_fxrack(const float *p, float sr, uint32_t *c) {
     svf_coef(p[OLFX_FR_FILTER_CUTOFF], p[OLFX_FR_FILTER_RESONANCE], p[OLFX_FR_FILTER_DRIVE], sr, &f, &d, &dr);
     put(FRC_FFREQ, f); put(FRC_FDAMP, d); put(FRC_FDRIVE, dr);
     c[FRC_FTYPE] = (uint32_t)(int32_t)p[OLFX_FR_FILTER_TYPE];
-    put(FRC_MASTER, p[OLFX_FR_MASTER_VOLUME]);
+    const uint32_t topo = p[OLFX_FR_TOPOLOGY] == 1.f ? 1u : 0u;
+    c[FRC_TOPO] = topo;
+    put(FRC_MASTER, topo ? 1.0f : p[OLFX_FR_MASTER_VOLUME]);   // x 1.0f is exact: no master stage
 }
 
 void derive_voice(const float *p, bool configured, bool moog, float sr, float *c) {
@@ -868,6 +871,8 @@ int olfx_set_params(olfx_engine *e, uint32_t first, uint32_t count, uint32_t fie
             // whose product leaves [0, 65536) have no defined meaning there
             if (predelay && !(v >= 0.f && v * 4800.0f < 65536.0f))
                 return e->fail(OLFX_E_ARG, "olfx_set_params: pre-delay outside [0, 65536/4800)");
+            if (e->kind == OLFX_KIND_FXRACK && field == OLFX_FR_TOPOLOGY && v != 0.f && v != 1.f)
+                return e->fail(OLFX_E_ARG, "olfx_set_params: rack topology must be 0 or 1");
         }
     }
     for (uint32_t f = 0; f < n_fields; ++f)

@@ -190,6 +190,7 @@ enum {
     FRC_FFREQ, FRC_FDAMP, FRC_FDRIVE,       // FxRack filter1 Svf
     FRC_FTYPE,          // uint: 0 low, 1 band, 2 high, 3 notch, 4 peak
     FRC_MASTER,
+    FRC_TOPO,           // uint: OLFX_FR_TOPOLOGY
     FRC_N
 };
 enum { FRS_DLOW = 0, FRS_DBAND, FRS_FLOW, FRS_FBAND, FRS_N };

@@ -43,7 +43,7 @@ PARAMS = {
                       "amp_decay", "amp_sustain", "amp_release", "portamento"],
     _lib.KIND_FXRACK: ["delay_time", "delay_feedback", "delay_balance", "delay_cutoff", "delay_resonance",
                        "reverb_balance", "filter_cutoff", "filter_resonance", "filter_drive", "filter_type",
-                       "master_volume"],
+                       "master_volume", "topology"],
 }
 PARAMS[_lib.KIND_VOICE_MOOG] = PARAMS[_lib.KIND_VOICE]
 PARAMS[_lib.KIND_CHAIN] = (["chorus_" + p for p in PARAMS[_lib.KIND_CHORUS]]

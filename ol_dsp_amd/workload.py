@@ -30,7 +30,7 @@ RANGES = {
     "voice": [(100, 8000), (0, .9), (0, 1), (0, 1), (.001, .5), (0, 1), (.001, .5), (0, 1), (.001, .5),
               (.2, 1), (.001, .5), (0, 1), (.001, .5), (0, 1), (.001, .5), (0, .05)],
     "fxrack": [(0.05, 1), (0, .9), (0, 1), (100, 12000), (0, .8), (0, 1), (100, 12000), (0, .8),
-               (0, 1), "int5", (0, 1)],
+               (0, 1), "int5", (0, 1), 0.0],
 }
 RANGES["voice_moog"] = RANGES["voice"]
 RANGES["chain"] = RANGES["chorus"] + RANGES["pitchshift"] + RANGES["dattorro"]

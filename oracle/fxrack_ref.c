@@ -180,6 +180,7 @@ void oracle_fxrack_defaults(float *p)
     p[OFR_FILTER_DRIVE] = 0.f;
     p[OFR_FILTER_TYPE] = 0.f;                                           /* LowPass */
     p[OFR_MASTER_VOLUME] = 0.8f;                                        /* Fx.h:405 */
+    p[OFR_TOPOLOGY] = 0.f;                                              /* FxRack<2>::Process */
 }
 
 static void rack_init(rack_t *r, float sr)
@@ -205,6 +206,18 @@ static void rack_tick(rack_t *r, const float in[2], float out[2])
     buf[0] = svf_process(&r->dfilt, buf[0], 0);        /* FilterFx (LowPass), channel 0 in place */
     float a[2], b[2];
     for (int i = 0; i < 2; ++i) a[i] = (buf[i] * p[OFR_DELAY_BALANCE]) + (in[i] * (1 - p[OFR_DELAY_BALANCE]));
+    if (p[OFR_TOPOLOGY] == 1.f) {
+        /* ol_daisy/app/synth/main.cpp:78-86: delay_fx (DelayFx<1>: line 0 and its filter, the same
+           arithmetic as the rack's channel 0) on mono; stereo[0] = stereo[1] = mono;
+           reverb_fx.Process(stereo, stereo); filter_fx.Process(stereo, stereo) writes channel 0
+           only, so channel 1 keeps the reverb's output; no master volume */
+        const float m = a[0];
+        const float v = m * 0.8f;
+        const float rv = (v * p[OFR_REVERB_BALANCE]) + (m * (1 - p[OFR_REVERB_BALANCE]));
+        out[0] = svf_process(&r->filt, rv, (int)p[OFR_FILTER_TYPE]);
+        out[1] = rv;
+        return;
+    }
     /* ReverbFx::Process over the ReverbSc stub */
     for (int i = 0; i < 2; ++i) {
         const float v = a[i] * 0.8f;

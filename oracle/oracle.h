@@ -95,6 +95,7 @@ enum {
     OFR_FILTER_DRIVE,          /* FxRack filter1 drive [0,1] */
     OFR_FILTER_TYPE,           /* 0 low, 1 band, 2 high, 3 notch, 4 peak                Fx.h:67-73 */
     OFR_MASTER_VOLUME,         /* FxRack master_volume                                  Fx.h:405 */
+    OFR_TOPOLOGY,              /* 0 FxRack<2>; 1 the synth firmware callback (main.cpp:78-86)    */
     OFR_NPARAMS
 };
 typedef struct oracle_fxrack oracle_fxrack;

@@ -25,7 +25,7 @@ DT_FIELDS = ["pre_delay", "pre_filter", "input_diffusion1", "input_diffusion2",
 CH_FIELDS = ["pitch", "mix", "q", "cutoff", "phase", "depth", "rate", "window"]
 FR_FIELDS = ["delay_time", "delay_feedback", "delay_balance", "delay_cutoff", "delay_resonance",
              "reverb_balance", "filter_cutoff", "filter_resonance", "filter_drive", "filter_type",
-             "master_volume"]
+             "master_volume", "topology"]
 VC_FIELDS = ["filter_cutoff", "filter_resonance", "filter_drive", "filter_env_amount",
              "filter_attack", "filter_attack_shape", "filter_decay", "filter_sustain",
              "filter_release", "amp_env_amount", "amp_attack", "amp_attack_shape",

@@ -180,6 +180,28 @@ TEST(FxRack, MidiControlledRackMatchesOracle) {
     oracle_fxrack_destroy(ref);
 }
 
+/* The Daisy synth firmware's callback chain (ol_daisy/app/synth/main.cpp:78-86) on every other
+   instance of one rack bank: mono voice bus in channel 0, delay, stereo copy, reverb, filter. */
+TEST(FxRack, DaisyFirmwareTopologyMatchesOracle) {
+    const uint32_t n = 33, frames = 700;
+    olfx::FxRackBank rack(n, 48000.f);
+    oracle_fxrack *ref = oracle_fxrack_create((int)n, 48000.f);
+    for (uint32_t i = 0; i < n; i += 2) {
+        rack.SetTopology(i, olfx::FxRackBank::Topology::DaisyFirmware);
+        oracle_fxrack_set(ref, (int)i, OFR_TOPOLOGY, 1.f);
+    }
+    std::vector<float> x = noise(2, frames, n, 11);
+    std::vector<float> y = run_blocks([&](const float *a, float *b, uint32_t f) { rack.Process(a, b, f); },
+                                      x, 2, 2, frames, n, 256);
+    std::vector<float> yr(y.size());
+    oracle_fxrack_process(ref, x.data(), yr.data(), (int)frames, 8);
+    EXPECT_TRUE(first_bit_mismatch(y, yr) == (size_t)-1);
+    bool ch1 = false;
+    for (uint32_t f = 0; f < frames; ++f) ch1 |= y[(size_t)frames * n + (size_t)f * n] != 0.f;
+    EXPECT_TRUE(ch1);
+    oracle_fxrack_destroy(ref);
+}
+
 /* Error behaviour: failures throw olfx::Error carrying the C-ABI code; nothing is silent. */
 /* The per-frame -> block adapter over the GPU rack, driven one frame at a time like the
    workout_buddy AudioCallback, with a MIDI CC queued mid-block: equals the oracle run in blocks

@@ -74,8 +74,8 @@ def test_abi_version_and_kind_info():
     assert vm.state_bytes_per_instance == (8 + 9 + 19) * 4      # + LadderFilter z0_[4], z1_[4], oldinput_
     assert ofx.kind_info(ofx.KIND_CHAIN).n_params == 8 + 2 + 7
     fr = ofx.kind_info(ofx.KIND_FXRACK)
-    assert fr.n_params == 11 and fr.in_channels == 2 and fr.out_channels == 2
-    assert fr.state_bytes_per_instance == (48000 * 2 + 4 + 13) * 4
+    assert fr.n_params == 12 and fr.in_channels == 2 and fr.out_channels == 2
+    assert fr.state_bytes_per_instance == (48000 * 2 + 4 + 14) * 4   # rings, Svf states, coefficients
     with pytest.raises(ofx.OlfxError):
         ofx.kind_info(99)
 

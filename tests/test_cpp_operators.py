@@ -47,7 +47,7 @@ def test_cpp_operators_on_gpu():
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=600)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "16 tests, 0 failures" in r.stdout
+    assert "17 tests, 0 failures" in r.stdout
 
 
 REF_BIN = os.path.join(CPP, "test_ref_surface")

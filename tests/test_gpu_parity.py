@@ -572,6 +572,28 @@ def test_fxrack_long_run_wraps_and_param_change(cuda):
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
 
+def test_fxrack_firmware_topology(cuda):
+    """OLFX_FR_TOPOLOGY 1, the Daisy synth firmware's callback (ol_daisy/app/synth/main.cpp:78-86:
+    DelayFx<1> -> stereo copy -> ReverbFx<2> -> FilterFx<2> in place, no master), mixed with
+    FxRack<2> instances in one engine: bit-exact against the oracle; channel 1 of a firmware
+    instance is its reverb output and does not depend on input channel 1."""
+    n = 96
+    rng = np.random.default_rng(77)
+    p = np.concatenate([fxrack_params(rng, n), np.zeros((1, n), np.float32)], 0)
+    p[11, 1::2] = 1.0
+    x = fast_noise(n, 1200, seed=77)
+    e, ref = _fxrack_pair(n, p)
+    y = run_gpu(e, x, [256, 256, 4, 684], cuda)
+    yr = ref.process(x, threads=8)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+    assert np.any(y[1, :, 1::2] != 0) and np.all(y[1, :, 0::2] == 0)
+    x2 = x.copy()
+    x2[1] = fast_noise(n, 1200, seed=78)[1]          # another input channel 1
+    e2, _ = _fxrack_pair(n, p)
+    y2 = run_gpu(e2, x2, [1200], cuda)
+    assert bits_equal(y2[:, :, 1::2], y[:, :, 1::2])
+
+
 def test_fxrack_golden_and_channel1_silent(cuda, golden):
     g = golden["fxrack"]
     p = np.asarray(g["params"], np.float32)
