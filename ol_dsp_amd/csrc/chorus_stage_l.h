@@ -401,6 +401,16 @@ struct ChStageL {
         } else {
             // generic chunk (partial, or a pitch window the lines cannot cover): per frame, with
             // per-frame guards and direct ring reads for the uncovered pitch taps
+            if (XPREV) {
+                // XPREV stores the chunk's own input only after its line loads (stores_and_next),
+                // but a direct read of an uncovered tap can reach into this chunk (a delay below
+                // 16 right after a phasor wrap): store it now, per lane (the coalesced store
+                // follows as usual).  The reads below are this lane's own, in issue order.
+                const uint32_t pb = own_pb();
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k)
+                    st1(rP, valid && k < C ? pb + ((w0 + (uint32_t)k) & pmask) * 8u : 0xFFFFFFF0u, 0, x[k]);
+            }
             float pl_lfo[2], pl_gA[2], pl_gB[2];
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) {

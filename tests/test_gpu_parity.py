@@ -526,6 +526,51 @@ def test_chain_vs_composed_oracle(cuda):
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
 
+def _chain_oracle(n, pc, pp, pd):
+    c1, c2, d = O.Chorus(n), O.Chorus(n, mode=1), O.Dattorro(n)
+    _chain_oracle_set(c1, c2, d, n, pc, pp, pd)
+    return c1, c2, d
+
+
+def _chain_oracle_set(c1, c2, d, n, pc, pp, pd):
+    for i in range(n):
+        for f in range(8):
+            c1.set(i, f, float(pc[f, i]))
+        c2.set(i, "pitch", float(pp[0, i]))
+        c2.set(i, "window", float(pp[1, i]))
+        for f in range(7):
+            d.set(i, f, float(pd[f, i]))
+
+
+def test_chain_predelays_long_run_and_param_change(cuda):
+    """The fused chain over 70,000 frames (the reverb's uint16 t passes the t = 32,768 modulation
+    turn and wraps, the chorus and pitch rings wrap many times), per-instance pre-delays on both
+    sides of the register-history limit (0..12), the block edges and the maximum, a ragged
+    instance count (two groups, the second partial) and every parameter changed at frame 35,000:
+    bit-exact against the composed oracle."""
+    n = 100
+    rng = np.random.default_rng(41)
+    pc, pp, pd = chorus_params(rng, n), chorus_params(rng, n)[[0, 7]], dt_params(rng, n, 0.0)
+    edge = np.array([0, 1, 3, 4, 7, 8, 9, 12, 13, 255, 256, 257, 4799, 4800], np.float32) / 4800
+    pd[0] = rng.uniform(0, 1, n)
+    pd[0, 64:64 + len(edge)] = edge
+    pd[0, :8] = edge[:8]
+    x = fast_noise(n, 70000, seed=41)
+    e = engine("chain", n)
+    e.set_params(0, np.concatenate([pc, pp, pd], 0))
+    y1 = run_gpu(e, x[:, :35000], [4096] * 8 + [2096, 4, 132], cuda)
+    c1, c2, d = _chain_oracle(n, pc, pp, pd)
+    yr1 = d.process(c2.process(c1.process(x[:, :35000])))
+    pc2, pp2, pd2 = chorus_params(rng, n), chorus_params(rng, n)[[0, 7]], dt_params(rng, n, 0.0)
+    pd2[0] = rng.uniform(0, 1, n)
+    e.set_params(0, np.concatenate([pc2, pp2, pd2], 0))
+    _chain_oracle_set(c1, c2, d, n, pc2, pp2, pd2)
+    y2 = run_gpu(e, x[:, 35000:], [4096] * 8 + [2232], cuda)
+    yr2 = d.process(c2.process(c1.process(x[:, 35000:])))
+    y, yr = np.concatenate([y1, y2], 1), np.concatenate([yr1, yr2], 1)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
 # ------------------------------------------------------------------------------- fx rack
 def _fxrack_pair(n, p):
     e = engine("fxrack", n)
