@@ -287,6 +287,33 @@ def test_chorus_line_carry_stress(cuda, kind):
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
 
+@pytest.mark.parametrize("kind", ["chorus", "pitchshift"])
+def test_chorus_long_run_many_wraps(cuda, kind):
+    """100,000 frames at the fastest pitch phasors (every instance's two pitch taps wrap 12 times,
+    each wrap a generic chunk with direct ring reads), ragged blocks with partial chunks:
+    bit-exact against the oracle."""
+    n, frames = 70, 100000
+    rng = np.random.default_rng(93)
+    p = chorus_params(rng, n)
+    p[0] = rng.uniform(2.5, 3.0, n)                      # pitch phasor Hz
+    x = fast_noise(n, frames, seed=93)
+    e = engine(kind, n)
+    ref = O.Chorus(n, mode=0 if kind == "chorus" else 1)
+    if kind == "chorus":
+        e.set_params(0, p)
+        for i in range(n):
+            for f in range(8):
+                ref.set(i, f, float(p[f, i]))
+    else:
+        e.set_params(0, p[[0, 7]])
+        for i in range(n):
+            ref.set(i, "pitch", float(p[0, i]))
+            ref.set(i, "window", float(p[7, i]))
+    y = run_gpu(e, x, [4096] * 24 + [1408, 4, 12, 272], cuda)
+    yr = ref.process(x, threads=8)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
 def test_chorus_defaults_and_edges(cuda):
     """RNBO defaults, params clamped to @min/@max (out-of-range values), mix 0 == dry."""
     n = 5
