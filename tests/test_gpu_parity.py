@@ -410,6 +410,39 @@ def test_voice_vs_oracle(cuda, kind):
     assert np.quantile(pw, 0.99) <= 1e-5
 
 
+@pytest.mark.parametrize("kind", ["voice", "voice_moog"])
+def test_voice_long_run_event_storm(cuda, kind):
+    """200 blocks with NoteOn / NoteOff for a random third of the voices at every block boundary
+    (retriggers in attack, decay, sustain and release; notes repeated and changed, so portamento
+    and both envelopes restart from every segment) and a config change half way: the voices stay
+    within the parity tolerance of the oracle and finite."""
+    n, blocks = 128, 200
+    rng = np.random.default_rng(57)
+    cfg = voice_configs(rng, n)
+    notes = [int(v) for v in rng.integers(36, 97, n)]
+    e, ref = _voice_pair(n, cfg, notes, kind=kind)
+    ys, yrs = [], []
+    for b in range(blocks):
+        if b == blocks // 2:
+            cfg = voice_configs(rng, n)
+            e.set_params(0, cfg)
+            for i in range(n):
+                ref.config(i, cfg[:, i])
+        if b:
+            who = np.flatnonzero(rng.random(n) < 1 / 3)
+            on = rng.random(len(who)) < 0.5
+            nn = rng.integers(36, 97, len(who))
+            ev = [(int(i), int(o), int(m)) for i, o, m in zip(who, on, nn)]
+            e.note_events(ev)
+            for i, o, m in ev:
+                ref.note(i, bool(o), m)
+        ys.append(_voice_run(e, 256, cuda))
+        yrs.append(ref.process(256))
+    y, yr = np.concatenate(ys, 1), np.concatenate(yrs, 1)
+    assert np.all(np.isfinite(y))
+    assert rel_err(y[0].T, yr[0].T) <= VOICE_TOL
+
+
 def test_voice_golden_and_pins(cuda, golden):
     g = golden["voice"]
     p = np.asarray(g["params"], np.float32)
