@@ -712,6 +712,65 @@ def test_fxrack_golden_and_channel1_silent(cuda, golden):
 
 
 # ------------------------------------------------------------------- control changes (8f row 4)
+def _tiny_blocks(rng, total):
+    """Random block lengths, multiples of 4 from 4 to 40 frames, summing to total."""
+    out, left = [], total
+    while left > 0:
+        b = min(left, 4 * int(rng.integers(1, 11)))
+        out.append(b)
+        left -= b
+    return out
+
+
+@pytest.mark.parametrize("kind", ["chain", "chorus", "pitchshift", "dattorro", "fxrack"])
+@pytest.mark.parametrize("n", [1, 70])
+def test_tiny_ragged_blocks(cuda, kind, n):
+    """Host callbacks of 4..40 frames (every chunk partial or short, one launch per callback),
+    a single instance and a ragged count: bit-exact against the oracle."""
+    rng = np.random.default_rng(1000 + n)
+    frames = 3000
+    x = fast_noise(n, frames, seed=n + 7)
+    blocks = _tiny_blocks(rng, frames)
+    e = engine(kind, n)
+    if kind == "chain":
+        pc, pp, pd = chorus_params(rng, n), chorus_params(rng, n)[[0, 7]], dt_params(rng, n, 0.0)
+        pd[0] = rng.uniform(0, 0.01, n)                  # pre-delays 0..48: registers and ring
+        e.set_params(0, np.concatenate([pc, pp, pd], 0))
+        c1, c2, d = _chain_oracle(n, pc, pp, pd)
+        yr = d.process(c2.process(c1.process(x)))
+    elif kind in ("chorus", "pitchshift"):
+        p = chorus_params(rng, n)
+        p[0, ::3] = 3.0                                  # fastest phasor: wraps inside the run
+        ref = O.Chorus(n, mode=0 if kind == "chorus" else 1)
+        if kind == "chorus":
+            e.set_params(0, p)
+            for i in range(n):
+                for f in range(8):
+                    ref.set(i, f, float(p[f, i]))
+        else:
+            e.set_params(0, p[[0, 7]])
+            for i in range(n):
+                ref.set(i, "pitch", float(p[0, i]))
+                ref.set(i, "window", float(p[7, i]))
+        yr = ref.process(x, threads=8)
+    elif kind == "dattorro":
+        p = dt_params(rng, n, 0.0)
+        p[0] = rng.uniform(0, 0.01, n)
+        e.set_params(0, p)
+        ref = O.Dattorro(n)
+        for i in range(n):
+            for f in range(7):
+                ref.set(i, f, float(p[f, i]))
+        yr = ref.process(x, threads=8)
+    else:
+        p = np.concatenate([fxrack_params(rng, n), np.zeros((1, n), np.float32)], 0)
+        p[11, ::2] = 1.0
+        e, ref = _fxrack_pair(n, p)
+        yr = ref.process(x, threads=8)
+    y = run_gpu(e, x, blocks, cuda)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
 def test_control_changes_equal_mapped_params(cuda):
     """olfx_control applies the reference's CC handlers: an engine driven by MIDI / hardware
     control changes matches one given the mapped values by set_param (bit-exact), and the fx
