@@ -443,6 +443,32 @@ def test_voice_long_run_event_storm(cuda, kind):
     assert rel_err(y[0].T, yr[0].T) <= VOICE_TOL
 
 
+@pytest.mark.parametrize("kind", ["voice", "voice_moog"])
+def test_voice_tiny_ragged_blocks(cuda, kind):
+    """Voices rendered in 4..40-frame callbacks (partial 16-sample chunks, one launch each) with
+    note events between them: within the parity tolerance of the oracle run as one stream."""
+    n = 70
+    rng = np.random.default_rng(88)
+    cfg = voice_configs(rng, n)
+    notes = [int(v) for v in rng.integers(36, 97, n)]
+    e, ref = _voice_pair(n, cfg, notes, kind=kind)
+    ys, yrs, total = [], [], 0
+    while total < 3000:
+        b = 4 * int(rng.integers(1, 11))
+        if total and rng.random() < 0.2:
+            who = np.flatnonzero(rng.random(n) < 0.5)
+            ev = [(int(i), int(rng.random() < 0.5), int(rng.integers(36, 97))) for i in who]
+            e.note_events(ev)
+            for i, o, m in ev:
+                ref.note(i, bool(o), m)
+        ys.append(_voice_run(e, b, cuda))
+        yrs.append(ref.process(b))
+        total += b
+    y, yr = np.concatenate(ys, 1), np.concatenate(yrs, 1)
+    assert np.all(np.isfinite(y))
+    assert rel_err(y[0].T, yr[0].T) <= VOICE_TOL
+
+
 def test_voice_golden_and_pins(cuda, golden):
     g = golden["voice"]
     p = np.asarray(g["params"], np.float32)
