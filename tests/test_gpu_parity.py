@@ -195,6 +195,46 @@ def test_dattorro_reset(cuda):
     assert bits_equal(a, b) and e.frames_processed == 512
 
 
+@pytest.mark.parametrize("kind", ["chain", "chorus", "pitchshift", "fxrack", "voice", "voice_moog"])
+def test_reset_every_kind(cuda, kind):
+    """olfx_reset is destroy + create without reallocating (include/olfx.h): every instance back
+    to its freshly created state (rings, recursive state, phasors, envelopes, stream time, default
+    parameters).  Run, reset, set the same parameters, run again: the same bits as the first run
+    and as a fresh engine."""
+    n = 40
+    rng = np.random.default_rng(3)
+    if kind in ("voice", "voice_moog"):
+        cfg = voice_configs(rng, n)
+
+        def run(e):
+            e.set_params(0, cfg)
+            e.note_events([(i, 1, 40 + i) for i in range(n)])
+            return np.concatenate([_voice_run(e, 256, cuda), _voice_run(e, 100, cuda)], 1)
+    else:
+        if kind == "chain":
+            p = np.concatenate([chorus_params(rng, n), chorus_params(rng, n)[[0, 7]], dt_params(rng, n, 0.05)], 0)
+        elif kind == "chorus":
+            p = chorus_params(rng, n)
+        elif kind == "pitchshift":
+            p = chorus_params(rng, n)[[0, 7]]
+        else:
+            p = fxrack_params(rng, n)
+        x = fast_noise(n, 1000, seed=3)
+
+        def run(e):
+            e.set_params(0, p)
+            return run_gpu(e, x, [256, 744], cuda)
+    e = engine(kind, n)
+    a = run(e)
+    e.reset()
+    assert e.frames_processed == 0
+    b = run(e)
+    c = run(engine(kind, n))
+    assert np.any(a != 0)
+    assert bits_equal(a, b), first_mismatch(a, b)
+    assert bits_equal(a, c), first_mismatch(a, c)
+
+
 def test_dattorro_full_size_properties(cuda):
     """65,536 instances (BASELINE config 3): sampled instances match the oracle exactly, and
     instances sharing params and input produce identical output (checksum of checksums)."""
