@@ -185,6 +185,45 @@ def test_dattorro_host_io_equals_device_io(cuda):
     assert bits_equal(yd, yh)
 
 
+@pytest.mark.parametrize("kind", ["chain", "chorus", "fxrack"])
+def test_host_io_streams_and_interleaved_engines(cuda, kind):
+    """The same job three ways: device buffers on torch's stream; host (numpy) buffers staged by
+    libolfx; and device buffers on a side stream, with a second engine of the same kind processing
+    different inputs in between on another stream.  All bit-identical."""
+    import torch
+    n = 50
+    rng = np.random.default_rng(12)
+    if kind == "chain":
+        p = np.concatenate([chorus_params(rng, n), chorus_params(rng, n)[[0, 7]], dt_params(rng, n, 0.02)], 0)
+    elif kind == "chorus":
+        p = chorus_params(rng, n)
+    else:
+        p = fxrack_params(rng, n)
+    x = fast_noise(n, 1024, seed=12)
+    other = fast_noise(n, 1024, seed=13)
+    ea, eb, ec, ed = (engine(kind, n) for _ in range(4))
+    for e in (ea, eb, ec, ed):
+        e.set_params(0, p)
+    ya = run_gpu(ea, x, [256] * 4, cuda)
+    yb = np.concatenate([eb.process(np.ascontiguousarray(x[:, f:f + 256])) for f in range(0, 1024, 256)], 1)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    # every input made before the loop and kept alive: a freed tensor's memory would be reused
+    # by the caching allocator while the other stream still reads it
+    xcs = [torch.from_numpy(np.ascontiguousarray(x[:, f:f + 256])).to(cuda) for f in range(0, 1024, 256)]
+    xds = [torch.from_numpy(np.ascontiguousarray(other[:, f:f + 256])).to(cuda) for f in range(0, 1024, 256)]
+    torch.cuda.synchronize()
+    outs = []
+    for xc, xd in zip(xcs, xds):
+        with torch.cuda.stream(s1):
+            outs.append(ec.process(xc, stream=s1.cuda_stream))
+        with torch.cuda.stream(s2):
+            ed.process(xd, stream=s2.cuda_stream)
+    torch.cuda.synchronize()
+    yc = np.concatenate([o.cpu().numpy() for o in outs], 1)
+    assert bits_equal(ya, yb), first_mismatch(ya, yb)
+    assert bits_equal(ya, yc), first_mismatch(ya, yc)
+
+
 def test_dattorro_reset(cuda):
     n = 8
     x = fast_noise(n, 512, seed=6)
