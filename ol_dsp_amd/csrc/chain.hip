@@ -29,7 +29,7 @@ namespace olfx {
 
 namespace {
 constexpr int kChainThreads = 256;            // 4 waves
-constexpr int kQCh = 16 * 64 + 32;            // floats per channel of one queue buffer (padded)
+constexpr int kQCh = 16 * 64 + 16;            // floats per channel of one queue buffer, padded to 16 mod 32: the two channels of a lane pair sit 16 banks apart
 constexpr int kQBuf = 2 * kQCh;               // one buffer: [ch][16 frames][64 instances]
 constexpr int kDepth = 3;                     // buffers per queue: a role may run 2 chunks ahead
 constexpr int kChainRegion = ch::ChStageL<true>::kRegion;

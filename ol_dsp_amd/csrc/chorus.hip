@@ -66,9 +66,10 @@ hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s) {
         return hipErrorInvalidValue;
     const uint32_t waves = (a.n + 31) / 32;              // 32 instances x 2 channels per wave
     const uint32_t blocks = (waves + ch::kThreads / 64 - 1) / (ch::kThreads / 64);
-    const size_t lds = (size_t)(ch::kThreads / 64) * ch::ChStageL<true>::kRegion * sizeof(float);
-    if (a.mode == 0) hipLaunchKernelGGL(chorus_block_v11<true>, dim3(blocks), dim3(ch::kThreads), lds, s, a);
-    else hipLaunchKernelGGL(chorus_block_v11<false>, dim3(blocks), dim3(ch::kThreads), lds, s, a);
+    const size_t lds_c = (size_t)(ch::kThreads / 64) * ch::ChStageL<true>::kRegion * sizeof(float);
+    const size_t lds_p = (size_t)(ch::kThreads / 64) * ch::ChStageL<false>::kRegion * sizeof(float);
+    if (a.mode == 0) hipLaunchKernelGGL(chorus_block_v11<true>, dim3(blocks), dim3(ch::kThreads), lds_c, s, a);
+    else hipLaunchKernelGGL(chorus_block_v11<false>, dim3(blocks), dim3(ch::kThreads), lds_p, s, a);
     return hipGetLastError();
 }
 

@@ -85,7 +85,9 @@ __device__ __forceinline__ PlanL plan_chunk_l(uint32_t lfo_acc, uint32_t lfo_inc
 template <bool FULL, bool XPREV = false>
 struct ChStageL {
     static constexpr int kChunk = 16, kWin = 24, kSlots = kWin + 1;
-    static constexpr int kRegion = 3 * kSlots * kRow;   // floats of LDS per wave (4,800), as v10
+    // floats of LDS per wave: one window per tap (chorus 4,800 = 19.2 KB: 2 waves/SIMD; pitch-shift
+    // alone 3,200 = 12.8 KB, so its 137-VGPR kernel runs 3 waves/SIMD)
+    static constexpr int kRegion = (FULL ? 3 : 2) * kSlots * kRow;
     static constexpr int kStride = 36;
     static constexpr uint32_t kPsvBase = 32u * kStride;
     static constexpr int kTaps = FULL ? 3 : 2;
@@ -97,11 +99,11 @@ struct ChStageL {
     float D, W, b0, b1, b2, a1, a2, mix, dry;
     uint32_t lfo_acc, ps_acc;
     float z1, z2;
-    uint32_t pmask, cmask, pstride, cstride;
+    uint32_t pmask, cmask, pshift, cshift;   // ring sizes are powers of two: instance offset = i << shift
     float pmax, cmax;
     Rsrc rP, rC;
     float *region;
-    float4 ln[3][2][4];       // [tap][line set][part]: piece (lane & 7) of a line of instance part*8 + lane/8
+    float4 ln[3][2][4];       // [tap][line set][part]: piece lane/8 of a line of instance part*8 + (lane & 7)
     uint32_t s15;             // window start & 15 per (tap, part), 2 bits each (start is 4-aligned)
     float strag;              // chorus straggler (own channel)
     uint32_t strag_slot;      // its LDS slot (kWin = junk)
@@ -136,7 +138,7 @@ struct ChStageL {
         pmax = (float)(a.psize - 2u); cmax = (float)(a.csize - 2u);
         rP = rsrc(a.pitch_ring, (uint64_t)n * 2 * a.psize * 4);
         rC = rsrc(a.chorus_ring, (uint64_t)n * 2 * a.csize * 4);
-        pstride = a.psize * 8u; cstride = a.csize * 8u;
+        pshift = (uint32_t)__builtin_ctz(a.psize) + 3u; cshift = (uint32_t)__builtin_ctz(a.csize) + 3u;
         region = lds_region;
         wpos = a.t0;
         started = false;
@@ -158,16 +160,19 @@ struct ChStageL {
         asm volatile("" : "+v"(l));
         return min(inst0 + (l >> 1), n - 1u);
     }
-    __device__ __forceinline__ uint32_t own_pb() const { return own_i() * pstride + (lane & 1u) * 4u; }
-    __device__ __forceinline__ uint32_t own_cb() const { return own_i() * cstride + (lane & 1u) * 4u; }
+    __device__ __forceinline__ uint32_t own_pb() const { return (own_i() << pshift) + (lane & 1u) * 4u; }
+    __device__ __forceinline__ uint32_t own_cb() const { return (own_i() << cshift) + (lane & 1u) * 4u; }
 
-    // cooperative line geometry: part r (0..3) -> instance r*8 + lane/8, piece lane & 7
-    __device__ __forceinline__ uint32_t pjj(int r) const { return (uint32_t)r * 8u + (lane >> 3); }
-    __device__ __forceinline__ uint32_t pm() const { return lane & 7u; }
+    // cooperative line geometry: part r (0..3) -> instance r*8 + (lane & 7), piece lane / 8.
+    // Pieces outermost: a ds_write_b64 lane group (16 contiguous lanes) then stages two pieces of
+    // eight instances (eight bank pairs, 2-way) instead of eight pieces of two instances (the
+    // same bank pair in eight rows, 8-way); the line loads still cover 8 whole lines per wave.
+    __device__ __forceinline__ uint32_t pjj(int r) const { return (uint32_t)r * 8u + (lane & 7u); }
+    __device__ __forceinline__ uint32_t pm() const { return lane >> 3; }
 
     __device__ __forceinline__ uint32_t line_off(int t, uint32_t oi, uint32_t q) const {
         const uint32_t pos = q * 16u + 2u * pm();
-        return t < 2 ? oi * pstride + (pos & pmask) * 8u : oi * cstride + (pos & cmask) * 8u;
+        return t < 2 ? (oi << pshift) + (pos & pmask) * 8u : (oi << cshift) + (pos & cmask) * 8u;
     }
     __device__ __forceinline__ float4 ld_line(int t, uint32_t off) const { return ld4(t < 2 ? rP : rC, off); }
 
@@ -229,8 +234,7 @@ struct ChStageL {
             const int st = (int)(((s15 >> (2 * (t * 4 + r))) & 3u) << 2);
             const int slo = 2 * (int)pm() - st;          // line L' piece -> slots slo, slo + 1
             const int shi = slo + 16;                     // line L'+1 piece
-            // only pieces inside the window are written (exec-masked): the 8 lanes of an
-            // instance hit the same two banks, so every skipped write is a conflict saved
+            // only pieces inside the window are written (exec-masked)
             const float4 a = ln[t][LO][r], b = ln[t][HI][r];
             if (slo >= 0) {
                 float *plo = base + slo * kRow + 2 * jj;
@@ -258,8 +262,8 @@ struct ChStageL {
             const float4 v = *(const float4 *)(region + base + o * kStride + 2u * f2);
             const uint32_t oi = inst0 + o;
             const bool ok = oi < n && (int)f2 < C;      // else an offset past the buffer: dropped
-            if (pitch) st4<kStreamAux>(rP, ok ? oi * pstride + ((w + f2) & pmask) * 8u : 0xFFFFFFF0u, v);
-            else st4<kStreamAux>(rC, ok ? oi * cstride + ((w + f2) & cmask) * 8u : 0xFFFFFFF0u, v);
+            if (pitch) st4<kStreamAux>(rP, ok ? (oi << pshift) + ((w + f2) & pmask) * 8u : 0xFFFFFFF0u, v);
+            else st4<kStreamAux>(rC, ok ? (oi << cshift) + ((w + f2) & cmask) * 8u : 0xFFFFFFF0u, v);
         }
     }
 

@@ -8,9 +8,9 @@ root=$(git rev-parse --show-toplevel)
 dst=$root/build/ab/src_$name
 rm -rf "$dst"; mkdir -p "$dst/ol_dsp_amd/csrc" "$dst/include"
 if [ "$rev" = wt ]; then
-  cp "$root"/ol_dsp_amd/csrc/* "$dst/ol_dsp_amd/csrc/"; cp "$root"/include/* "$dst/include/"
+  find "$root"/ol_dsp_amd/csrc -maxdepth 1 -type f -exec cp {} "$dst/ol_dsp_amd/csrc/" \; ; cp "$root"/include/* "$dst/include/"
 else
   git -C "$root" archive "$rev" ol_dsp_amd/csrc include | tar -x -C "$dst"
 fi
-make -s -C "$dst/ol_dsp_amd/csrc" OUT="$root/build/ab/$name.so" EXTRA="$*" -B 2>&1 | grep -v warning || true
+make -s -j8 -C "$dst/ol_dsp_amd/csrc" OUT="$root/build/ab/$name.so" EXTRA="$*" -B 2>&1 | grep -v warning || true
 ls -la "$root/build/ab/$name.so"
