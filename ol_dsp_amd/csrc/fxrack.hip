@@ -134,12 +134,17 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v2(FxRackArgs a) {
     // window of the chunk starting at t: first position (t - D - 1) rounded down to even, as an
     // offset from t (the ring position of t is (a.t0 + f0) mod 48000)
     auto rel_of = [&](uint32_t t) { return (int)(((int64_t)t - (int64_t)D - 1) & ~(int64_t)1) - (int)t; };
-    // cooperative window load: piece P = r * 64 + lane of 320 -> instance jj = P / 10, piece m
+    // cooperative window load: piece P = r * 64 + lane of 320 -> piece m = P / 32 of instance
+    // jj = P % 32 (instances innermost).  A ds_write_b64 lane group (16 contiguous lanes) then
+    // stages one piece of 16 instances: 16 distinct bank pairs, conflict-free.  (Pieces innermost,
+    // m = P % 10, put up to ten pieces of one instance -- one bank pair -- in a group.)
+    auto piece_inst = [&](int) { return lane & 31u; };
+    auto piece_idx = [&](int r) { return (uint32_t)r * 2u + (lane >> 5); };
     float4 v[5];
     auto load_window = [&](uint32_t t) {
 #pragma unroll
         for (int r = 0; r < 5; ++r) {
-            const uint32_t P = (uint32_t)r * 64u + lane, jj = P / 10u, m = P % 10u;
+            const uint32_t jj = piece_inst(r), m = piece_idx(r);
             const int rel = __builtin_amdgcn_ds_bpermute((int)(jj << 3), rel_of(t));   // lane 2 jj
             const uint32_t oj = min(inst0 + jj, n - 1) - inst0;   // ring within the wave's descriptor
             const uint32_t pos = wrap48k((int64_t)t + rel + 2 * (int)m);
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v2(FxRackArgs a) {
     auto stage_window = [&]() {
 #pragma unroll
         for (int r = 0; r < 5; ++r) {
-            const uint32_t P = (uint32_t)r * 64u + lane, jj = P / 10u, m = P % 10u;
+            const uint32_t jj = piece_inst(r), m = piece_idx(r);
             float *p = win + 2u * m * 64u + 2u * jj;
             *(float2 *)p = make_float2(v[r].x, v[r].y);
             *(float2 *)(p + 64) = make_float2(v[r].z, v[r].w);
