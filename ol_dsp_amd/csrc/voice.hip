@@ -129,7 +129,10 @@ struct Env {
     }
 };
 
-constexpr int kVcChunk = 16;        // samples per hand-off between the roles
+// samples per hand-off between the roles: 8 (34 barrier steps per 256-frame block, pipeline fill
+// 2 of them) measured 2 % faster than 16 (18 steps) for the Svf voice and equal for the Moog
+// voice; 32 halves the workgroups per CU (96 KB of LDS each) and is 1.7x slower
+constexpr int kVcChunk = 8;
 
 // Runs f(j) for the m samples of a chunk: unrolled when the chunk is full, so the off-recurrence
 // work of neighbouring samples interleaves (ILP for a wave that is alone on its SIMD).
@@ -144,7 +147,7 @@ __device__ __forceinline__ void for_chunk(uint32_t m, F &&f) {
 }
 
 // voice_block_v4: the MoogFilter voice.  One workgroup = 64 voices, the voice pipelined over two
-// waves that hand each sample's values on through an LDS double buffer (one barrier per 16-sample
+// waves that hand each sample's values on through an LDS double buffer (one barrier per 8-sample
 // chunk):
 //   feed wave   : amp envelope, portamento, oscillator, filter envelope, cutoff,
 //                 LadderFilter::SetFreq -> SetAlpha          -> (src * drive, amp, alpha, Qadjust)
@@ -305,9 +308,9 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
 //   OSC  : Port, the oscillator's phase, the polyBLEP saw                     -> (src, amp)
 //   FREQ : Svf::SetFreq(fc_in)                                                -> (fq, damp)
 //   FILT : the two Svf passes, Low() * amp, the output store
-// A three-stage pipeline over 16-sample chunks: at step k ENV makes chunk k, OSC and FREQ chunk
-// k-1, FILT chunk k-2; one barrier per step; 48 KB of LDS per workgroup.  Measured per role
-// alone (the others skipping their arithmetic): the skeleton (launch, state,
+// A three-stage pipeline over 8-sample chunks (kVcChunk): at step k ENV makes chunk k, OSC and FREQ chunk
+// k-1, FILT chunk k-2; one barrier per step; 24 KB of LDS per workgroup.  Measured per role (16-sample chunks,
+// 18 steps; the others skipping their arithmetic): the skeleton (launch, state,
 // 18 barriers) 9.7 us, FREQ 10.0, FILT 15, OSC 20, ENV 26 of the kernel's 43.6 us.  The envelopes
 // of a full chunk run speculatively (Env::step_spec, no per-sample lane vote and branch) and the
 // chunk is redone exactly when a lane's segment ended in it.  Role = wave: rotating the roles of
