@@ -61,8 +61,20 @@ WORKLOADS = {
     "fxrack": ("fxrack", 65536, "SURVEY 8f row 1: fxlib FxRack<2> (delay -> reverb -> filter -> master), 65,536 instances"),
     "voice_poly": ("voice", 32768, "SURVEY 8a A17: configs[3] voices summed into Polyvoice buses of 8 voices "
                    "(olfx_mix) inside every step"),
+    "voice_events": ("voice", 32768, "configs[3] voices with note events every block: NoteOn for 2.5 % and NoteOff "
+                     "for 2.5 % of the voices (5 %), SynthVoice.h:245-256, applied at the block start"),
+    "chain_cc": ("chain", 16384, "configs[4]'s per-GPU shard with a control change every block: one parameter of "
+                 "1 % of the chains (163 scattered instances) set before each block, as a MIDI CC fanned out "
+                 "to objects (olfx_set_param_list)"),
+    "dattorro_rpd": ("dattorro", 65536, "configs[2] with a random per-instance pre-delay (SURVEY 8d: 'a variant "
+                     "with random preDelay measures the gather path', verb.cpp:137-139)"),
+    "chain_rpd": ("chain", 65536, "north_star chains (65,536) with a random per-instance reverb pre-delay"),
 }
-DEFAULT_ALSO = "dattorro,chain_65536,chain,voice,fxrack"
+# parameter set of a workload (ol_dsp_amd.workload.RANGES key) where it is not the kind's own
+PARAM_SET = {"dattorro_rpd": "dattorro_rpd", "chain_rpd": "chain_rpd"}
+# the event-free workload a control leg is compared with (same kind and instances)
+EVENT_FREE = {"voice_events": "voice", "chain_cc": "chain"}
+DEFAULT_ALSO = "dattorro,chain_65536,chain,voice,voice_moog,fxrack,voice_events,chain_cc,dattorro_rpd,chain_rpd"
 
 
 def parse():
@@ -110,10 +122,10 @@ def host_facts() -> dict:
     return {"nproc": nproc, "host_cpus": os.cpu_count(), "cpu_model": model}
 
 
-def _cpu_bank(kind: str, n: int, sr: float, o0: bool, ref: bool):
+def _cpu_bank(kind: str, n: int, sr: float, o0: bool, ref: bool, pset: str = ""):
     import oracle as O
     from ol_dsp_amd.workload import instance_params, voice_notes
-    p = instance_params(kind, 0, n)
+    p = instance_params(pset or kind, 0, n)
     if kind == "dattorro":
         bank = O.Dattorro(n, ref=ref, o0=o0)
         for i in range(n):
@@ -151,7 +163,7 @@ def _cpu_bank(kind: str, n: int, sr: float, o0: bool, ref: bool):
     return lambda x, t: d.process(c2.process(c1.process(x, t), t), t), (c1, c2, d)
 
 
-def cpu_baseline(kind: str, block: int, sr: float, budget_s: float, threads: int) -> dict:
+def cpu_baseline(kind: str, block: int, sr: float, budget_s: float, threads: int, pset: str = "") -> dict:
     """Time the CPU oracle (or, for the reverb, the reference verb.cpp compiled here) on a bounded
     sample of the same workload: the same global instances 0..n-1 with the same parameters and
     input streams, 256-frame blocks, OpenMP schedule(static) over instances, until the wall
@@ -165,7 +177,7 @@ def cpu_baseline(kind: str, block: int, sr: float, budget_s: float, threads: int
     ref = kind in ("dattorro", "chain") and O.ref_available() and O.ref_available(o0=True)
 
     def timed(o0: bool, budget: float):
-        step, _keep = _cpu_bank(kind, n, sr, o0, ref)
+        step, _keep = _cpu_bank(kind, n, sr, o0, ref, pset)
         step(x, threads)  # warm
         t0 = time.perf_counter()
         blocks = 0
@@ -239,7 +251,8 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
     first, n = shard(total, world, rank)
     B = args.block
     eng = ofx.Engine(kind, n, sample_rate=args.sample_rate, block=B, device=dev.index or 0)
-    eng.set_params(0, instance_params(kind, first, n))
+    pset = PARAM_SET.get(name, kind)
+    eng.set_params(0, instance_params(pset, first, n))
     ich, och = eng.info.in_channels, eng.info.out_channels
 
     # input pool: distinct synthetic blocks of each global instance's own stream, on the device
@@ -253,6 +266,29 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
     if voice:   # NoteOn for every voice at block 0, NoteOff at the middle of the timed blocks
         eng.note_events(eng.make_events(np.arange(n), 1, notes))
         note_off = eng.make_events(np.arange(n), 0, notes)
+    # control legs: the per-step calls are prebuilt (untimed), so a step is the library call only
+    step_events = None
+    if name == "voice_events":     # voices i % 40 == k % 40 get NoteOn, i % 40 == (k + 20) % 40 NoteOff
+        gi = np.arange(first, first + n)
+        step_events = []
+        for k in range(40):
+            on = np.nonzero(gi % 40 == k)[0]
+            off = np.nonzero(gi % 40 == (k + 20) % 40)[0]
+            ev_on = eng.make_events(on, 1, (notes[on] + 12 * (k & 1)) % 128)
+            ev_off = eng.make_events(off, 0, notes[off])
+            step_events.append(np.concatenate([ev_on, ev_off]))
+    step_ccs = None
+    if name == "chain_cc":         # chains i % 100 == k % 100 get a new value of one field per step
+        from ol_dsp_amd.workload import uniform01
+        gi = np.arange(first, first + n)
+        fields = [("chorus_depth", .08, 1.0), ("chorus_mix", 0.0, 1.0), ("verb_decay", .25, .95),
+                  ("verb_damping", .05, .95), ("pitch_shift", 0.0, 3.0)]
+        step_ccs = []
+        for k in range(100):
+            sel = np.nonzero(gi % 100 == k)[0].astype(np.uint32)
+            fname, lo, hi = fields[k % len(fields)]
+            vals = (lo + (hi - lo) * uniform01(7, k, int(first), n)[sel]).astype(np.float32)
+            step_ccs.append((eng.field(fname), sel, vals))
     bus = None
     if name == "voice_poly":       # Polyvoice buses of 8 voices (Polyvoice.h:28-33)
         eng.mix_config([list(range(g, min(g + 8, n))) for g in range(0, n, 8)])
@@ -260,17 +296,46 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
     stream = torch.cuda.Stream(dev)        # dedicated non-default stream: events see the kernels
     torch.cuda.synchronize(dev)
     K, W = args.steps, args.warmup
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-    evm = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)] if bus is not None else None
+    # Kernel timing: ONE event pair on the launch stream around the K timed steps: GPU time per
+    # step = the kernel's average launch duration plus the gap between launches.  (A pair per step
+    # adds two timestamp markers between consecutive kernels -- ~3-4 us each on the command
+    # processor, 10-20 % of a 35 us voice block, measured: tools/loop_probe.py.)  Only voice_poly,
+    # whose steps run two kernels, times each kernel with its own pair.
+    per_step = bus is not None
+    region = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)] if per_step else None
+    evm = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)] if per_step else None
+
+    # The timed loop calls the C-ABI directly with prebuilt arguments (Engine.process's checks and
+    # tensor handling cost ~20 us of Python per call, more than a voice block's kernel): the host
+    # must stay ahead of the GPU, or the event pairs below would time the host's launch latency.
+    import ctypes
+
+    from ol_dsp_amd import _lib
+    lib, h = eng.lib, eng.handle
+    c_stream = ctypes.c_void_p(stream.cuda_stream)
+    c_out = ctypes.c_void_p(out.data_ptr())
+    proc_args = [(h, ctypes.c_void_p(p.data_ptr() if p is not None else 0), c_out, B, _lib.IO_DEVICE, c_stream)
+                 for p in pool]
+    ev_args = [(h, e_.ctypes.data_as(ctypes.POINTER(_lib.Event)), len(e_)) for e_ in step_events or []]
+    cc_args = [(h, f, sel.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                vals.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), len(sel)) for f, sel, vals in step_ccs or []]
 
     def step(k, t=None):
+        rc = 0
         if voice and k == W + K // 2:
             eng.note_events(note_off)
-        if t is not None:
+        if ev_args:
+            rc |= lib.olfx_note_events(*ev_args[k % 40])
+        if cc_args:
+            rc |= lib.olfx_set_param_list(*cc_args[k % 100])
+        if t is not None and per_step:
             ev[t][0].record(stream)
-        eng.process(pool[k % pool_n], out=out, n_frames=B, stream=stream.cuda_stream)
-        if t is not None:
+        rc |= lib.olfx_process(*proc_args[k % pool_n])
+        if t is not None and per_step:
             ev[t][1].record(stream)
+        if rc:
+            _lib.check(rc, h)
         if bus is not None:
             if t is not None:
                 evm[t][0].record(stream)
@@ -285,14 +350,16 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    region[0].record(stream)
     for k in range(K):
         step(W + k, k)
+    region[1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if per_step else region[0].elapsed_time(region[1]) / K
     mix_ms = float(np.mean([a.elapsed_time(b) for a, b in evm])) if evm else None
 
     # sum |y| over the finite outputs of the last block (a voice whose Svf diverges -- possible in
@@ -325,18 +392,20 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
         if rd:
             measured.update({"traffic_read": rd, "hbm_read_gbs_measured": rd / (kern_ms * 1e-3) / 1e9,
                              "frac_read_measured": rd / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS})
+    timing = ("HIP event pair per step around olfx_process" if per_step else
+              "one HIP event pair on the launch stream around the K timed steps / K (launch duration + launch gap)")
     if voice:
         fps = VOICE_MOOG_FLOPS_PER_SAMPLE if kind == "voice_moog" else VOICE_FLOPS_PER_SAMPLE
         tflops = fps * per_launch / (kern_ms * 1e-3) / 1e12
         roofline = {"bound": "valu", "achieved": tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,
-                    "kernel": kname, "kernel_ms": kern_ms, "algorithmic_flops_per_frame": fps,
+                    "kernel": kname, "kernel_ms": kern_ms, "kernel_timing": timing, "algorithmic_flops_per_frame": fps,
                     "algorithmic_bytes_per_frame": bpf, "hbm_gbs": achieved, "frames_per_launch": per_launch}
     else:
         roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                     "achieved_read": achieved_r, "frac_read": achieved_r / HBM_PEAK_GBS,
-                    "kernel": kname, "kernel_ms": kern_ms,
+                    "kernel": kname, "kernel_ms": kern_ms, "kernel_timing": timing,
                     "algorithmic_bytes_per_frame": bpf, "algorithmic_read_bytes_per_frame": rbpf,
                     "frames_per_launch": per_launch, **measured}
     res = {"metric": METRIC, "value": frames / elapsed,
@@ -354,9 +423,18 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
                       "achieved": mix_bytes / (mix_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                       "frac": mix_bytes / (mix_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                       "algorithmic_bytes_per_launch": mix_bytes, "bus_checksum_rank0": bus_sum}
+    if step_events is not None:
+        res["control"] = {"events_per_block": int(np.mean([len(e) for e in step_events])),
+                          "note": "NoteOn/NoteOff folded per voice on the host and applied by the voice kernel at "
+                                  "the block start (olfx_engine.cpp fold_events, voice.hip voice_event)"}
+    if step_ccs is not None:
+        res["control"] = {"instances_changed_per_block": int(np.mean([len(c[1]) for c in step_ccs])),
+                          "note": "changed coefficients re-derived on the host for those instances only and "
+                                  "scattered on the device ahead of the block (control.hip coef_scatter)"}
     if with_cpu and world == 1 and args.cpu_seconds > 0:
         threads = args.cpu_threads or host_facts()["nproc"]
-        res["cpu_baseline"] = cpu_baseline(kind, B, args.sample_rate, args.cpu_seconds, threads)
+        res["cpu_baseline"] = cpu_baseline(kind, B, args.sample_rate, args.cpu_seconds, threads,
+                                           PARAM_SET.get(name, ""))
     else:
         res["cpu_baseline"] = None
     return res
@@ -380,11 +458,25 @@ def main():
     also = args.also if args.also is not None else (DEFAULT_ALSO if args.workload == "chorus" else "")
     also_res = {}
     for name in [a for a in also.split(",") if a]:
-        r = run_workload(name, WORKLOADS[name][1], args, rank, world, dev, with_cpu=True)
+        twin = EVENT_FREE.get(name)
+        tkey = twin if twin != "chain" else "chain_16384"
+        # a control leg's CPU work per block is its twin's (the CPU oracle applies events and
+        # parameters per instance at block boundaries): the twin's measured baseline is reused
+        r = run_workload(name, WORKLOADS[name][1], args, rank, world, dev, with_cpu=not (twin and tkey in also_res))
+        if rank == 0 and twin and tkey in also_res and also_res[tkey].get("cpu_baseline"):
+            r["cpu_baseline"] = dict(also_res[tkey]["cpu_baseline"], reused_from=tkey)
         if rank == 0:
             key = name if name != "chain" else "chain_16384"
-            also_res[key] = {k: r[k] for k in ("value", "unit", "ms_per_step", "config", "roofline",
+            also_res[key] = {k: r[k] for k in ("value", "unit", "ms_per_step", "config", "roofline", "control",
                                                 "cpu_baseline", "output_checksum", "output_nonfinite_rank0") if k in r}
+            base = EVENT_FREE.get(name)
+            bkey = base if base != "chain" else "chain_16384"
+            if base and bkey in also_res:   # the control leg's cost against its event-free twin
+                b = also_res[bkey]
+                also_res[key]["control"].update({
+                    "event_free_kernel_ms": b["roofline"]["kernel_ms"], "event_free_ms_per_step": b["ms_per_step"],
+                    "kernel_ms_ratio": r["roofline"]["kernel_ms"] / b["roofline"]["kernel_ms"],
+                    "ms_per_step_ratio": r["ms_per_step"] / b["ms_per_step"]})
 
     if rank == 0:
         res = {

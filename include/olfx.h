@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define OLFX_ABI_VERSION 1
+#define OLFX_ABI_VERSION 2
 
 /* ---- status codes ---- */
 enum {
@@ -126,7 +126,19 @@ enum {
                                     1: the Daisy synth firmware's audio callback (ol_daisy/app/synth/main.cpp:
                                     78-86): DelayFx<1> on channel 0 -> stereo[0] = stereo[1] -> ReverbFx<2>
                                     -> FilterFx<2> in place (channel 1 keeps the reverb's output), no master
-                                    volume (MASTER_VOLUME ignored).  Input: the mono signal in channel 0. */
+                                    volume (MASTER_VOLUME ignored).  Input: the mono signal in channel 0.
+                                    Controls (olfx_control) follow the firmware too (main.cpp:201-207): the
+                                    voice-filter CCs 41-44 drive FILTER_*, CCs 45-48 and 7 are ignored.
+                                    2, 3, 4: one component alone, as the firmware's objects (main.cpp:82-85):
+                                    2 DelayFx<2>::Process (Fx.h:193-206; DELAY_* fields; channel 0 filtered
+                                      by its filter_, channel 1 not; DelayFx<1> = channel 0);
+                                    3 ReverbFx<2>::Process over the ReverbSc stub (Fx.h:293-299; REVERB_BALANCE):
+                                      per channel 0.8 in balance + in (1 - balance);
+                                    4 FilterFx<2>::Process (Fx.h:88-108; FILTER_*): the Svf on channel 0, and
+                                      channel 1 passes through (the reference leaves frame_out[1] unwritten:
+                                      in place, as the firmware calls it, that is channel 1 of the input).
+                                    olfx_control gives each its own controls only (DelayFx 35-39, ReverbFx 34,
+                                    FilterFx 41-44).  One engine may mix every topology. */
     OLFX_FR_NPARAMS
 };
 /* Chain: chorus params, then pitch-shift params, then dattorro params */
@@ -166,7 +178,9 @@ typedef struct olfx_voice_event {
    mapped to one parameter field, per kind:
      OLFX_KIND_VOICE : SynthVoice::UpdateMidiControl / UpdateHardwareControl (SynthVoice.h:100-229)
      OLFX_KIND_FXRACK: FxRack::UpdateMidiControl / UpdateHardwareControl (Fx.h:451-489) and the
-                       DelayFx / ReverbFx / FilterFx handlers it forwards to (Fx.h:116-163, 218-267, 313-391)
+                       DelayFx / ReverbFx / FilterFx handlers it forwards to (Fx.h:116-163, 218-267, 313-391);
+                       olfx_control_map gives topology 0's mapping, olfx_control uses each instance's
+                       topology (OLFX_FR_TOPOLOGY 1: the firmware's direct FilterFx routing)
    Controls the reference ignores for a kind (its `default: update = false`) are skipped. */
 enum { OLFX_CTL_MIDI = 0, OLFX_CTL_HARDWARE = 1 };
 #define OLFX_IGNORED 1                 /* olfx_control_map: the reference ignores this control */
@@ -215,6 +229,19 @@ int olfx_set_params(olfx_engine *e, uint32_t first, uint32_t count, uint32_t fie
                     uint32_t n_fields, const float *values);
 /* Convenience: one field of one instance. */
 int olfx_set_param(olfx_engine *e, uint32_t inst, uint32_t field, float value);
+/* One field of `count` scattered instances: inst[k] gets values[k] (the per-instance setter called
+   on each, e.g. one MIDI CC fanned out to many objects).  Validated first: a rejected call changes
+   nothing.  Applied at the start of the next olfx_process, like every parameter change; the
+   engine re-derives and uploads the coefficients of changed instances only, asynchronously. */
+int olfx_set_param_list(olfx_engine *e, uint32_t field, const uint32_t *inst, const float *values,
+                        uint32_t count);
+/* A member value without Update(): the state the reference's setters leave when they are called
+   BEFORE Init (the Daisy firmware configures its voices that way, ol_daisy/app/synth/main.cpp:114-128
+   then :149).  For voices, SynthVoice::Init resets the components to DaisySP's defaults, while
+   Process keeps reading the members filter_cutoff, filter_env_amount, amp_env_amount and Init hands
+   portamento_htime to the Port (SynthVoice.h:31-53): the field is stored without the Update() that
+   olfx_set_params implies.  For the other kinds it is olfx_set_param. */
+int olfx_set_member(olfx_engine *e, uint32_t inst, uint32_t field, float value);
 /* Read back the current (host shadow) value of one parameter. */
 int olfx_get_param(olfx_engine *e, uint32_t inst, uint32_t field, float *value);
 

@@ -269,6 +269,9 @@ protected:
         check(olfx_sample_voice_event(need(), type, midi_note, velocity, value), nullptr, "olfx_sample_voice_event");
     }
     void update() { check(olfx_sample_update(need()), nullptr, "olfx_sample_update"); }
+    void set_member(uint32_t field, float value) {
+        check(olfx_sample_set_member(need(), field, value), nullptr, "olfx_sample_set_member");
+    }
     bool live() const { return s_ != nullptr; }
 
 private:

@@ -35,15 +35,18 @@
  * across the instances of a generation.  Errors throw olfx::Error (the reference returns void).
  * Gate() and Playing() are host-side and change at the call, as SynthVoice.h:231-262 does.
  *
- * FxRack's components are not DSP objects of their own here: FxRack<2>::Init binds them to one
- * GPU rack instance, and their controls (before or after Init) reach that instance.  A component
- * processed outside a rack (Process on an unbound DelayFx / ReverbFx / FilterFx) throws
- * OLFX_E_STATE: no standalone kernel exists for them.
+ * FxRack's components: inside an FxRack<2>, FxRack::Init binds them to the rack's GPU instance and
+ * their controls (before or after Init) reach it.  On their own -- the Daisy synth firmware's
+ * delay_fx -> stereo copy -> reverb_fx -> filter_fx callback (ol_daisy/app/synth/main.cpp:78-88) --
+ * Init gives each a GPU rack instance whose topology is the component alone (OLFX_FR_TOPOLOGY
+ * 2 DelayFx, 3 ReverbFx, 4 FilterFx), so that callback compiles and runs unchanged; a chain of k
+ * such objects is k blocks late (each object one block).
  */
 #ifndef OLFX_REF_HPP
 #define OLFX_REF_HPP
 
 #include <cstdint>
+#include <memory>
 #include <vector>
 
 #include "olfx_fx.hpp"
@@ -148,17 +151,22 @@ public:
                         Portamento *portamento = nullptr)
         : kind_(pick_kind(sound_source, filter, filter_envelope, amp_envelope, portamento)) {}
 
+    /* SynthVoice::Init (SynthVoice.h:31-39).  Members set before it (the Daisy firmware's order,
+       ol_daisy/app/synth/main.cpp:114-128 then :149) keep their values; the components start at
+       DaisySP's defaults, as Init leaves them (olfx_set_member). */
     void Init(t_sample sample_rate) override {
         create(kind_, sample_rate);
+        for (uint32_t f = 0; f < OLFX_VC_NPARAMS; ++f)
+            if (pre_set_[f]) set_member(f, pre_[f]);
         playing_ = 0;
         gate_ = false;
     }
-    void Update() override { update(); }
-    void Process(t_sample *frame_out) override { frame(nullptr, frame_out); }
-    void UpdateMidiControl(uint8_t control_, uint8_t value) override { control(control_, OLFX_CTL_MIDI, value); }
-    void UpdateHardwareControl(uint8_t control_, t_sample value) override {
-        control(control_, OLFX_CTL_HARDWARE, value);
+    void Update() override {
+        if (live()) update();   /* before Init: Init resets the components anyway */
     }
+    void Process(t_sample *frame_out) override { frame(nullptr, frame_out); }
+    void UpdateMidiControl(uint8_t control_, uint8_t value) override { ctl(control_, OLFX_CTL_MIDI, value); }
+    void UpdateHardwareControl(uint8_t control_, t_sample value) override { ctl(control_, OLFX_CTL_HARDWARE, value); }
     /* copies the 16 members, then Update() (SynthVoice.h:55-76) */
     void UpdateConfig(Config &config) override {
         static constexpr t_sample Config::*kFields[OLFX_VC_NPARAMS] = {
@@ -166,6 +174,10 @@ public:
             &Config::filter_attack, &Config::filter_attack_shape, &Config::filter_decay, &Config::filter_sustain,
             &Config::filter_release, &Config::amp_env_amount, &Config::amp_attack, &Config::amp_attack_shape,
             &Config::amp_decay, &Config::amp_sustain, &Config::amp_release, &Config::portamento};
+        if (!live()) {
+            for (uint32_t f = 0; f < OLFX_VC_NPARAMS; ++f) { pre_[f] = config.*kFields[f]; pre_set_[f] = true; }
+            return;
+        }
         for (uint32_t f = 0; f < OLFX_VC_NPARAMS; ++f) set(f, config.*kFields[f]);
         update();
     }
@@ -205,9 +217,23 @@ private:
         if (dynamic_cast<MoogFilter *>(filter)) return OLFX_KIND_VOICE_MOOG;
         throw olfx::Error(OLFX_E_KIND, "SynthVoice: only SvfFilter / MoogFilter run on the GPU voice kernel");
     }
+    /* a control before Init: the member it sets (SynthVoice::UpdateMidiControl's mapping,
+       olfx_control_map), applied at Init without Update() */
+    void ctl(uint8_t control_, int source, float value) {
+        if (live()) return control(control_, source, value);
+        uint32_t field;
+        float v;
+        const int rc = olfx_control_map(kind_, control_, source, value, &field, &v);
+        if (rc == OLFX_IGNORED || (rc == OLFX_OK && field == OLFX_FIELD_UPDATE_ONLY)) return;
+        if (rc != OLFX_OK) throw olfx::Error(rc, "SynthVoice control before Init");
+        pre_[field] = v;
+        pre_set_[field] = true;
+    }
     int kind_;
     uint8_t playing_ = 0;
     bool gate_ = false;
+    float pre_[OLFX_VC_NPARAMS] = {};
+    bool pre_set_[OLFX_VC_NPARAMS] = {};
 };
 
 }  // namespace ol::synth
@@ -223,36 +249,69 @@ public:
     void Control(uint8_t cc, int source, float value) { control(cc, source, value); }
 };
 
-/* A rack component: its controls go to the rack instance it is bound to; controls given before
-   the rack's Init are kept and replayed, in order, when it binds (the rack's state at Init equals
-   the reference components' state at that point). */
+/* A rack component.  Inside an FxRack<2> (FxRack::Init binds it) its controls go to the rack's
+   instance; on its own -- the Daisy synth firmware's delay_fx / reverb_fx / filter_fx
+   (ol_daisy/app/synth/main.cpp:55-67, 82-85) -- Init gives it a GPU rack instance of its own whose
+   topology is the component alone (OLFX_FR_TOPOLOGY 2 / 3 / 4).  Controls given before either
+   exists are kept and replayed, in order, when it does; a component that an FxRack binds after
+   its own Init hands its instance over (the rack gets every control so far). */
 class RackComponent {
 public:
-    RackComponent() = default;
+    explicit RackComponent(int topology) : topology_(topology) {}
     RackComponent(const RackComponent &) = delete;
     RackComponent &operator=(const RackComponent &) = delete;
+    virtual ~RackComponent() = default;
 
     void bind(RackInstance *rack) {
+        own_.reset();                               /* a rack member has no instance of its own */
         rack_ = rack;
-        for (const Ctl &c : queued_) rack_->Control(c.cc, c.source, c.value);
-        queued_.clear();
+        for (const Ctl &c : history_) deliver(c);   /* every control so far, in order */
+        history_.clear();
     }
     void unbind(RackInstance *rack) { if (rack_ == rack) rack_ = nullptr; }
 
 protected:
+    /* Init outside a rack: the component's own instance (a rack member keeps the rack's) */
+    void init_alone(float sample_rate) {
+        if (rack_) return;
+        own_.reset(new RackInstance());
+        own_->Init(sample_rate);
+        own_->set(OLFX_FR_TOPOLOGY, (float)topology_);
+        for (const Ctl &c : history_) deliver(c);
+    }
+    /* one frame of the component alone: [2] in, [2] out, one block late */
+    void process_alone(const float in[2], float out[2]) {
+        if (rack_) throw olfx::Error(OLFX_E_STATE, "component of an FxRack: FxRack::Process runs it");
+        if (!own_) throw olfx::Error(OLFX_E_STATE, "component used before Init");
+        if (!processed_) history_.clear();          /* it runs alone from now on: no replay needed */
+        processed_ = true;
+        own_->Process(in, out);
+    }
     void send(uint8_t cc, int source, float value) {
-        if (rack_) rack_->Control(cc, source, value);
-        else queued_.push_back(Ctl{cc, source, value});
+        const Ctl c{cc, source, value};
+        if (rack_ || own_) deliver(c);
+        /* kept for an FxRack that may bind it later (until it has run alone) */
+        if (!rack_ && !processed_) history_.push_back(c);
     }
-    [[noreturn]] static void standalone(const char *what) {
-        throw olfx::Error(OLFX_E_STATE, std::string(what) + ": only inside an FxRack<2> (FxRack::Init binds it); "
-                                        "there is no standalone GPU kernel for it");
-    }
-    RackInstance *rack_ = nullptr;
+    /* the control's number at the rack's own map (FxRack forwards CC_FX_FILTER_* to its filter1 as
+       CC_FILTER_*, Fx.h:451-470); 0 = no rack member takes it.  A component alone keeps its own
+       numbers (the engine routes them by topology, olfx_control). */
+    virtual uint8_t rack_cc(uint8_t cc) const { return cc; }
 
 private:
     struct Ctl { uint8_t cc; int source; float value; };
-    std::vector<Ctl> queued_;
+    void deliver(const Ctl &c) {
+        if (rack_) {
+            if (const uint8_t rc = rack_cc(c.cc)) rack_->Control(rc, c.source, c.value);
+        } else {
+            own_->Control(c.cc, c.source, c.value);
+        }
+    }
+    int topology_;
+    bool processed_ = false;
+    RackInstance *rack_ = nullptr;
+    std::unique_ptr<RackInstance> own_;
+    std::vector<Ctl> history_;
 };
 
 /* cc_map.h numbers (modules/corelib/cc_map.h:8-67) */
@@ -264,42 +323,65 @@ enum : uint8_t {
     kEarlyPredelay = 50, kReverbPredelay = 52, kReverbPrefilter = 53, kReverbInputDiffusion1 = 54,
     kReverbInputDiffusion2 = 55, kReverbDecayDiffusion = 56,
 };
+
+/* frame_in / frame_out of a CHANNEL_COUNT-channel component on the stereo instance */
+template <int CH>
+inline void to_stereo(const t_sample *in, float x[2], bool dup) { x[0] = in[0]; x[1] = CH > 1 ? in[1] : (dup ? in[0] : 0.f); }
 }  // namespace detail
 
-/* Fx.h:65-165.  As the rack's filter1: CC_FILTER_* map to the rack's CC_FX_FILTER_* (Fx.h:451-462). */
+/* Fx.h:65-165: the Svf on channel 0 with the selected output (FilterFx::Process, Fx.h:88-108).  In an
+   FxRack<2> it is filter1: CC_FILTER_* map to the rack's CC_FX_FILTER_* (Fx.h:451-462).  Alone
+   (OLFX_FR_TOPOLOGY 4), channel 1 of frame_out is channel 1 of frame_in one block late: the reference
+   leaves frame_out[1] unwritten, which in place -- the firmware's call -- keeps channel 1 of the input. */
 template <int CHANNEL_COUNT>
 class FilterFx : public detail::RackComponent {
 public:
-    void Init(t_sample) {}
+    FilterFx() : RackComponent(4) {}
+    void Init(t_sample sample_rate) { init_alone(sample_rate); }
     void Update() {}
-    void Process(const t_sample *, t_sample *) { standalone("FilterFx::Process"); }
+    void Process(const t_sample *frame_in, t_sample *frame_out) {
+        float x[2], y[2];
+        detail::to_stereo<CHANNEL_COUNT>(frame_in, x, false);
+        process_alone(x, y);
+        for (int c = 0; c < CHANNEL_COUNT; ++c) frame_out[c] = y[c];
+    }
     void UpdateMidiControl(uint8_t control, uint8_t value) { route(control, OLFX_CTL_MIDI, value); }
     void UpdateHardwareControl(uint8_t control, t_sample value) { route(control, OLFX_CTL_HARDWARE, value); }
 
 private:
     void route(uint8_t control, int source, float value) {
-        using namespace detail;
-        switch (control) {
-        case kFilterCutoff: send(kFxFilterCutoff, source, value); break;
-        case kFilterResonance: send(kFxFilterResonance, source, value); break;
-        case kFilterDrive: send(kFxFilterDrive, source, value); break;
-        case kFilterType: send(kFxFilterType, source, value); break;
-        default: break;                                 /* ignored (Fx.h:131-133) */
-        }
+        if (control >= detail::kFilterCutoff && control <= detail::kFilterDrive) send(control, source, value);
+        /* anything else: ignored (Fx.h:131-133) */
     }
+    uint8_t rack_cc(uint8_t cc) const override { return (uint8_t)(cc - detail::kFilterCutoff + detail::kFxFilterCutoff); }
 };
 
-/* Fx.h:168-268.  The delay lines are the GPU rack's ([n][48000][2] rings): the constructor takes the
-   reference's `std::vector<daisysp::DelayLine<t_sample, MAX_DELAY> *> &` (any type) and ignores it. */
+/* Fx.h:168-268.  The delay lines are the GPU instance's ([n][48000][2] rings): the constructor takes
+   the reference's `std::vector<daisysp::DelayLine<t_sample, MAX_DELAY> *> &` (any type) and ignores
+   it.  Alone (OLFX_FR_TOPOLOGY 2) it is DelayFx<2>: channel 0 through its filter_, channel 1 not;
+   DelayFx<1> is channel 0 of it. */
 template <int CHANNEL_COUNT>
 class DelayFx : public detail::RackComponent {
 public:
-    DelayFx() = default;
+    DelayFx() : RackComponent(2) {}
     template <class DelayLines>
-    explicit DelayFx(DelayLines &) {}
-    void Init(t_sample) {}
+    explicit DelayFx(DelayLines &) : RackComponent(2) {}
+    /* DelayFx::Init (Fx.h:183-192): its filter_ at UpdateMidiControl(CC_FILTER_CUTOFF, 64) and
+       (CC_FILTER_RESONANCE, 24) -- the rack's delay cutoff / resonance fields -- after any earlier
+       control.  (Called again after processing started, it re-applies those settings; the delay
+       lines keep their contents.) */
+    void Init(t_sample sample_rate) {
+        init_alone(sample_rate);
+        send(detail::kDelayCutoff, OLFX_CTL_MIDI, 64.f);
+        send(detail::kDelayResonance, OLFX_CTL_MIDI, 24.f);
+    }
     void Update() {}
-    void Process(const t_sample *, t_sample *) { standalone("DelayFx::Process"); }
+    void Process(const t_sample *frame_in, t_sample *frame_out) {
+        float x[2], y[2];
+        detail::to_stereo<CHANNEL_COUNT>(frame_in, x, false);
+        process_alone(x, y);
+        for (int c = 0; c < CHANNEL_COUNT; ++c) frame_out[c] = y[c];
+    }
     void UpdateHardwareControl(uint8_t control, t_sample value) {   /* time / feedback / balance (Fx.h:220-240) */
         using namespace detail;
         if (control == kDelayTime || control == kDelayFeedback || control == kDelayBalance)
@@ -321,14 +403,21 @@ public:
 };
 
 /* Fx.h:270-393.  Of its members only `balance` reaches the output through the ReverbSc stub; the
-   others are accepted and have no audible effect, as in the reference. */
+   others are accepted and have no audible effect, as in the reference.  Alone (OLFX_FR_TOPOLOGY 3):
+   per channel 0.8 in balance + in (1 - balance); ReverbFx<1> (DaisyVerb<1> feeds the one channel to
+   both stub inputs, Reverb.h:82-91) is channel 0 of it. */
 template <int CHANNEL_COUNT>
 class ReverbFx : public detail::RackComponent {
 public:
-    explicit ReverbFx(DaisyVerb<CHANNEL_COUNT> &) {}
-    void Init(t_sample) {}
+    explicit ReverbFx(DaisyVerb<CHANNEL_COUNT> &) : RackComponent(3) {}
+    void Init(t_sample sample_rate) { init_alone(sample_rate); }
     void Update() {}
-    void Process(const t_sample *, t_sample *) { standalone("ReverbFx::Process"); }
+    void Process(const t_sample *frame_in, t_sample *frame_out) {
+        float x[2], y[2];
+        detail::to_stereo<CHANNEL_COUNT>(frame_in, x, true);
+        process_alone(x, y);
+        for (int c = 0; c < CHANNEL_COUNT; ++c) frame_out[c] = y[c];
+    }
     void UpdateMidiControl(uint8_t control, uint8_t value) { route(control, OLFX_CTL_MIDI, value); }
     void UpdateHardwareControl(uint8_t control, t_sample value) { route(control, OLFX_CTL_HARDWARE, value); }
 

@@ -47,6 +47,8 @@ int olfx_sample_destroy(olfx_sample *s);
 /* Per-instance parameter (OLFX_DT_* / OLFX_CH_* / OLFX_VC_* / OLFX_FR_* field and value, as
    olfx_set_param), note event (voices) and control change (as olfx_control). */
 int olfx_sample_set_param(olfx_sample *s, uint32_t field, float value);
+/* A member value without Update() (olfx_set_member: setters called before the reference's Init). */
+int olfx_sample_set_member(olfx_sample *s, uint32_t field, float value);
 int olfx_sample_note(olfx_sample *s, uint8_t type, uint8_t note, uint8_t velocity);
 /* Any voice event (olfx_voice_event: GateOn / GateOff / SetFrequency as well) and Update(). */
 int olfx_sample_voice_event(olfx_sample *s, uint8_t type, uint8_t note, uint8_t velocity, float value);

@@ -105,6 +105,8 @@ SIGNATURES = {
     "olfx_reset": (ctypes.c_int, [_P]),
     "olfx_set_params": (ctypes.c_int, [_P, _U32, _U32, _U32, _U32, ctypes.POINTER(_F)]),
     "olfx_set_param": (ctypes.c_int, [_P, _U32, _U32, _F]),
+    "olfx_set_member": (ctypes.c_int, [_P, _U32, _U32, _F]),
+    "olfx_set_param_list": (ctypes.c_int, [_P, _U32, ctypes.POINTER(_U32), ctypes.POINTER(_F), _U32]),
     "olfx_get_param": (ctypes.c_int, [_P, _U32, _U32, ctypes.POINTER(_F)]),
     "olfx_note_events": (ctypes.c_int, [_P, ctypes.POINTER(Event), _U32]),
     "olfx_voice_events": (ctypes.c_int, [_P, ctypes.POINTER(VoiceEvent), _U32]),
@@ -130,6 +132,7 @@ SIGNATURES = {
     "olfx_sample_create": (ctypes.c_int, [ctypes.c_int, _F, ctypes.POINTER(_P)]),
     "olfx_sample_destroy": (ctypes.c_int, [_P]),
     "olfx_sample_set_param": (ctypes.c_int, [_P, _U32, _F]),
+    "olfx_sample_set_member": (ctypes.c_int, [_P, _U32, _F]),
     "olfx_sample_note": (ctypes.c_int, [_P, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
     "olfx_sample_voice_event": (ctypes.c_int, [_P, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, _F]),
     "olfx_sample_update": (ctypes.c_int, [_P]),

@@ -186,14 +186,11 @@ hipError_t launch_chain(const ChainArgs &a, hipStream_t s) {
     if ((a.n_frames & 3u) || (a.c1.t0 & 3u) || (a.d.t0 & 3u) || a.d.n < ((a.n + 63u) & ~63u)) return hipErrorInvalidValue;
     if ((uint64_t)a.n * 2 * a.c1.csize * 4 >= (1ull << 32) || (a.plane + (uint64_t)a.n_frames * a.n) * 4 >= (1ull << 32))
         return hipErrorInvalidValue;
-    // one workgroup per CU (LDS and registers allow no more), each running its groups back to back
-    static int cus[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return hipErrorInvalidDevice;
+    // one workgroup per CU (LDS and registers allow no more), each running its groups back to back;
+    // the CU count is the engine's (olfx_create), so concurrent engines share no launcher state
+    if (a.cus == 0) return hipErrorInvalidValue;
     const uint32_t groups = (a.n + 63u) / 64u;
-    const uint32_t blocks = groups < (uint32_t)cus[dev] ? groups : (uint32_t)cus[dev];
+    const uint32_t blocks = groups < a.cus ? groups : a.cus;
     hipLaunchKernelGGL(chain_block_v5, dim3(blocks), dim3(kChainThreads), (size_t)kChainLds * sizeof(float), s, a);
     return hipGetLastError();
 }

@@ -10,7 +10,8 @@
 // Topology 1 (OLFX_FR_TOPOLOGY, the Daisy synth firmware's callback, ol_daisy/app/synth/main.cpp:
 // 78-86): DelayFx<1> is the rack's channel-0 delay with its filter; stereo[0] = stereo[1] makes the
 // reverb's two outputs equal, FilterFx<2> in place leaves channel 1 at the reverb output, and there
-// is no master volume (x 1.0f).
+// is no master volume (x 1.0f).  Topologies 2 / 3 / 4 are DelayFx<2>, ReverbFx<2> and FilterFx<2> on
+// their own (the firmware's objects outside a rack; the COMP instantiation below).
 // DelayLine<float, 48000> (DaisySP, restated): read at delay D and D + 1, linear interpolation,
 // read before write.  Here the ring is time-forward (position = t mod 48000) and stereo-
 // interleaved [n][48000][2]: both channels share the delay, so one window load serves both.
@@ -80,6 +81,11 @@ __device__ __forceinline__ uint32_t wrap48k(int64_t p) {
 
 }  // namespace
 
+// COMP = some instance of the engine is a standalone component (OLFX_FR_TOPOLOGY 2 DelayFx<2>,
+// 3 ReverbFx<2>, 4 FilterFx<2>; the firmware's objects, ol_daisy/app/synth/main.cpp:82-85): the
+// same lanes and ticks, with per-instance selects of what each lane outputs.  Engines of racks only
+// (topologies 0 / 1) run COMP = false, the rack's own instruction stream.
+template <bool COMP>
 __global__ __launch_bounds__(kFrThreads) void fxrack_block_v2(FxRackArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const uint32_t tid = threadIdx.x;
@@ -108,7 +114,14 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v2(FxRackArgs a) {
     const float master = __uint_as_float(a.coef[FRC_MASTER * n + i]);
     // topology 1 (the synth firmware's callback): lane D's output is channel 1 = the reverb
     // output of the mono delay's stereo copy, which equals channel 0's reverb output b0
-    const bool fw = a.coef[FRC_TOPO * n + i] != 0u;
+    const uint32_t topo = a.coef[FRC_TOPO * n + i];
+    const bool fw = topo == 1u;
+    // components: lane F's channel-0 output is D's value of the previous frame for DelayFx and
+    // ReverbFx (no filter1); lane D's channel-1 output is F's value of the previous frame for all
+    // three.  filter1 (lane F's Svf) keeps its state only where it runs: racks and FilterFx.
+    const bool comp = COMP && topo >= 2u;
+    const bool pass0 = COMP && (topo == 2u || topo == 3u);
+    const bool filt_on = !COMP || !pass0;
     // Lane roles (v2): both filters act on channel 0 only (Fx.h:88-108, DelayFx filter_), so the
     // lane pair of an instance splits them: lane ch 0 ("D") runs DelayFx's filter_, lane ch 1 ("F")
     // runs FxRack's filter1 one tick behind, on D's reverb output of the previous frame (a DPP
@@ -212,6 +225,7 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v2(FxRackArgs a) {
         // ---- 3. the frames: C + 1 ticks; tick k runs frame k's delay line (both lanes, own
         //         channel) and one filter step per lane: D on frame k, F on frame k - 1 ----
         float b0p = 0.f;                                // F's input: D's b0 of the previous tick
+        float a1p = 0.f;                                // components: F's value of the previous tick
         auto tick = [&](auto generic_tag, auto k_tag) {
             constexpr bool GENERIC = decltype(generic_tag)::value;
             constexpr int k = decltype(k_tag)::value;
@@ -231,18 +245,36 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v2(FxRackArgs a) {
             float lo = slow, ba = sband;
             const float so = svf_tick(ch ? b0p : r, sfreq, sdamp, sdrive, stype, lo, ba);
             // D steps on frames 0..C-1, F on frames -1+1..C: the idle end of each lane keeps its state
-            const bool commit = ch ? k >= 1 : frame_k;
+            const bool commit = ch ? (k >= 1 && filt_on) : frame_k;
             slow = commit ? lo : slow;
             sband = commit ? ba : sband;
             // F: channel 0 of frame k-1; D: channel 1 (0, or in topology 1 frame k-1's b0)
-            if constexpr (k >= 1) o[k - 1] = (ch ? so : (fw ? b0p : 0.0f)) * master;
+            if constexpr (!COMP) {
+                if constexpr (k >= 1) o[k - 1] = (ch ? so : (fw ? b0p : 0.0f)) * master;
+            } else {
+                if constexpr (k >= 1)
+                    o[k - 1] = ch ? (pass0 ? b0p : so * master) : (comp ? a1p : (fw ? b0p : 0.0f)) * master;
+            }
             if (frame_k) {
-                // DelayFx: a = filtered * balance + in * (1 - balance) (D lane: channel 0)
-                const float a0 = (so * dbal) + (x[kk] * (1 - dbal));
-                // ReverbFx over the ReverbSc stub
-                const float vb = a0 * 0.8f;
-                const float b0 = (vb * rbal) + (a0 * (1 - rbal));
-                b0p = ch::pair_even(b0);
+                if constexpr (!COMP) {
+                    // DelayFx: a = filtered * balance + in * (1 - balance) (D lane: channel 0)
+                    const float a0 = (so * dbal) + (x[kk] * (1 - dbal));
+                    // ReverbFx over the ReverbSc stub
+                    const float vb = a0 * 0.8f;
+                    const float b0 = (vb * rbal) + (a0 * (1 - rbal));
+                    b0p = ch::pair_even(b0);
+                } else {
+                    // DelayFx's out = buf balance + in (1 - balance): D on its filtered read (channel 0),
+                    // F on its raw read (channel 1 has no filter, FilterFx acts on channel 0 only)
+                    const float da = ((ch ? r : so) * dbal) + (x[kk] * (1 - dbal));
+                    // ReverbFx over the stub: on the delay's output, or on the input when alone
+                    const float src = topo == 3u ? x[kk] : da;
+                    const float rv = ((src * 0.8f) * rbal) + (src * (1 - rbal));
+                    // D: the value lane F filters / outputs next tick; F: its channel-1 output
+                    const float val = topo == 2u ? da : (topo == 4u ? x[kk] : rv);
+                    b0p = ch::pair_even(val);
+                    a1p = ch::pair_odd(val);
+                }
             }
         };
         if (C == kFrChunk) static_for<kFrChunk + 1>([&](auto kt) { tick(std::false_type{}, kt); });
@@ -273,7 +305,8 @@ hipError_t launch_fxrack(const FxRackArgs &a, hipStream_t s) {
     const uint32_t waves = (a.n + 31) / 32;
     const uint32_t blocks = (waves + kFrThreads / 64 - 1) / (kFrThreads / 64);
     const size_t lds = (size_t)(kFrThreads / 64) * kFrRegion * sizeof(float);
-    hipLaunchKernelGGL(fxrack_block_v2, dim3(blocks), dim3(kFrThreads), lds, s, a);
+    if (a.components) hipLaunchKernelGGL(fxrack_block_v2<true>, dim3(blocks), dim3(kFrThreads), lds, s, a);
+    else hipLaunchKernelGGL(fxrack_block_v2<false>, dim3(blocks), dim3(kFrThreads), lds, s, a);
     return hipGetLastError();
 }
 

@@ -8,7 +8,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -280,9 +283,9 @@ void derive_fxrack(const float *p, float sr, uint32_t *c) {
     svf_coef(p[OLFX_FR_FILTER_CUTOFF], p[OLFX_FR_FILTER_RESONANCE], p[OLFX_FR_FILTER_DRIVE], sr, &f, &d, &dr);
     put(FRC_FFREQ, f); put(FRC_FDAMP, d); put(FRC_FDRIVE, dr);
     c[FRC_FTYPE] = (uint32_t)(int32_t)p[OLFX_FR_FILTER_TYPE];
-    const uint32_t topo = p[OLFX_FR_TOPOLOGY] == 1.f ? 1u : 0u;
+    const uint32_t topo = (uint32_t)p[OLFX_FR_TOPOLOGY];     // 0..4 (validated by olfx_set_params)
     c[FRC_TOPO] = topo;
-    put(FRC_MASTER, topo ? 1.0f : p[OLFX_FR_MASTER_VOLUME]);   // x 1.0f is exact: no master stage
+    put(FRC_MASTER, topo ? 1.0f : p[OLFX_FR_MASTER_VOLUME]);   // x 1.0f is exact: no FxRack, no master
 }
 
 void derive_voice(const float *p, bool configured, bool moog, float sr, float *c) {
@@ -320,9 +323,9 @@ void derive_voice(const float *p, bool configured, bool moog, float sr, float *c
     c[VCC_AMP_AMT] = p[OLFX_VC_AMP_ENV_AMOUNT];
     c[VCC_CUTOFF] = p[OLFX_VC_FILTER_CUTOFF];
     c[VCC_FENV_AMT] = p[OLFX_VC_FILTER_ENV_AMOUNT];
-    // daisysp::Port (in-tree stub, Portamento.h:223-226); Init happens with htime 0 and
-    // SetHtime(portamento) on Update
-    float htime = configured ? p[OLFX_VC_PORTAMENTO] : 0.0f;
+    // daisysp::Port (in-tree stub, Portamento.h:223-226): SynthVoice::Init passes the member
+    // portamento_htime (SynthVoice.h:37), Update SetHtime(portamento_htime): either way the member
+    float htime = p[OLFX_VC_PORTAMENTO];
     c[VCC_PORT_COEF] = expf(-1.0f / (htime * sr));
     c[VCC_FC_MAX] = sr / 3.f;
     c[VCC_SR] = sr;
@@ -350,6 +353,7 @@ struct olfx_engine {
     uint32_t block = 0;
     float sr = 48000.f;
     hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;            // recorded after each olfx_process's work, on its stream
     uint64_t frames = 0;
     std::string err;
 
@@ -357,7 +361,36 @@ struct olfx_engine {
     uint32_t n_params = 0;
     std::vector<float> params;
     std::vector<uint8_t> configured;     // voice: UpdateConfig seen
-    bool dirty = true;
+    // instances whose coefficients must be re-derived at the next block (each listed once)
+    std::vector<uint32_t> dirty_list;
+    std::vector<uint8_t> dirty_mark;
+    int cus = 0;                          // compute units (the chain's persistent grid)
+    int64_t n_components = 0;             // rack instances with OLFX_FR_TOPOLOGY >= 2
+
+    // control packets: a block's changed coefficients and folded note events, in pinned host
+    // slots the block's kernels read (submit_control).  A slot is rewritten only after the
+    // kernels that read it are done (consumed).
+    static constexpr int kSlots = 4;
+    struct Slot {
+        uint32_t *h = nullptr, *d = nullptr;
+        bool d_owned = false;
+        size_t cap = 0;                   // words
+        hipEvent_t copied = nullptr, consumed = nullptr;
+        bool used = false;
+    } slot[kSlots];
+    int slot_next = 0;
+    std::vector<int32_t> ev_slot;         // voice -> its record in `folded` during fold_events, else -1
+    struct Folded { uint32_t inst, op, freq, pad; };
+    std::vector<Folded> folded, ev_sorted;
+    std::vector<uint32_t> ev_off, ev_fill;   // per-workgroup offsets of ev_sorted
+    std::vector<uint32_t> h_words;        // scratch for a record
+    // OLFX_TRACE_CONTROL=1 (read at create): host time of each control-path step, summed and
+    // printed to stderr at destroy (tracing)
+    bool trace = false;
+    int ctl_mode = 2;                     // OLFX_CTL_MODE (A/B diagnostic): 1 copy on the caller's stream,
+                                          // 2 pinned host memory read by the kernels
+    double tr[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t tr_calls = 0;
 
     // device memory: one allocation per engine, carved
     void *d_mem = nullptr;
@@ -386,11 +419,14 @@ struct olfx_engine {
     uint32_t *mix_dev = nullptr;
     hipEvent_t mix_done = nullptr;          // recorded after every olfx_mix launch
     uint32_t n_buses = 0;
-    std::vector<float> h_vstate;                         // host copy for event application
 
     // host-pointer I/O staging
     float *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
     size_t stage_floats_in = 0, stage_floats_out = 0;
+    // device staging of frame tiles whose channel planes are too far apart for the kernels'
+    // 32-bit buffer offsets (olfx_process on > 4 GiB planes), allocated on first need
+    float *tile_in = nullptr, *tile_out = nullptr;
+    size_t tile_floats = 0;
 
     int fail(int code, const char *fmt, ...) {
         char buf[512];
@@ -451,114 +487,230 @@ uint64_t state_bytes(int kind, uint32_t n, float sr) {
     }
 }
 
-int upload_params(olfx_engine *e, hipStream_t s) {
-    if (!e->dirty) return OLFX_OK;
-    const uint32_t n = e->n, np = e->n_params;
-    std::vector<float> p(np);
-    auto gather = [&](uint32_t i) {
-        for (uint32_t f = 0; f < np; ++f) p[f] = e->params[(size_t)f * n + i];
+// ---------------------------------------------------------------------------------------------
+// Control path (parameters and note events at the block boundary; JUCE-host pattern,
+// modules/juce/host/host.cpp:646-653): O(changed), asynchronous, no host<->device round trip.
+// ---------------------------------------------------------------------------------------------
+
+// Coefficient words per instance and their destination arrays (field-major, CoefScatterArgs).
+uint32_t coef_segments(const olfx_engine *e, CoefScatterArgs *a) {
+    auto seg = [&](void *dst, uint32_t words, uint32_t stride) {
+        a->dst[a->nseg] = (uint32_t *)dst;
+        a->words[a->nseg] = words;
+        a->stride[a->nseg] = stride;
+        ++a->nseg;
     };
-    if (e->kind == OLFX_KIND_DATTORRO || e->kind == OLFX_KIND_CHAIN) {
-        const uint32_t base = e->kind == OLFX_KIND_CHAIN ? OLFX_CN_VERB0 : 0;
-        const uint32_t nd = e->n_dt;                   // padding instances get zero coefficients
-        std::vector<float> c((size_t)DTC_N * nd, 0.f);
-        float cc[DTC_N];
-        for (uint32_t i = 0; i < n; ++i) {
-            gather(i);
-            derive_dattorro(p.data() + base, cc);
-            for (int k = 0; k < DTC_N; ++k) c[(size_t)k * nd + i] = cc[k];
-        }
-        HIPCHK(e, hipMemcpyAsync(e->dt_coef, c.data(), c.size() * 4, hipMemcpyHostToDevice, s));
-        HIPCHK(e, hipStreamSynchronize(s));
+    a->nseg = 0;
+    switch (e->kind) {
+    case OLFX_KIND_DATTORRO: seg(e->dt_coef, DTC_N, e->n_dt); break;
+    case OLFX_KIND_CHORUS:
+    case OLFX_KIND_PITCHSHIFT: seg(e->ch_coef, CHC_N, e->n); break;
+    case OLFX_KIND_CHAIN:       // padding reverb instances keep their zeroed coefficients
+        seg(e->ch_coef, CHC_N, e->n);
+        seg(e->ps_coef, CHC_N, e->n);
+        seg(e->dt_coef, DTC_N, e->n_dt);
+        break;
+    case OLFX_KIND_FXRACK: seg(e->fr_coef, FRC_N, e->n); break;
+    case OLFX_KIND_VOICE:
+    case OLFX_KIND_VOICE_MOOG: seg(e->vc_coef, VCC_N, e->n); break;
+    default: break;
     }
-    if (e->kind == OLFX_KIND_CHORUS || e->kind == OLFX_KIND_PITCHSHIFT || e->kind == OLFX_KIND_CHAIN) {
-        std::vector<uint32_t> c((size_t)CHC_N * n), c2;
-        if (e->kind == OLFX_KIND_CHAIN) c2.resize((size_t)CHC_N * n);
-        uint32_t cc[CHC_N];
-        for (uint32_t i = 0; i < n; ++i) {
-            gather(i);
-            if (e->kind == OLFX_KIND_PITCHSHIFT) derive_pitchshift(p.data(), e->sr, cc);
-            else derive_chorus(p.data() + (e->kind == OLFX_KIND_CHAIN ? OLFX_CN_CHORUS0 : 0), e->sr, cc);
-            for (int k = 0; k < CHC_N; ++k) c[(size_t)k * n + i] = cc[k];
-            if (e->kind == OLFX_KIND_CHAIN) {
-                derive_pitchshift(p.data() + OLFX_CN_PITCH0, e->sr, cc);
-                for (int k = 0; k < CHC_N; ++k) c2[(size_t)k * n + i] = cc[k];
-            }
-        }
-        HIPCHK(e, hipMemcpyAsync(e->ch_coef, c.data(), c.size() * 4, hipMemcpyHostToDevice, s));
-        if (e->kind == OLFX_KIND_CHAIN)
-            HIPCHK(e, hipMemcpyAsync(e->ps_coef, c2.data(), c2.size() * 4, hipMemcpyHostToDevice, s));
-        HIPCHK(e, hipStreamSynchronize(s));
-    }
-    if (e->kind == OLFX_KIND_FXRACK) {
-        std::vector<uint32_t> c((size_t)FRC_N * n);
-        uint32_t cc[FRC_N];
-        for (uint32_t i = 0; i < n; ++i) {
-            gather(i);
-            derive_fxrack(p.data(), e->sr, cc);
-            for (int k = 0; k < FRC_N; ++k) c[(size_t)k * n + i] = cc[k];
-        }
-        HIPCHK(e, hipMemcpyAsync(e->fr_coef, c.data(), c.size() * 4, hipMemcpyHostToDevice, s));
-        HIPCHK(e, hipStreamSynchronize(s));
-    }
-    if (is_voice_kind(e->kind)) {
-        std::vector<float> c((size_t)VCC_N * n);
-        float cc[VCC_N];
-        for (uint32_t i = 0; i < n; ++i) {
-            gather(i);
-            derive_voice(p.data(), e->configured[i] != 0, e->kind == OLFX_KIND_VOICE_MOOG, e->sr, cc);
-            for (int k = 0; k < VCC_N; ++k) c[(size_t)k * n + i] = cc[k];
-        }
-        HIPCHK(e, hipMemcpyAsync(e->vc_coef, c.data(), c.size() * 4, hipMemcpyHostToDevice, s));
-        HIPCHK(e, hipStreamSynchronize(s));
-    }
-    e->dirty = false;
-    return OLFX_OK;
+    uint32_t w = 0;
+    for (uint32_t k = 0; k < a->nseg; ++k) w += a->words[k];
+    return w;
 }
 
-// Voice note events: NoteOn = GateOn + freq = mtof(note) + Retrigger(true) on both envelopes
-// (SynthVoice.h:245-251); NoteOff = GateOff (:253-256).  Applied to the device state with a
-// read-modify-write of the affected instances (control rate, between blocks).
-int apply_events(olfx_engine *e, hipStream_t s) {
-    if (e->events.empty()) return OLFX_OK;
-    const uint32_t n = e->n;
-    std::vector<float> st((size_t)VCS_N * n);
-    HIPCHK(e, hipMemcpyAsync(st.data(), e->vc_state, st.size() * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(e, hipStreamSynchronize(s));
-    for (const olfx_voice_event &ev : e->events) {
-        const uint32_t i = ev.inst;
-        uint32_t flags;
-        std::memcpy(&flags, &st[(size_t)VCS_FLAGS * n + i], 4);
-        switch (ev.type) {
-        case OLFX_EV_NOTE_ON:
-            flags |= 1u << 8;                                   // gate = true
-            // Retrigger(true): mode = ATTACK (1), x = 0, for amp (bits 0-2) and filter (3-5)
-            flags = (flags & ~0x3Fu) | 1u | (1u << 3);
-            st[(size_t)VCS_ENVA_X * n + i] = 0.f;
-            st[(size_t)VCS_ENVF_X * n + i] = 0.f;
-            st[(size_t)VCS_FREQ * n + i] = powf(2.f, (ev.note - 69.0f) / 12.0f) * 440.0f;  // daisysp::mtof
-            break;
-        case OLFX_EV_GATE_ON: flags |= 1u << 8; break;         // SynthVoice::GateOn (:231-234)
-        case OLFX_EV_SET_FREQUENCY: st[(size_t)VCS_FREQ * n + i] = ev.value; break;   // :264-267
-        default: flags &= ~(1u << 8); break;                    // NoteOff / GateOff (:236-239)
+// The coefficient record of instance i from its current parameters (the reference setters'
+// arithmetic, derive_*), in the word order of coef_segments.
+void derive_record(olfx_engine *e, uint32_t i, uint32_t *w) {
+    const uint32_t n = e->n, np = e->n_params;
+    float p[OLFX_CN_NPARAMS > OLFX_VC_NPARAMS ? OLFX_CN_NPARAMS : OLFX_VC_NPARAMS];
+    for (uint32_t f = 0; f < np; ++f) p[f] = e->params[(size_t)f * n + i];
+    float fc[VCC_N > DTC_N ? VCC_N : DTC_N];
+    switch (e->kind) {
+    case OLFX_KIND_DATTORRO:
+        derive_dattorro(p, fc);
+        std::memcpy(w, fc, DTC_N * 4);
+        break;
+    case OLFX_KIND_CHORUS: derive_chorus(p, e->sr, w); break;
+    case OLFX_KIND_PITCHSHIFT: derive_pitchshift(p, e->sr, w); break;
+    case OLFX_KIND_CHAIN:
+        derive_chorus(p + OLFX_CN_CHORUS0, e->sr, w);
+        derive_pitchshift(p + OLFX_CN_PITCH0, e->sr, w + CHC_N);
+        derive_dattorro(p + OLFX_CN_VERB0, fc);
+        std::memcpy(w + 2 * CHC_N, fc, DTC_N * 4);
+        break;
+    case OLFX_KIND_FXRACK: derive_fxrack(p, e->sr, w); break;
+    case OLFX_KIND_VOICE:
+    case OLFX_KIND_VOICE_MOOG:
+        derive_voice(p, e->configured[i] != 0, e->kind == OLFX_KIND_VOICE_MOOG, e->sr, fc);
+        std::memcpy(w, fc, VCC_N * 4);
+        break;
+    default: break;
+    }
+}
+
+void mark_dirty(olfx_engine *e, uint32_t first, uint32_t count) {
+    for (uint32_t k = first; k < first + count; ++k)
+        if (!e->dirty_mark[k]) {
+            e->dirty_mark[k] = 1;
+            e->dirty_list.push_back(k);
         }
-        std::memcpy(&st[(size_t)VCS_FLAGS * n + i], &flags, 4);
+}
+
+// The block's note events, one record per voice, in voice order (VEV_*, olfx_internal.h).
+// Calls on one voice compose field by field, as their in-order application does
+// (SynthVoice.h:231-268): NoteOn = GateOn + freq_ = mtof(note) + Retrigger(true) on both
+// envelopes (:245-251); NoteOff / GateOff = gate off (:236-239, :253-256); GateOn = gate on
+// (:231-234); SetFrequency = freq_ (:264-267).  The last gate call decides the gate, any NoteOn
+// retriggers (gate calls do not touch the envelope modes), the last NoteOn / SetFrequency the pitch.
+void fold_events(olfx_engine *e) {
+    e->folded.clear();
+    for (const olfx_voice_event &ev : e->events) {
+        int32_t &k = e->ev_slot[ev.inst];
+        if (k < 0) {
+            k = (int32_t)e->folded.size();
+            e->folded.push_back(olfx_engine::Folded{ev.inst, 0u, 0u, 0u});
+        }
+        olfx_engine::Folded &r = e->folded[(size_t)k];
+        switch (ev.type) {
+        case OLFX_EV_NOTE_ON: {
+            r.op |= VEV_GATE_SET | VEV_GATE_ON | VEV_RETRIGGER | VEV_FREQ;
+            const float hz = powf(2.f, (ev.note - 69.0f) / 12.0f) * 440.0f;   // daisysp::mtof
+            std::memcpy(&r.freq, &hz, 4);
+            break;
+        }
+        case OLFX_EV_GATE_ON: r.op |= VEV_GATE_SET | VEV_GATE_ON; break;
+        case OLFX_EV_SET_FREQUENCY:
+            r.op |= VEV_FREQ;
+            std::memcpy(&r.freq, &ev.value, 4);
+            break;
+        default: r.op = (r.op | VEV_GATE_SET) & ~VEV_GATE_ON; break;   // NoteOff / GateOff
+        }
     }
     e->events.clear();
-    HIPCHK(e, hipMemcpyAsync(e->vc_state, st.data(), st.size() * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(e, hipStreamSynchronize(s));
+    // bucket the records by workgroup (64 voices), a counting sort: ev_off[g] .. ev_off[g+1] are
+    // group g's records (any order inside a group: a lane finds its voice's record by slot)
+    const uint32_t groups = (e->n + 63u) / 64u;
+    e->ev_off.assign(groups + 1, 0u);
+    for (const olfx_engine::Folded &r : e->folded) {
+        e->ev_off[(r.inst >> 6) + 1]++;
+        e->ev_slot[r.inst] = -1;
+    }
+    for (uint32_t g = 0; g < groups; ++g) e->ev_off[g + 1] += e->ev_off[g];
+    e->ev_sorted.resize(e->folded.size());
+    e->ev_fill.assign(e->ev_off.begin(), e->ev_off.end() - 1);
+    for (const olfx_engine::Folded &r : e->folded) e->ev_sorted[e->ev_fill[r.inst >> 6]++] = r;
+}
+
+// This block's control packet -- the changed instances' coefficient records and the folded note
+// events -- in a pinned host slot that the block's kernels read directly over the host link
+// (zero-copy: no copy command, no second stream, no host wait on the device).  The coefficients are
+// scattered on `s` ahead of the block's kernel; the voice kernel reads its events itself.  A slot is
+// rewritten only after the kernels that read it are done (its `consumed` event, recorded by the
+// caller after them: *used_slot).  Packet layout (u32 words, 16-B aligned sections): instance list
+// (absent when every instance changed) | coefficient records [W][m] | event offsets [groups + 1] |
+// event records [mev][4].
+int submit_control(olfx_engine *e, hipStream_t s, VoiceArgs *va, olfx_engine::Slot **used_slot) {
+    *used_slot = nullptr;
+    const bool voice = is_voice_kind(e->kind);
+    const size_t m = e->dirty_list.size();
+    if (!m && !(voice && !e->events.empty())) return OLFX_OK;
+    using clk = std::chrono::steady_clock;
+    auto t_prev = clk::now();
+    auto lap = [&](int k) {
+        if (!e->trace) return;
+        const auto t = clk::now();
+        e->tr[k] += std::chrono::duration<double, std::micro>(t - t_prev).count();
+        t_prev = t;
+    };
+    e->tr_calls++;
+    const bool evs = voice && !e->events.empty();
+    if (evs) fold_events(e);
+    const size_t mev = evs ? e->ev_sorted.size() : 0;
+    lap(0);
+    CoefScatterArgs ca{};
+    const uint32_t W = coef_segments(e, &ca);
+    const bool dense = m == e->n;                        // every instance: no instance list
+    const uint32_t groups = (e->n + 63u) / 64u;
+    auto up4 = [](size_t x) { return (x + 3) & ~(size_t)3; };
+    const size_t o_inst = 0;
+    const size_t o_val = o_inst + (dense ? 0 : up4(m));
+    const size_t o_off = up4(o_val + (size_t)W * m);
+    const size_t o_ev = up4(o_off + (mev ? groups + 1 : 0));
+    const size_t words = o_ev + 4 * mev;
+
+    olfx_engine::Slot &sl = e->slot[e->slot_next];
+    e->slot_next = (e->slot_next + 1) % olfx_engine::kSlots;
+    const int mode = e->ctl_mode;
+    if (sl.used) HIPCHK(e, hipEventSynchronize(mode == 2 ? sl.consumed : sl.copied));   // the host half is free
+    lap(1);
+    if (sl.cap < words) {
+        if (sl.used) HIPCHK(e, hipEventSynchronize(sl.consumed));  // the device half too
+        if (sl.h) (void)hipHostFree(sl.h);
+        if (sl.d && sl.d_owned) (void)hipFree(sl.d);
+        sl.h = nullptr; sl.d = nullptr; sl.cap = 0; sl.used = false; sl.d_owned = false;
+        const size_t cap = std::max<size_t>(words + words / 2, 4096);
+        HIPCHK(e, hipHostMalloc((void **)&sl.h, cap * 4, hipHostMallocDefault));
+        if (mode == 2) {         // the kernels read the pinned host memory
+            void *dp = nullptr;
+            HIPCHK(e, hipHostGetDevicePointer(&dp, sl.h, 0));
+            sl.d = (uint32_t *)dp;
+        } else {
+            HIPCHK(e, hipMalloc((void **)&sl.d, cap * 4));
+            sl.d_owned = true;
+        }
+        sl.cap = cap;
+    }
+    lap(2);
+    // coefficient records, field-major [W][m]
+    uint32_t *val = sl.h + o_val;
+    e->h_words.resize(W);
+    for (size_t r = 0; r < m; ++r) {
+        const uint32_t i = dense ? (uint32_t)r : e->dirty_list[r];
+        if (!dense) sl.h[o_inst + r] = i;
+        derive_record(e, i, e->h_words.data());
+        for (uint32_t w = 0; w < W; ++w) val[(size_t)w * m + r] = e->h_words[w];
+    }
+    for (const uint32_t i : e->dirty_list) e->dirty_mark[i] = 0;
+    e->dirty_list.clear();
+    lap(3);
+    if (mev) {
+        std::memcpy(sl.h + o_off, e->ev_off.data(), (groups + 1) * 4);
+        std::memcpy(sl.h + o_ev, e->ev_sorted.data(), mev * 16);
+    }
+    if (mode == 2) {
+        std::atomic_thread_fence(std::memory_order_seq_cst);     // the packet's stores before the launch
+    } else {
+        HIPCHK(e, hipMemcpyAsync(sl.d, sl.h, words * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(e, hipEventRecord(sl.copied, s));
+    }
+    sl.used = true;
+    *used_slot = &sl;
+    lap(4);
+    if (m) {
+        ca.inst = dense ? nullptr : sl.d + o_inst;
+        ca.val = sl.d + o_val;
+        ca.m = (uint32_t)m;
+        ca.W = W;
+        const hipError_t r = launch_coef_scatter(ca, s);
+        if (r != hipSuccess) return e->hip_fail(r, "coefficient scatter launch");
+    }
+    if (mev) {
+        va->ev_off = sl.d + o_off;
+        va->ev = reinterpret_cast<const uint4 *>(sl.d + o_ev);
+    }
+    lap(5);
     return OLFX_OK;
 }
 
 int init_state(olfx_engine *e) {
+    // all of the engine's earlier work (on any stream) is done: control slots included
+    for (olfx_engine::Slot &sl : e->slot)
+        if (sl.used) HIPCHK(e, hipEventSynchronize(sl.consumed));
     HIPCHK(e, hipMemsetAsync(e->d_mem, 0, e->d_bytes, e->stream));
-    if (is_voice_kind(e->kind)) {
-        // daisysp Oscillator::Init phase 0; Svf::Init states 0 and freq 0.25; Adsr idle;
-        // freq_ = 0 (SynthVoice.h:276); Port z1 = 0.
-        std::vector<float> st((size_t)VCS_N * e->n, 0.f);
-        for (uint32_t i = 0; i < e->n; ++i) st[(size_t)VCS_FREQ * e->n + i] = 0.f;
-        HIPCHK(e, hipMemcpyAsync(e->vc_state, st.data(), st.size() * 4, hipMemcpyHostToDevice, e->stream));
-    }
+    // voices: daisysp Oscillator::Init phase 0; Svf::Init states 0; Adsr idle; freq_ = 0
+    // (SynthVoice.h:276); Port z1 = 0 -- all zeros
     HIPCHK(e, hipStreamSynchronize(e->stream));
     e->params.assign((size_t)e->n_params * e->n, 0.f);
     std::vector<float> d(e->n_params);
@@ -566,9 +718,13 @@ int init_state(olfx_engine *e) {
     for (uint32_t f = 0; f < e->n_params; ++f)
         std::fill(e->params.begin() + (size_t)f * e->n, e->params.begin() + (size_t)(f + 1) * e->n, d[f]);
     e->configured.assign(e->n, 0);
+    e->n_components = 0;
     e->events.clear();
+    e->ev_slot.assign(e->n, -1);
     e->frames = 0;
-    e->dirty = true;
+    e->dirty_list.clear();
+    e->dirty_mark.assign(e->n, 0);
+    mark_dirty(e, 0, e->n);                  // every coefficient is derived at the first block
     return OLFX_OK;
 }
 
@@ -593,7 +749,10 @@ int ensure_staging(olfx_engine *e, size_t fin, size_t fout) {
 }
 
 
-int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hipStream_t s) {
+// One launch over frames [e->frames, e->frames + n_frames) of every instance: in / out hold those
+// frames with channel planes `plane` floats apart.  `ev` carries the block's note events (voices).
+int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, uint64_t plane, hipStream_t s,
+           const VoiceArgs &ev) {
     hipError_t r = hipSuccess;
     const uint32_t t0 = (uint32_t)(e->frames & 0xFFFFFFFFu);
     auto dt_args = [&](const float *in, float *out) {
@@ -607,7 +766,7 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hip
         a.coef = e->dt_coef;
         a.in = in;
         a.out = out;
-        a.plane = (uint64_t)n_frames * e->n;
+        a.plane = plane;
         a.n = e->n_dt;
         a.n_frames = n_frames;
         a.t0 = t0 & 0xFFFFu;
@@ -623,7 +782,7 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hip
         a.coef = cf;
         a.in = in;
         a.out = out;
-        a.plane = (uint64_t)n_frames * e->n;
+        a.plane = plane;
         a.n = e->n;
         a.n_frames = n_frames;
         a.t0 = t0;
@@ -649,6 +808,8 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hip
         a.n = e->n;
         a.n_frames = n_frames;
         a.moog = e->kind == OLFX_KIND_VOICE_MOOG;
+        a.ev_off = ev.ev_off;
+        a.ev = ev.ev;
         r = launch_voice(a, s);
         break;
     }
@@ -659,10 +820,11 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hip
         a.coef = e->fr_coef;
         a.in = din;
         a.out = dout;
-        a.plane = (uint64_t)n_frames * e->n;
+        a.plane = plane;
         a.n = e->n;
         a.n_frames = n_frames;
         a.t0 = (uint32_t)(e->frames % kFrMaxDelay);
+        a.components = e->n_components > 0;
         r = launch_fxrack(a, s);
         break;
     }
@@ -674,9 +836,10 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hip
         a.d = dt_args(nullptr, nullptr);
         a.in = din;
         a.out = dout;
-        a.plane = (uint64_t)n_frames * e->n;
+        a.plane = plane;
         a.n = e->n;
         a.n_frames = n_frames;
+        a.cus = (uint32_t)e->cus;
         r = launch_chain(a, s);
         break;
     }
@@ -688,6 +851,67 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, hip
 
 uint32_t in_channels(int kind) { return is_voice_kind(kind) ? 0u : 2u; }
 uint32_t out_channels(int kind) { return is_voice_kind(kind) ? 1u : 2u; }
+
+// Kinds whose kernels address the audio planes with 32-bit buffer offsets from `in` / `out`.
+bool planes_32bit(int kind) {
+    return kind == OLFX_KIND_CHORUS || kind == OLFX_KIND_PITCHSHIFT || kind == OLFX_KIND_CHAIN ||
+           kind == OLFX_KIND_FXRACK;
+}
+
+// All n_frames of a call, as frame tiles where a launch's planes would leave the kernels' 32-bit
+// offset range (planes_32bit): a tile is frames [f0, f0 + F) at in + f0 n with the caller's
+// plane distance, so the launch spans plane + F n floats (< 4 GiB); when the caller's planes alone
+// are >= 4 GiB apart, tiles are staged through a compact device buffer.  Frames run in order and
+// the state carries between launches, so tiles compute exactly what one launch would.  The note
+// events apply before the first tile (the block's start).
+int run_frames(olfx_engine *e, const float *in, float *out, uint32_t n_frames, hipStream_t s, const VoiceArgs &ev) {
+    const uint64_t n = e->n, plane = (uint64_t)n_frames * n;
+    const uint64_t lim = (1ull << 30) - 1;                     // floats addressable in 32-bit bytes
+    const VoiceArgs none{};
+    if (!planes_32bit(e->kind) || plane + plane <= lim) {
+        const int rc = launch(e, in, out, n_frames, plane, s, ev);
+        if (rc) return rc;
+        e->frames += n_frames;
+        return OLFX_OK;
+    }
+    if (plane + 4 * n <= lim) {
+        const uint32_t F = (uint32_t)std::min<uint64_t>(n_frames, ((lim - plane) / n) & ~3ull);
+        for (uint32_t f0 = 0; f0 < n_frames; f0 += F) {
+            const uint32_t Ft = std::min(F, n_frames - f0);
+            const int rc = launch(e, in ? in + (size_t)f0 * n : nullptr, out + (size_t)f0 * n, Ft, plane, s,
+                                  f0 ? none : ev);
+            if (rc) return rc;
+            e->frames += Ft;
+        }
+        return OLFX_OK;
+    }
+    // staged: tiles of up to 256 MiB per direction, compact [ch][F][n]
+    const uint32_t ich = in_channels(e->kind), och = out_channels(e->kind);
+    const uint32_t F = (uint32_t)std::max<uint64_t>(4, std::min<uint64_t>(n_frames, ((1ull << 26) / (2 * n)) & ~3ull));
+    if (e->tile_floats < (size_t)2 * F * n) {
+        if (e->tile_in) (void)hipFree(e->tile_in);
+        if (e->tile_out) (void)hipFree(e->tile_out);
+        e->tile_in = e->tile_out = nullptr;
+        e->tile_floats = 0;
+        HIPCHK(e, hipMalloc((void **)&e->tile_in, (size_t)2 * F * n * 4));
+        HIPCHK(e, hipMalloc((void **)&e->tile_out, (size_t)2 * F * n * 4));
+        e->tile_floats = (size_t)2 * F * n;
+    }
+    for (uint32_t f0 = 0; f0 < n_frames; f0 += F) {
+        const uint32_t Ft = std::min(F, n_frames - f0);
+        const size_t bytes = (size_t)Ft * n * 4;
+        for (uint32_t c = 0; c < ich; ++c)
+            HIPCHK(e, hipMemcpyAsync(e->tile_in + (size_t)c * Ft * n, in + c * plane + (size_t)f0 * n, bytes,
+                                     hipMemcpyDeviceToDevice, s));
+        const int rc = launch(e, e->tile_in, e->tile_out, Ft, (uint64_t)Ft * n, s, f0 ? none : ev);
+        if (rc) return rc;
+        for (uint32_t c = 0; c < och; ++c)
+            HIPCHK(e, hipMemcpyAsync(out + c * plane + (size_t)f0 * n, e->tile_out + (size_t)c * Ft * n, bytes,
+                                     hipMemcpyDeviceToDevice, s));
+        e->frames += Ft;
+    }
+    return OLFX_OK;
+}
 
 }  // namespace
 
@@ -739,14 +963,22 @@ int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32
     e->block = block;
     e->sr = sample_rate;
     e->n_params = n_params_of(kind);
+    e->trace = std::getenv("OLFX_TRACE_CONTROL") && std::getenv("OLFX_TRACE_CONTROL")[0] == '1';
+    if (const char *m = std::getenv("OLFX_CTL_MODE")) e->ctl_mode = std::atoi(m) == 1 ? 1 : 2;
     chorus_sizes(sample_rate, &e->psize, &e->csize);
     e->n_dt = kind == OLFX_KIND_CHAIN ? (n_inst + 63u) & ~63u : n_inst;
 
     hipError_t r = hipSetDevice(device);
+    if (r == hipSuccess) r = hipDeviceGetAttribute(&e->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (r == hipSuccess) r = hipEventCreateWithFlags(&e->done, hipEventDisableTiming);
+    for (olfx_engine::Slot &sl : e->slot) {
+        if (r == hipSuccess) r = hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming);
+        if (r == hipSuccess) r = hipEventCreateWithFlags(&sl.consumed, hipEventDisableTiming);
+    }
     if (r != hipSuccess) {
-        int rc = e->hip_fail(r, "olfx_create: stream");
-        delete e;
+        int rc = e->hip_fail(r, "olfx_create: stream / events");
+        olfx_destroy(e);
         return rc;
     }
 
@@ -791,8 +1023,8 @@ int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32
     r = hipMalloc(&e->d_mem, e->d_bytes);
     if (r != hipSuccess) {
         int rc = e->fail(OLFX_E_NOMEM, "olfx_create: hipMalloc(%zu bytes): %s", e->d_bytes, hipGetErrorString(r));
-        (void)hipStreamDestroy(e->stream);
-        delete e;
+        e->d_mem = nullptr;
+        olfx_destroy(e);
         return rc;
     }
     char *base = (char *)e->d_mem;
@@ -833,8 +1065,28 @@ int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32
 
 int olfx_destroy(olfx_engine *e) {
     if (!e) return OLFX_E_ARG;
+    if (e->trace && e->tr_calls)
+        std::fprintf(stderr, "olfx control trace (kind %d, %llu packets, mean us): fold %.2f slot-free %.2f "
+                     "alloc %.2f coefficients %.2f events+deliver %.2f scatter %.2f\n", e->kind,
+                     (unsigned long long)e->tr_calls, e->tr[0] / e->tr_calls, e->tr[1] / e->tr_calls,
+                     e->tr[2] / e->tr_calls, e->tr[3] / e->tr_calls, e->tr[4] / e->tr_calls, e->tr[5] / e->tr_calls);
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->done) (void)hipEventSynchronize(e->done);          // the last block, on the caller's stream
+    if (e->mix_done) (void)hipEventSynchronize(e->mix_done);
+    for (olfx_engine::Slot &sl : e->slot) {
+        if (sl.used) {
+            (void)hipEventSynchronize(sl.copied);
+            (void)hipEventSynchronize(sl.consumed);
+        }
+        if (sl.h) (void)hipHostFree(sl.h);
+        if (sl.d && sl.d_owned) (void)hipFree(sl.d);
+        if (sl.copied) (void)hipEventDestroy(sl.copied);
+        if (sl.consumed) (void)hipEventDestroy(sl.consumed);
+    }
+    if (e->done) (void)hipEventDestroy(e->done);
+    if (e->tile_in) (void)hipFree(e->tile_in);
+    if (e->tile_out) (void)hipFree(e->tile_out);
     if (e->d_mem) (void)hipFree(e->d_mem);
     if (e->h_in) (void)hipHostFree(e->h_in);
     if (e->h_out) (void)hipHostFree(e->h_out);
@@ -851,8 +1103,37 @@ int olfx_reset(olfx_engine *e) {
     if (!e) return OLFX_E_ARG;
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipEventSynchronize(e->done));                    // the last block, on any stream
     return init_state(e);
 }
+
+}  // extern "C"
+
+namespace {
+// A parameter value the reference's setter gives a meaning to (nullptr) or why not.
+const char *bad_value(const olfx_engine *e, uint32_t field, float v) {
+    if (!std::isfinite(v)) return "non-finite value";
+    // the reference converts value * MAX_PREDELAY (4800) to uint16 (verb.cpp:137-139): values whose
+    // product leaves [0, 65536) have no defined meaning there
+    const bool predelay = (e->kind == OLFX_KIND_DATTORRO && field == OLFX_DT_PREDELAY) ||
+                          (e->kind == OLFX_KIND_CHAIN && field == OLFX_CN_VERB0 + OLFX_DT_PREDELAY);
+    if (predelay && !(v >= 0.f && v * 4800.0f < 65536.0f)) return "pre-delay outside [0, 65536/4800)";
+    if (e->kind == OLFX_KIND_FXRACK && field == OLFX_FR_TOPOLOGY && !(v >= 0.f && v <= 4.f && v == (float)(int)v))
+        return "rack topology must be 0, 1, 2, 3 or 4";
+    return nullptr;
+}
+
+// One parameter of one instance; the rack's count of standalone components (topology >= 2, the
+// kernel variant that serves them) follows its topology field.
+void store_param(olfx_engine *e, uint32_t field, uint32_t inst, float v) {
+    float &slot = e->params[(size_t)field * e->n + inst];
+    if (e->kind == OLFX_KIND_FXRACK && field == OLFX_FR_TOPOLOGY)
+        e->n_components += (v >= 2.f ? 1 : 0) - (slot >= 2.f ? 1 : 0);
+    slot = v;
+}
+}  // namespace
+
+extern "C" {
 
 int olfx_set_params(olfx_engine *e, uint32_t first, uint32_t count, uint32_t field0, uint32_t n_fields,
                     const float *values) {
@@ -860,27 +1141,32 @@ int olfx_set_params(olfx_engine *e, uint32_t first, uint32_t count, uint32_t fie
     if (!values || (uint64_t)first + count > e->n || (uint64_t)field0 + n_fields > e->n_params)
         return e->fail(OLFX_E_ARG, "olfx_set_params: range out of bounds");
     // validate everything first: a rejected call changes nothing
-    for (uint32_t f = 0; f < n_fields; ++f) {
-        const uint32_t field = field0 + f;
-        const bool predelay = (e->kind == OLFX_KIND_DATTORRO && field == OLFX_DT_PREDELAY) ||
-                              (e->kind == OLFX_KIND_CHAIN && field == OLFX_CN_VERB0 + OLFX_DT_PREDELAY);
-        for (uint32_t k = 0; k < count; ++k) {
-            const float v = values[(size_t)f * count + k];
-            if (!std::isfinite(v)) return e->fail(OLFX_E_ARG, "olfx_set_params: non-finite value");
-            // the reference converts value * MAX_PREDELAY (4800) to uint16 (verb.cpp:137-139): values
-            // whose product leaves [0, 65536) have no defined meaning there
-            if (predelay && !(v >= 0.f && v * 4800.0f < 65536.0f))
-                return e->fail(OLFX_E_ARG, "olfx_set_params: pre-delay outside [0, 65536/4800)");
-            if (e->kind == OLFX_KIND_FXRACK && field == OLFX_FR_TOPOLOGY && v != 0.f && v != 1.f)
-                return e->fail(OLFX_E_ARG, "olfx_set_params: rack topology must be 0 or 1");
-        }
-    }
     for (uint32_t f = 0; f < n_fields; ++f)
         for (uint32_t k = 0; k < count; ++k)
-            e->params[(size_t)(field0 + f) * e->n + first + k] = values[(size_t)f * count + k];
+            if (const char *why = bad_value(e, field0 + f, values[(size_t)f * count + k]))
+                return e->fail(OLFX_E_ARG, "olfx_set_params: %s", why);
+    for (uint32_t f = 0; f < n_fields; ++f)
+        for (uint32_t k = 0; k < count; ++k) store_param(e, field0 + f, first + k, values[(size_t)f * count + k]);
     if (is_voice_kind(e->kind))
         for (uint32_t k = 0; k < count; ++k) e->configured[first + k] = 1;
-    e->dirty = true;
+    mark_dirty(e, first, count);
+    return OLFX_OK;
+}
+
+int olfx_set_param_list(olfx_engine *e, uint32_t field, const uint32_t *inst, const float *values, uint32_t count) {
+    if (!e) return OLFX_E_ARG;
+    if (count && (!inst || !values)) return e->fail(OLFX_E_ARG, "olfx_set_param_list: null list");
+    if (field >= e->n_params) return e->fail(OLFX_E_ARG, "olfx_set_param_list: field out of range");
+    for (uint32_t k = 0; k < count; ++k) {
+        if (inst[k] >= e->n) return e->fail(OLFX_E_ARG, "olfx_set_param_list: instance %u out of range", inst[k]);
+        if (const char *why = bad_value(e, field, values[k]))
+            return e->fail(OLFX_E_ARG, "olfx_set_param_list: %s", why);
+    }
+    for (uint32_t k = 0; k < count; ++k) {
+        store_param(e, field, inst[k], values[k]);
+        if (is_voice_kind(e->kind)) e->configured[inst[k]] = 1;
+        mark_dirty(e, inst[k], 1);
+    }
     return OLFX_OK;
 }
 
@@ -955,12 +1241,28 @@ int olfx_control(olfx_engine *e, const olfx_control_event *ev, uint32_t n) {
         if (ev[k].inst >= e->n) return e->fail(OLFX_E_ARG, "olfx_control: event %u: instance out of range", k);
         uint32_t field;
         float v;
-        const int rc = olfx_control_map(e->kind, ev[k].control, ev[k].source, ev[k].value, &field, &v);
+        uint8_t control = ev[k].control;
+        const float topo = e->kind == OLFX_KIND_FXRACK ? e->params[(size_t)OLFX_FR_TOPOLOGY * e->n + ev[k].inst] : 0.f;
+        if (topo != 0.f) {
+            // No FxRack around these instances (ol_daisy/app/synth/main.cpp:201-207 sends every CC to
+            // delay_fx, reverb_fx and filter_fx directly): CC_FILTER_* (41-44) reach a FilterFx's own
+            // handler (Fx.h:116-139), which the rack field map reaches as CC_FX_FILTER_* (45-48);
+            // FxRack's own CC_FX_FILTER_* and master volume (CC 7) reach nothing.  A component alone
+            // takes only its own controls: DelayFx 35-39 (Fx.h:218-267), ReverbFx the reverb CCs (of
+            // which only the balance, 34, is audible through the ReverbSc stub), FilterFx 41-44.
+            const bool filter_cc = control >= CC_FILTER_CUTOFF && control <= CC_FILTER_DRIVE;
+            const bool delay_cc = control >= CC_DELAY_TIME && control <= CC_DELAY_BALANCE;
+            const bool takes = topo == 1.f ? (filter_cc || delay_cc || control == CC_REVERB_BALANCE)
+                             : topo == 2.f ? delay_cc : topo == 3.f ? control == CC_REVERB_BALANCE : filter_cc;
+            if (!takes) continue;
+            if (filter_cc) control = (uint8_t)(control - CC_FILTER_CUTOFF + CC_FX_FILTER_CUTOFF);
+        }
+        const int rc = olfx_control_map(e->kind, control, ev[k].source, ev[k].value, &field, &v);
         if (rc == OLFX_IGNORED) continue;
         if (rc != OLFX_OK) return e->fail(rc, "olfx_control: event %u", k);
         if (field == OLFX_FIELD_UPDATE_ONLY) {    // Update() with unchanged members
             if (is_voice_kind(e->kind)) e->configured[ev[k].inst] = 1;
-            e->dirty = true;
+            mark_dirty(e, ev[k].inst, 1);
             continue;
         }
         const int r2 = olfx_set_params(e, ev[k].inst, 1, field, 1, &v);
@@ -971,6 +1273,16 @@ int olfx_control(olfx_engine *e, const olfx_control_event *ev, uint32_t n) {
 
 int olfx_set_param(olfx_engine *e, uint32_t inst, uint32_t field, float value) {
     return olfx_set_params(e, inst, 1, field, 1, &value);
+}
+
+int olfx_set_member(olfx_engine *e, uint32_t inst, uint32_t field, float value) {
+    if (!e) return OLFX_E_ARG;
+    if (!is_voice_kind(e->kind)) return olfx_set_params(e, inst, 1, field, 1, &value);
+    if (inst >= e->n || field >= e->n_params) return e->fail(OLFX_E_ARG, "olfx_set_member: out of range");
+    if (const char *why = bad_value(e, field, value)) return e->fail(OLFX_E_ARG, "olfx_set_member: %s", why);
+    store_param(e, field, inst, value);                 // no Update(): `configured` unchanged
+    mark_dirty(e, inst, 1);
+    return OLFX_OK;
 }
 
 int olfx_get_param(olfx_engine *e, uint32_t inst, uint32_t field, float *value) {
@@ -1010,7 +1322,7 @@ int olfx_update(olfx_engine *e, uint32_t first, uint32_t count) {
     if ((uint64_t)first + count > e->n) return e->fail(OLFX_E_ARG, "olfx_update: range out of bounds");
     if (is_voice_kind(e->kind))
         for (uint32_t k = 0; k < count; ++k) e->configured[first + k] = 1;
-    e->dirty = true;
+    mark_dirty(e, first, count);
     return OLFX_OK;
 }
 
@@ -1023,31 +1335,42 @@ int olfx_process(olfx_engine *e, const float *in, float *out, uint32_t n_frames,
         return e->fail(OLFX_E_ARG, "olfx_process: bad io_flags");
     HIPCHK(e, hipSetDevice(e->device));
     hipStream_t s = (hipStream_t)stream;   // NULL = the HIP default (null) stream
-    int rc = upload_params(e, s);
-    if (rc) return rc;
-    if (is_voice_kind(e->kind)) {
-        rc = apply_events(e, s);
-        if (rc) return rc;
-    }
     const size_t fin = (size_t)in_channels(e->kind) * n_frames * e->n;
     const size_t fout = (size_t)out_channels(e->kind) * n_frames * e->n;
+    int rc = OLFX_OK;
     if (io_flags == OLFX_IO_HOST) {
         rc = ensure_staging(e, fin ? fin : 1, fout);
         if (rc) return rc;
+    }
+    // the block's parameter changes and note events: asynchronous, O(changed)
+    VoiceArgs ev{};
+    olfx_engine::Slot *sl = nullptr;
+    rc = submit_control(e, s, &ev, &sl);
+    if (rc) return rc;
+    if (io_flags == OLFX_IO_HOST) {
+        hipError_t r = hipSuccess;
         if (fin) {
             std::memcpy(e->h_in, in, fin * 4);
-            HIPCHK(e, hipMemcpyAsync(e->d_in, e->h_in, fin * 4, hipMemcpyHostToDevice, s));
+            r = hipMemcpyAsync(e->d_in, e->h_in, fin * 4, hipMemcpyHostToDevice, s);
         }
-        rc = launch(e, e->d_in, e->d_out, n_frames, s);
-        if (rc) return rc;
+        rc = r == hipSuccess ? run_frames(e, fin ? e->d_in : nullptr, e->d_out, n_frames, s, ev)
+                             : e->hip_fail(r, "olfx_process: input copy");
+    } else {
+        rc = run_frames(e, in, out, n_frames, s, ev);
+    }
+    // the slot is free again once whatever was queued on `s` (the scatter, the kernels) is done --
+    // recorded on the error paths too, so a later block never overwrites a packet still being read
+    if (sl) {
+        const hipError_t r = hipEventRecord(sl->consumed, s);
+        if (!rc && r != hipSuccess) rc = e->hip_fail(r, "hipEventRecord(consumed)");
+    }
+    if (rc) return rc;
+    if (io_flags == OLFX_IO_HOST) {
         HIPCHK(e, hipMemcpyAsync(e->h_out, e->d_out, fout * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(e, hipStreamSynchronize(s));
         std::memcpy(out, e->h_out, fout * 4);
-    } else {
-        rc = launch(e, in, out, n_frames, s);
-        if (rc) return rc;
     }
-    e->frames += n_frames;
+    HIPCHK(e, hipEventRecord(e->done, s));
     return OLFX_OK;
 }
 
@@ -1087,8 +1410,12 @@ int olfx_mix_config(olfx_engine *e, uint32_t n_buses, const uint32_t *offsets, c
         }
     }
     if (e->mix_dev) {   // the last mix launched (on any stream) may still read the old lists
-        if (e->mix_done) HIPCHK(e, hipEventSynchronize(e->mix_done));
-        HIPCHK(e, hipFree(e->mix_dev));
+        hipError_t r = e->mix_done ? hipEventSynchronize(e->mix_done) : hipSuccess;
+        if (r == hipSuccess) r = hipFree(e->mix_dev);
+        if (r != hipSuccess) {          // the current configuration stays; the new lists are dropped
+            if (fresh) (void)hipFree(fresh);
+            return e->hip_fail(r, "olfx_mix_config: releasing the previous lists");
+        }
     }
     e->mix_dev = fresh;
     e->n_buses = n_buses;

@@ -169,13 +169,42 @@ enum {
 inline bool is_voice_kind(int k) { return k == OLFX_KIND_VOICE || k == OLFX_KIND_VOICE_MOOG; }
 inline uint32_t voice_state_slots(int k) { return k == OLFX_KIND_VOICE_MOOG ? (uint32_t)VCS_N_MOOG : (uint32_t)VCS_N; }
 
+// Note events of one block, folded per voice on the host (olfx_engine.cpp fold_events) and applied
+// by the voice kernel itself as its first act on the voice's state (SynthVoice.h:231-268: the
+// events of a block compose field by field -- the last gate call wins, any NoteOn retriggers, the
+// last NoteOn / SetFrequency sets the pitch).
+enum : uint32_t {
+    VEV_GATE_SET = 1u,          // gate := VEV_GATE_ON bit (NoteOn / GateOn / NoteOff / GateOff)
+    VEV_GATE_ON = 2u,
+    VEV_RETRIGGER = 4u,         // Adsr::Retrigger(true) on both envelopes: mode ATTACK, x = 0
+    VEV_FREQ = 8u,              // freq_ := rec.z (mtof(note) for NoteOn, SetFrequency's Hz)
+};
+
 struct VoiceArgs {
     float *state;               // [VCS_N][n], MoogFilter voices [VCS_N_MOOG][n]
     const float *coef;          // [VCC_N][n]
     float *out;                 // [1][n_frames][n]
     uint32_t n, n_frames;
     uint32_t moog;              // 1: daisysp::LadderFilter (MoogFilter) in place of the Svf
+    // this block's events (nullptr: none): workgroup g's records are ev[ev_off[g] .. ev_off[g+1]),
+    // sorted by voice, at most one per voice: (voice, VEV_* ops, frequency bits, 0)
+    const uint32_t *ev_off;     // [n_groups + 1], n_groups = ceil(n / 64)
+    const uint4 *ev;
 };
+
+// Coefficient records of the instances whose parameters changed (olfx_engine.cpp upload_params):
+// word w of record r goes to dst[s][(w - first word of segment s) * stride[s] + inst[r]].  Field-
+// major records ([w][m]) so consecutive threads write consecutive instances.
+struct CoefScatterArgs {
+    const uint32_t *inst;       // [m] instance of each record; nullptr = the identity (m == every instance)
+    const uint32_t *val;        // [W][m]
+    uint32_t m, W;
+    uint32_t nseg;
+    uint32_t *dst[3];
+    uint32_t words[3];          // words of each segment (sum = W)
+    uint32_t stride[3];         // instance stride of each segment's field-major array
+};
+hipError_t launch_coef_scatter(const CoefScatterArgs &a, hipStream_t s);
 
 // ----------------------------------------------------------------------------------------------
 // Effect rack ol::fx::FxRack<2> (fxrack.hip): delay lines + two Svf (channel 0) + ReverbSc stub.
@@ -190,7 +219,7 @@ enum {
     FRC_FFREQ, FRC_FDAMP, FRC_FDRIVE,       // FxRack filter1 Svf
     FRC_FTYPE,          // uint: 0 low, 1 band, 2 high, 3 notch, 4 peak
     FRC_MASTER,
-    FRC_TOPO,           // uint: OLFX_FR_TOPOLOGY
+    FRC_TOPO,           // uint: OLFX_FR_TOPOLOGY (0..4)
     FRC_N
 };
 enum { FRS_DLOW = 0, FRS_DBAND, FRS_FLOW, FRS_FBAND, FRS_N };
@@ -203,6 +232,7 @@ struct FxRackArgs {
     uint64_t plane;
     uint32_t n, n_frames;
     uint32_t t0;                // ring position of the first frame: frames since create mod 48000
+    uint32_t components;        // some instance is a standalone component (topology 2..4)
 };
 
 // Launchers (defined in the .hip files).
@@ -217,6 +247,7 @@ struct ChainArgs {
     float *out;                 // [2][..][n]
     uint64_t plane;             // floats between channel planes of in / out
     uint32_t n, n_frames;       // real instances; frames (multiple of 4)
+    uint32_t cus;               // compute units of the device (the persistent grid), from olfx_create
 };
 
 hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s);

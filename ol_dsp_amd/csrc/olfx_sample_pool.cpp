@@ -42,7 +42,7 @@ struct olfx_sample {
 namespace {
 
 struct PendingOp {      // a call waiting for the next block boundary
-    enum { PARAM, EVENT, CONTROL, UPDATE } type;
+    enum { PARAM, MEMBER, EVENT, CONTROL, UPDATE } type;
     uint32_t inst, field;
     float value;
     uint8_t a, b, c;
@@ -83,6 +83,7 @@ int apply(Generation *g, const PendingOp &op) {
     olfx_engine *e = g->e.load();
     switch (op.type) {
     case PendingOp::PARAM: return olfx_set_param(e, op.inst, op.field, op.value);
+    case PendingOp::MEMBER: return olfx_set_member(e, op.inst, op.field, op.value);
     case PendingOp::EVENT: {
         olfx_voice_event ev{};
         ev.inst = op.inst; ev.type = op.a; ev.note = op.b; ev.velocity = op.c; ev.value = op.value;
@@ -238,6 +239,11 @@ int olfx_sample_destroy(olfx_sample *s) {
 int olfx_sample_set_param(olfx_sample *s, uint32_t field, float value) {
     if (!s) return OLFX_E_ARG;
     return queue_or_apply(s, PendingOp{PendingOp::PARAM, s->idx, field, value, 0, 0, 0});
+}
+
+int olfx_sample_set_member(olfx_sample *s, uint32_t field, float value) {
+    if (!s) return OLFX_E_ARG;
+    return queue_or_apply(s, PendingOp{PendingOp::MEMBER, s->idx, field, value, 0, 0, 0});
 }
 
 int olfx_sample_note(olfx_sample *s, uint8_t type, uint8_t note, uint8_t velocity) {

@@ -69,6 +69,47 @@ struct Ladder {
     float z0[4], z1[4], old;
 };
 
+// The block's folded note events (VoiceArgs::ev, VEV_*) of this lane's voice: the wave stages its
+// workgroup's records (at most 64, one per voice) into its own 64 LDS slots, slot = voice within the
+// group, and each lane reads its own.  `me` is the lane's voice within the group (dead lanes of the
+// last group mirror voice n-1, so they read its slot too).  No events: one uniform test.
+struct VoiceEv {
+    uint32_t op;
+    float freq;
+};
+__device__ __forceinline__ VoiceEv voice_event(const VoiceArgs &a, uint2 *slot, uint32_t lane, uint32_t me) {
+    VoiceEv r{0u, 0.0f};
+    if (!a.ev_off) return r;
+    const uint32_t lo = a.ev_off[blockIdx.x], hi = a.ev_off[blockIdx.x + 1];
+    if (lo == hi) return r;
+    slot[lane] = make_uint2(0u, 0u);
+    if (lo + lane < hi) {
+        const uint4 e = a.ev[lo + lane];
+        slot[e.x & 63u] = make_uint2(e.y, e.z);
+    }
+    // one wave writes and reads its slots: LDS operations of a wave complete in order; the fences
+    // keep the compiler from moving the read above the other lanes' writes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint2 v = slot[me];
+    r.op = v.x;
+    r.freq = __uint_as_float(v.y);
+    return r;
+}
+
+// NoteOn / GateOn / NoteOff / GateOff on the envelope flags word and levels (SynthVoice.h:231-251):
+// Retrigger(true) = mode ATTACK and x = 0 for the amp (bits 0-2) and filter (bits 3-5) envelopes;
+// the gate is bit 8
+__device__ __forceinline__ void apply_gate_events(const VoiceEv &ev, uint32_t &flags, float &xa, float &xf) {
+    if (ev.op & VEV_RETRIGGER) {
+        flags = (flags & ~0x3Fu) | 1u | (1u << 3);
+        xa = 0.0f;
+        xf = 0.0f;
+    }
+    if (ev.op & VEV_GATE_SET) flags = (flags & ~0x100u) | ((ev.op & VEV_GATE_ON) ? 0x100u : 0u);
+}
+
 }  // namespace
 
 // daisysp::Adsr as a segment machine.  The gate is constant inside a block (note events apply
@@ -158,26 +199,33 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
     constexpr uint32_t kRoles = 2u;
     __shared__ float4 q[2][kVcChunk][64];
     __shared__ uint32_t fflags[64];
+    __shared__ uint2 evslot[64];
     const uint32_t n = a.n;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t i0 = blockIdx.x * 64 + lane;
-    // dead lanes of the last workgroup mirror voice n-1 exactly (same state, same coefficients),
-    // so their stores write the values voice n-1's lane writes
+    // dead lanes of the last workgroup mirror voice n-1 exactly (same state, same coefficients,
+    // same events), so their stores write the values voice n-1's lane writes
     const uint32_t i = i0 < n ? i0 : n - 1;
+    const uint32_t me = i - blockIdx.x * 64;
     const uint32_t nf = a.n_frames;
     const uint32_t nchunks = (nf + kVcChunk - 1) / kVcChunk;
     const float *c = a.coef;
     float *s = a.state;
     const bool filt_role = wave == kRoles - 1;
-    const uint32_t flags0 = __float_as_uint(s[VCS_FLAGS * n + i]);
-    const bool gate = (flags0 >> 8) & 1u;
 
     // ---------------- amp and/or cutoff roles (compile-time role flags: straight-line chunks) ----------------
     auto feed = [&](auto amp_c, auto cut_c) {
         constexpr bool AMP = decltype(amp_c)::value, CUT = decltype(cut_c)::value;
+        // the block's note events first (one feed wave per workgroup applies them)
+        const VoiceEv ev = voice_event(a, evslot, lane, me);
+        uint32_t flags0 = __float_as_uint(s[VCS_FLAGS * n + i]);
+        float xa0 = s[VCS_ENVA_X * n + i], xf0 = s[VCS_ENVF_X * n + i];
+        apply_gate_events(ev, flags0, xa0, xf0);
+        const bool gate = (flags0 >> 8) & 1u;
         const float amp_amt = c[VCC_AMP_AMT * n + i], port_c = c[VCC_PORT_COEF * n + i];
-        const float inv_sr = c[VCC_INV_SR * n + i], freq = s[VCS_FREQ * n + i];
+        const float inv_sr = c[VCC_INV_SR * n + i];
+        const float freq = (ev.op & VEV_FREQ) ? ev.freq : s[VCS_FREQ * n + i];
         const float cutoff = c[VCC_CUTOFF * n + i], fenv_amt = c[VCC_FENV_AMT * n + i];
         // ladder: drive_scaled (VCC_DRIVE), 1/(4 sr) (VCC_FC_MAX)
         const float drive = c[VCC_DRIVE * n + i];
@@ -187,10 +235,10 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
         bool gprev_a = (flags0 >> 6) & 1u, gprev_f = (flags0 >> 7) & 1u;
         Env ea, ef;
         if constexpr (AMP)
-            ea.begin(gate, gprev_a, flags0 & 7u, s[VCS_ENVA_X * n + i], c[VCC_ATK_D0A * n + i],
+            ea.begin(gate, gprev_a, flags0 & 7u, xa0, c[VCC_ATK_D0A * n + i],
                      c[VCC_ATK_TGT_A * n + i], c[VCC_DEC_D0A * n + i], c[VCC_REL_D0A * n + i], c[VCC_SUS_A * n + i]);
         if constexpr (CUT)
-            ef.begin(gate, gprev_f, (flags0 >> 3) & 7u, s[VCS_ENVF_X * n + i], c[VCC_ATK_D0F * n + i],
+            ef.begin(gate, gprev_f, (flags0 >> 3) & 7u, xf0, c[VCC_ATK_D0F * n + i],
                      c[VCC_ATK_TGT_F * n + i], c[VCC_DEC_D0F * n + i], c[VCC_REL_D0F * n + i], c[VCC_SUS_F * n + i]);
 
         for (uint32_t k = 0; k <= nchunks; ++k) {
@@ -243,6 +291,7 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
             s[VCS_PORT_Z * n + i] = port_z;
             s[VCS_ENVA_X * n + i] = ea.x;
             s[VCS_FLAGS * n + i] = __uint_as_float(ea.mode | fbits | (uint32_t)gprev_a << 6 | (uint32_t)gate << 8);
+            if (ev.op & VEV_FREQ) s[VCS_FREQ * n + i] = freq;
         }
         if constexpr (CUT) s[VCS_ENVF_X * n + i] = ef.x;
     };
@@ -320,11 +369,13 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     __shared__ float2 eq[2][kVcChunk][64];      // ENV -> OSC, FREQ: (amp, fc_in)
     __shared__ float2 sq[2][kVcChunk][64];      // OSC -> FILT: (src, amp)
     __shared__ float2 fdq[2][kVcChunk][64];     // FREQ -> FILT: (fq, damp)
+    __shared__ uint2 evslot[2][64];             // ENV's and OSC's staging of the block's events
     const uint32_t n = a.n;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t i0 = blockIdx.x * 64 + lane;
     const uint32_t i = i0 < n ? i0 : n - 1;      // dead lanes mirror voice n-1, as in v4
+    const uint32_t me = i - blockIdx.x * 64;
     const uint32_t nf = a.n_frames;
     const uint32_t nsteps = (nf + kVcChunk - 1) / kVcChunk + 2;
     const float *c = a.coef;
@@ -337,15 +388,19 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
 
     if (role == 0) {
         // ---- ENV (SynthVoice.h:42,46-47): the amp and filter Adsr, the cutoff sum ----
-        const uint32_t flags0 = __float_as_uint(s[VCS_FLAGS * n + i]);
+        // the block's gate events first (NoteOn / GateOn / NoteOff / GateOff)
+        const VoiceEv ev = voice_event(a, evslot[0], lane, me);
+        uint32_t flags0 = __float_as_uint(s[VCS_FLAGS * n + i]);
+        float xa0 = s[VCS_ENVA_X * n + i], xf0 = s[VCS_ENVF_X * n + i];
+        apply_gate_events(ev, flags0, xa0, xf0);
         const bool gate = (flags0 >> 8) & 1u;
         bool gprev_a = (flags0 >> 6) & 1u, gprev_f = (flags0 >> 7) & 1u;
         const float amp_amt = c[VCC_AMP_AMT * n + i];
         const float cutoff = c[VCC_CUTOFF * n + i], fenv_amt = c[VCC_FENV_AMT * n + i];
         Env ea, ef;
-        ea.begin(gate, gprev_a, flags0 & 7u, s[VCS_ENVA_X * n + i], c[VCC_ATK_D0A * n + i],
+        ea.begin(gate, gprev_a, flags0 & 7u, xa0, c[VCC_ATK_D0A * n + i],
                  c[VCC_ATK_TGT_A * n + i], c[VCC_DEC_D0A * n + i], c[VCC_REL_D0A * n + i], c[VCC_SUS_A * n + i]);
-        ef.begin(gate, gprev_f, (flags0 >> 3) & 7u, s[VCS_ENVF_X * n + i], c[VCC_ATK_D0F * n + i],
+        ef.begin(gate, gprev_f, (flags0 >> 3) & 7u, xf0, c[VCC_ATK_D0F * n + i],
                  c[VCC_ATK_TGT_F * n + i], c[VCC_DEC_D0F * n + i], c[VCC_REL_D0F * n + i], c[VCC_SUS_F * n + i]);
         for (uint32_t k = 0; k < nsteps; ++k) {
             if (k + 2 < nsteps) {
@@ -389,8 +444,12 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     } else if (role == 1) {
         // ---- OSC (SynthVoice.h:44-45): Port::Process, Oscillator::SetFreq / Process, WAVE_POLYBLEP_SAW,
         //      amp 0.5 ----
+        // the block's pitch events (NoteOn: mtof(note), SetFrequency: Hz) first
+        const VoiceEv ev = voice_event(a, evslot[1], lane, me);
         const float port_c = c[VCC_PORT_COEF * n + i];
-        const float inv_sr = c[VCC_INV_SR * n + i], freq = s[VCS_FREQ * n + i];
+        const float inv_sr = c[VCC_INV_SR * n + i];
+        const float freq = (ev.op & VEV_FREQ) ? ev.freq : s[VCS_FREQ * n + i];
+        if (ev.op & VEV_FREQ) s[VCS_FREQ * n + i] = freq;
         float phase = s[VCS_PHASE * n + i], port_z = s[VCS_PORT_Z * n + i];
         for (uint32_t k = 0; k < nsteps; ++k) {
             if (k >= 1 && k + 1 < nsteps) {

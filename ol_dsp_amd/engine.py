@@ -126,6 +126,14 @@ class Engine:
         check(self.lib.olfx_set_params(self._h, int(first), int(cnt), self.field(field0), int(nf),
                                        arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float))), self._h)
 
+    def set_param_list(self, field, inst, values) -> None:
+        """One field of scattered instances: inst[k] <- values[k] (olfx_set_param_list)."""
+        ii = np.ascontiguousarray(np.asarray(inst, dtype=np.uint32).ravel())
+        vv = np.ascontiguousarray(np.asarray(values, dtype=np.float32).ravel())
+        assert ii.shape == vv.shape
+        check(self.lib.olfx_set_param_list(self._h, self.field(field), ii.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                           vv.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), len(ii)), self._h)
+
     @staticmethod
     def make_events(inst, type_, note, velocity=100):
         """A prebuilt event array (numpy-vectorised) for note_events: inst / note arrays (or

@@ -34,6 +34,9 @@ RANGES = {
 }
 RANGES["voice_moog"] = RANGES["voice"]
 RANGES["chain"] = RANGES["chorus"] + RANGES["pitchshift"] + RANGES["dattorro"]
+# random per-instance pre-delay in [0, 1] x 4800 samples (section 8d's gather-path variant)
+RANGES["dattorro_rpd"] = [(0, 1)] + RANGES["dattorro"][1:]
+RANGES["chain_rpd"] = RANGES["chorus"] + RANGES["pitchshift"] + RANGES["dattorro_rpd"]
 
 
 def _splitmix64(z: np.ndarray) -> np.ndarray:

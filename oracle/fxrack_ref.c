@@ -206,6 +206,30 @@ static void rack_tick(rack_t *r, const float in[2], float out[2])
     buf[0] = svf_process(&r->dfilt, buf[0], 0);        /* FilterFx (LowPass), channel 0 in place */
     float a[2], b[2];
     for (int i = 0; i < 2; ++i) a[i] = (buf[i] * p[OFR_DELAY_BALANCE]) + (in[i] * (1 - p[OFR_DELAY_BALANCE]));
+    /* the components alone, each as the firmware's objects run it (main.cpp:82-85):
+       2 DelayFx<2>::Process (Fx.h:193-206): the rack's delay stage, both channels out */
+    if (p[OFR_TOPOLOGY] == 2.f) {
+        out[0] = a[0];
+        out[1] = a[1];
+        return;
+    }
+    /* 3 ReverbFx<2>::Process over DaisyVerb<2> and the ReverbSc stub (Fx.h:293-299, Reverb.h:26-31,
+       :82-91): per channel 0.8 in balance + in (1 - balance); the delay line runs unobserved */
+    if (p[OFR_TOPOLOGY] == 3.f) {
+        for (int i = 0; i < 2; ++i) {
+            const float v = in[i] * 0.8f;
+            out[i] = (v * p[OFR_REVERB_BALANCE]) + (in[i] * (1 - p[OFR_REVERB_BALANCE]));
+        }
+        return;
+    }
+    /* 4 FilterFx<2>::Process (Fx.h:88-108): the Svf on channel 0 with the selected output; channel 1
+       of frame_out is not written (Filter.h:85-91): in place -- the firmware's use -- it keeps
+       channel 1 of the input */
+    if (p[OFR_TOPOLOGY] == 4.f) {
+        out[0] = svf_process(&r->filt, in[0], (int)p[OFR_FILTER_TYPE]);
+        out[1] = in[1];
+        return;
+    }
     if (p[OFR_TOPOLOGY] == 1.f) {
         /* ol_daisy/app/synth/main.cpp:78-86: delay_fx (DelayFx<1>: line 0 and its filter, the same
            arithmetic as the rack's channel 0) on mono; stereo[0] = stereo[1] = mono;

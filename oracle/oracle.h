@@ -77,6 +77,8 @@ oracle_voice *oracle_voice_create(int n_inst, float sample_rate);
 oracle_voice *oracle_voice_create_model(int n_inst, float sample_rate, int model);
 void oracle_voice_destroy(oracle_voice *o);
 int oracle_voice_config(oracle_voice *o, int inst, const float *values);
+/* member values set before Init, then Init (no Update): see voice_ref.c */
+int oracle_voice_init_members(oracle_voice *o, int inst, const float *values);
 int oracle_voice_note(oracle_voice *o, int inst, int on, int note);
 /* 0 NoteOff, 1 NoteOn, 2 GateOn, 3 GateOff, 4 SetFrequency(value Hz) (Voice.h:33-57) */
 int oracle_voice_event(oracle_voice *o, int inst, int type, int note, float value);
@@ -95,7 +97,8 @@ enum {
     OFR_FILTER_DRIVE,          /* FxRack filter1 drive [0,1] */
     OFR_FILTER_TYPE,           /* 0 low, 1 band, 2 high, 3 notch, 4 peak                Fx.h:67-73 */
     OFR_MASTER_VOLUME,         /* FxRack master_volume                                  Fx.h:405 */
-    OFR_TOPOLOGY,              /* 0 FxRack<2>; 1 the synth firmware callback (main.cpp:78-86)    */
+    OFR_TOPOLOGY,              /* 0 FxRack<2>; 1 the synth firmware callback (main.cpp:78-86); 2 DelayFx<2>,
+                                  3 ReverbFx<2>, 4 FilterFx<2> alone (main.cpp:82-85) */
     OFR_NPARAMS
 };
 typedef struct oracle_fxrack oracle_fxrack;

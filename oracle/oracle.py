@@ -71,6 +71,7 @@ def lib(o0: bool = False) -> ctypes.CDLL:
         L.oracle_voice_create_model.argtypes = [ctypes.c_int, _F, ctypes.c_int]
         L.oracle_voice_destroy.argtypes = [ctypes.c_void_p]
         L.oracle_voice_config.argtypes = [ctypes.c_void_p, ctypes.c_int, _PF]
+        L.oracle_voice_init_members.argtypes = [ctypes.c_void_p, ctypes.c_int, _PF]
         L.oracle_chorus64_create.restype = ctypes.c_void_p
         L.oracle_chorus64_create.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_int]
         L.oracle_chorus64_destroy.argtypes = [ctypes.c_void_p]
@@ -251,6 +252,12 @@ class Voice(_Bank):
         v = np.ascontiguousarray(np.asarray(values, dtype=np.float32))
         assert v.shape == (len(VC_FIELDS),)
         assert self.L.oracle_voice_config(self.h, inst, _pf(v)) == 0
+
+    def init_members(self, inst: int, values) -> None:
+        """Member values set before Init, then Init (no Update): voice_ref.c oracle_voice_init_members."""
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.float32))
+        assert v.shape == (len(VC_FIELDS),)
+        assert self.L.oracle_voice_init_members(self.h, inst, _pf(v)) == 0
 
     def note(self, inst: int, on: bool, note: int = 60) -> None:
         assert self.L.oracle_voice_note(self.h, inst, int(bool(on)), int(note)) == 0

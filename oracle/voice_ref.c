@@ -196,7 +196,7 @@ static void voice_init(voice_t *v, float sr, int model)
     v->res = 0.5f; v->pre_drive = 0.5f; v->drive = 0.5f;
     adsr_init(&v->amp_env, sr);                     /* SynthVoice::Init: Init(sr, 1) x2 */
     adsr_init(&v->filt_env, sr);
-    v->port_coef = expf(-1.0f / (0.0f * sr));       /* Port::Init(sr, htime = 0) */
+    v->port_coef = expf(-1.0f / (0.0f * sr));       /* Port::Init(sr, portamento_htime = 0, the member default) */
     v->amp_env_amount = 0.8f;
     v->filter_cutoff = 0.0f;
     v->filter_env_amount = 1.0f;
@@ -293,6 +293,23 @@ int oracle_voice_config(oracle_voice *o, int inst, const float *values)
     if (!o || inst < 0 || inst >= o->n || !values) return -1;
     memcpy(o->params + (size_t)inst * OVC_NPARAMS, values, sizeof(float) * OVC_NPARAMS);
     voice_update(&o->v[inst], values, o->sr);
+    return 0;
+}
+
+/* Setters called before SynthVoice::Init, then Init (SynthVoice.h:31-39; the Daisy firmware's
+   order, ol_daisy/app/synth/main.cpp:114-128, 149): the members hold the values, Init resets the
+   components to DaisySP's defaults and hands the member portamento_htime to Port::Init; Process
+   reads filter_cutoff, filter_env_amount and amp_env_amount from the members. */
+int oracle_voice_init_members(oracle_voice *o, int inst, const float *values)
+{
+    if (!o || inst < 0 || inst >= o->n || !values) return -1;
+    voice_t *v = &o->v[inst];
+    voice_init(v, o->sr, v->model);
+    memcpy(o->params + (size_t)inst * OVC_NPARAMS, values, sizeof(float) * OVC_NPARAMS);
+    v->filter_cutoff = values[OVC_FILTER_CUTOFF];
+    v->filter_env_amount = values[OVC_FILTER_ENV_AMOUNT];
+    v->amp_env_amount = values[OVC_AMP_ENV_AMOUNT];
+    v->port_coef = expf(-1.0f / (values[OVC_PORTAMENTO] * o->sr));
     return 0;
 }
 

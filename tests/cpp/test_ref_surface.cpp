@@ -304,11 +304,193 @@ TEST(RefFxRack, ComponentsAndRackControlsBitExact) {
     EXPECT_TRUE(ok);
     oracle_fxrack_destroy(ref);
 
-    int code = 0;                                      /* a component on its own has no GPU kernel */
-    ol::fx::FilterFx<2> lone;
+    int code = 0;                                      /* a rack's component is run by its rack */
     float in2[2] = {0.f, 0.f}, out2[2];
+    try { filter_a.Process(in2, out2); } catch (const olfx::Error &e) { code = e.code(); }
+    EXPECT_EQ(code, OLFX_E_STATE);
+    code = 0;
+    ol::fx::FilterFx<2> lone;                          /* ... and a lone one needs its Init */
     try { lone.Process(in2, out2); } catch (const olfx::Error &e) { code = e.code(); }
     EXPECT_EQ(code, OLFX_E_STATE);
+}
+
+/* The Daisy synth firmware, ol_daisy/app/synth/main.cpp: its objects built as it builds them
+   (:48-67), its voice set-up before Init (:114-128, 149-152), MIDI control changes fanned out to all
+   four objects as handleMidi does (:201-207), and the body of audio_callback (:78-88) run verbatim
+   over an interleaved AUDIO_BLOCK_SIZE buffer.  The objects are the GPU's (olfx_ref.hpp): the four
+   MoogFilter voices one generation, delay_fx / reverb_fx / filter_fx standalone rack instances
+   (OLFX_FR_TOPOLOGY 2 / 3 / 4), each object one block late.
+   Checks: (1) the fx chain is bit-exact against oracle/fxrack_ref.c topology 1 (the firmware's
+   chain as one instance) fed the voices' GPU output, 3 blocks late (delay, reverb, filter);
+   (2) that voice output is within the voice tolerance of the oracle voices (4 MoogFilter
+   SynthVoices, members set before Init), 1 block late. */
+TEST(RefFirmware, SynthCallbackVerbatim) {
+    const uint32_t kBlocks = 10, F = kBlocks * B;
+    struct DelayLine { int dummy; } delay_line1;        /* stands for daisysp::DelayLine<t_sample, 48000> */
+    struct ReverbSc { int dummy; } verb;                /* stands for daisysp::ReverbSc */
+    /* ---- main.cpp:48-67, verbatim but for the two stand-in types ---- */
+    ol::synth::SynthVoice v1(new ol::synth::OscillatorSoundSource(), new ol::synth::MoogFilter());
+    ol::synth::SynthVoice v2(new ol::synth::OscillatorSoundSource(), new ol::synth::MoogFilter());
+    ol::synth::SynthVoice v3(new ol::synth::OscillatorSoundSource(), new ol::synth::MoogFilter());
+    ol::synth::SynthVoice v4(new ol::synth::OscillatorSoundSource(), new ol::synth::MoogFilter());
+    std::vector<ol::synth::Voice *> voices{&v1, &v2, &v3, &v4};
+    ol::synth::Polyvoice voice(voices);
+    std::vector<DelayLine *> delay_lines{&delay_line1};
+    ol::fx::DelayFx<1> delay_fx(delay_lines);
+    ol::fx::DaisyVerb<2> daisy_verb(verb);
+    ol::fx::ReverbFx<2> reverb_fx(daisy_verb);
+    ol::fx::FilterFx<2> filter_fx;
+    t_sample mono = 0;
+    t_sample stereo[]{0, 0};
+    auto audio_callback = [&](const float *in, float *out, size_t size) {
+        (void)in;
+        /* ---- main.cpp:78-88, the loop body verbatim ---- */
+        for (size_t i = 0; i < size; i += 2) {
+            mono = 0;
+            voice.Process(&mono);
+
+            delay_fx.Process(&mono, &mono);
+            stereo[0] = stereo[1] = mono;
+            reverb_fx.Process(stereo, stereo);
+            filter_fx.Process(stereo, stereo);
+            out[i] = stereo[0];
+            out[i + 1] = stereo[1];
+        }
+    };
+    /* ---- main.cpp:114-128, 149-152 ---- */
+    voice.UpdateMidiControl(CC_CTL_PORTAMENTO, 48);
+    voice.UpdateMidiControl(CC_FILTER_CUTOFF, 0);
+    voice.UpdateMidiControl(CC_FILTER_RESONANCE, 0);
+    voice.UpdateMidiControl(CC_ENV_FILT_A, 0);
+    voice.UpdateMidiControl(CC_ENV_FILT_D, 100);
+    voice.UpdateMidiControl(CC_ENV_FILT_S, 0);
+    voice.UpdateMidiControl(CC_ENV_FILT_R, 24);
+    voice.UpdateMidiControl(CC_ENV_FILT_AMT, 127);
+    voice.UpdateMidiControl(CC_ENV_AMP_A, 0);
+    voice.UpdateMidiControl(CC_ENV_AMP_D, 127);
+    voice.UpdateMidiControl(CC_ENV_AMP_S, 127);
+    voice.UpdateMidiControl(CC_ENV_AMP_R, 100);
+    voice.UpdateMidiControl(CC_OSC_1_VOLUME, 100);
+    voice.UpdateMidiControl(CC_CTL_VOLUME, 80);
+    const float sample_rate = 48000.f;
+    voice.Init(sample_rate);
+    delay_fx.Init(sample_rate);
+    reverb_fx.Init(sample_rate);
+    filter_fx.Init(sample_rate);
+    /* handleMidi (main.cpp:190-207): notes to the Polyvoice, every CC to all four objects */
+    auto cc = [&](uint8_t c, uint8_t v) {
+        voice.UpdateMidiControl(c, v);
+        delay_fx.UpdateMidiControl(c, v);
+        reverb_fx.UpdateMidiControl(c, v);
+        filter_fx.UpdateMidiControl(c, v);
+    };
+    std::vector<float> out(2 * (size_t)F);
+    const size_t size = 2 * 128;                        /* AUDIO_BLOCK_SIZE 128, interleaved (main.cpp:22) */
+    for (uint32_t f0 = 0; f0 < F; f0 += 128) {
+        if (f0 == 0) { voice.NoteOn(48, 100); voice.NoteOn(55, 90); }
+        if (f0 == 2 * B) { cc(CC_DELAY_TIME, 3); cc(CC_DELAY_FEEDBACK, 80); cc(CC_REVERB_BALANCE, 70); }
+        if (f0 == 3 * B + 128) { cc(CC_FILTER_CUTOFF, 50); cc(CC_FILTER_RESONANCE, 40); voice.NoteOn(60, 100); }
+        if (f0 == 5 * B) { cc(CC_FILTER_TYPE, 60); cc(CC_DELAY_BALANCE, 100); voice.NoteOff(48, 0); }
+        audio_callback(nullptr, out.data() + 2 * (size_t)f0, size);
+    }
+
+    /* (1) the voices' GPU output: the same objects, configured and driven the same way, alone */
+    ol::synth::SynthVoice w1(new ol::synth::OscillatorSoundSource(), new ol::synth::MoogFilter());
+    ol::synth::SynthVoice w2(new ol::synth::OscillatorSoundSource(), new ol::synth::MoogFilter());
+    ol::synth::SynthVoice w3(new ol::synth::OscillatorSoundSource(), new ol::synth::MoogFilter());
+    ol::synth::SynthVoice w4(new ol::synth::OscillatorSoundSource(), new ol::synth::MoogFilter());
+    std::vector<ol::synth::Voice *> wv{&w1, &w2, &w3, &w4};
+    ol::synth::Polyvoice wpoly(wv);
+    const uint8_t setup[][2] = {{CC_CTL_PORTAMENTO, 48}, {CC_FILTER_CUTOFF, 0}, {CC_FILTER_RESONANCE, 0},
+                                {CC_ENV_FILT_A, 0}, {CC_ENV_FILT_D, 100}, {CC_ENV_FILT_S, 0}, {CC_ENV_FILT_R, 24},
+                                {CC_ENV_FILT_AMT, 127}, {CC_ENV_AMP_A, 0}, {CC_ENV_AMP_D, 127}, {CC_ENV_AMP_S, 127},
+                                {CC_ENV_AMP_R, 100}, {CC_OSC_1_VOLUME, 100}, {CC_CTL_VOLUME, 80}};
+    for (auto &c : setup) wpoly.UpdateMidiControl(c[0], c[1]);
+    wpoly.Init(sample_rate);
+    std::vector<float> m(F);
+    for (uint32_t t = 0; t < F; ++t) {
+        if (t == 0) { wpoly.NoteOn(48, 100); wpoly.NoteOn(55, 90); }
+        if (t == 3 * B + 128) { wpoly.UpdateMidiControl(CC_FILTER_CUTOFF, 50); wpoly.UpdateMidiControl(CC_FILTER_RESONANCE, 40);
+                                wpoly.NoteOn(60, 100); }
+        if (t == 5 * B) { wpoly.UpdateMidiControl(CC_FILTER_TYPE, 60); wpoly.NoteOff(48, 0); }
+        if (t == 2 * B) { wpoly.UpdateMidiControl(CC_DELAY_TIME, 3); wpoly.UpdateMidiControl(CC_DELAY_FEEDBACK, 80);
+                          wpoly.UpdateMidiControl(CC_REVERB_BALANCE, 70); }
+        if (t == 5 * B) wpoly.UpdateMidiControl(CC_DELAY_BALANCE, 100);
+        float s = 0.f;
+        wpoly.Process(&s);
+        m[t] = s;
+    }
+    /* The chain oracle: one topology-1 rack instance fed delay_fx's input stream, which is m (both
+       are the Polyvoice's output at the caller's frame).  Each fx object is one block late, so
+       reverb_fx sees the chain's input one block behind and filter_fx two: a control that lands at
+       caller boundary T reaches the chain's input frame T (delay_fx), T - B (reverb_fx) or T - 2B
+       (filter_fx); the chain's output frame t is out[t + 3B]. */
+    oracle_fxrack *ref = oracle_fxrack_create(1, sample_rate);
+    oracle_fxrack_set(ref, 0, OFR_TOPOLOGY, 1.f);
+    std::vector<float> yr(2 * (size_t)F, 0.f);
+    auto at = [&](uint32_t t) {
+        if (t == 2 * B) { oracle_fxrack_set(ref, 0, OFR_DELAY_TIME, ol::core::scale(3, 0, 127, 0, 1, 1));
+                          oracle_fxrack_set(ref, 0, OFR_DELAY_FEEDBACK, ol::core::scale(80, 0, 127, 0, 1, 1)); }
+        if (t == 2 * B - B) oracle_fxrack_set(ref, 0, OFR_REVERB_BALANCE, ol::core::scale(70, 0, 127, 0, 1, 1));
+        /* called mid-block at 3B + 128: lands at 4B */
+        if (t == 4 * B - 2 * B) { oracle_fxrack_set(ref, 0, OFR_FILTER_CUTOFF, ol::core::scale(50, 0, 127, 0, 20000, 1));
+                                  oracle_fxrack_set(ref, 0, OFR_FILTER_RESONANCE, ol::core::scale(40, 0, 127, 0, 1, 1)); }
+        if (t == 5 * B - 2 * B) oracle_fxrack_set(ref, 0, OFR_FILTER_TYPE, (float)(int)ol::core::scale(60, 0, 127, 0, 5, 1));
+        if (t == 5 * B) oracle_fxrack_set(ref, 0, OFR_DELAY_BALANCE, ol::core::scale(100, 0, 127, 0, 1, 1));
+    };
+    for (uint32_t t = 0; t + 3 * B < F; ++t) {
+        at(t);
+        const float x[2] = {m[t], 0.f};
+        float y[2];
+        oracle_fxrack_process(ref, x, y, 1, 1);
+        yr[2 * (size_t)(t + 3 * B)] = y[0];
+        yr[2 * (size_t)(t + 3 * B) + 1] = y[1];
+    }
+    oracle_fxrack_destroy(ref);
+    const size_t bad = first_bit_mismatch(out, yr);
+    if (bad != (size_t)-1) std::printf("  first mismatch at %zu: %.9g vs %.9g\n", bad, out[bad], yr[bad]);
+    EXPECT_TRUE(bad == (size_t)-1);
+    bool moving = false;
+    for (uint32_t t = 5 * B; t < F; ++t) moving = moving || out[2 * (size_t)t] != 0.f;
+    EXPECT_TRUE(moving);
+
+    /* (2) the voices against the oracle: members set before Init (no Update), then the notes */
+    OracleVoices vref({1, 1, 1, 1});
+    float mem[OVC_NPARAMS] = {0.f, 0.f, 0.f, 1.f, 0.f, 1.f, 0.2f, 0.f, 0.f, 0.8f, 0.01f, 1.f, 0.f, 1.f, 0.01f, 0.f};
+    mem[OVC_PORTAMENTO] = ol::core::scale(48, 0, 127, 0, 1, 4);          /* SynthVoice.h:164-229 */
+    mem[OVC_FILTER_CUTOFF] = ol::core::scale(0, 0, 127, 0, 20000, 2.5);
+    mem[OVC_FILTER_RESONANCE] = 0.f;
+    mem[OVC_FILTER_ATTACK] = 0.f;
+    mem[OVC_FILTER_DECAY] = ol::core::scale(100, 0, 127, 0, 1, 3);
+    mem[OVC_FILTER_SUSTAIN] = 0.f;
+    mem[OVC_FILTER_RELEASE] = ol::core::scale(24, 0, 127, 0, 1, 1);
+    mem[OVC_FILTER_ENV_AMOUNT] = ol::core::scale(127, 0, 127, 0, 1, 1);
+    mem[OVC_AMP_ATTACK] = 0.f;
+    mem[OVC_AMP_DECAY] = ol::core::scale(127, 0, 127, 0, 1, 1);
+    mem[OVC_AMP_SUSTAIN] = ol::core::scale(127, 0, 127, 0, 1, 1);
+    mem[OVC_AMP_RELEASE] = ol::core::scale(100, 0, 127, 0, 1, 1);
+    mem[OVC_AMP_ENV_AMOUNT] = ol::core::scale(80, 0, 127, 0, 1, 1);
+    for (size_t v = 0; v < 4; ++v) oracle_voice_init_members(vref.of(v), vref.slot[v], mem);
+    std::vector<float> mr(F, 0.f);
+    for (uint32_t t = 0; t + B < F; ++t) {
+        if (t == 0) { vref.event(0, 1, 48); vref.event(1, 1, 55); }
+        if (t == 4 * B) {                               /* CUTOFF / RESONANCE -> Update() of every voice */
+            for (size_t v = 0; v < 4; ++v) {
+                float cfg[OVC_NPARAMS];
+                std::memcpy(cfg, mem, sizeof cfg);
+                cfg[OVC_FILTER_CUTOFF] = ol::core::scale(50, 0, 127, 0, 20000, 2.5);
+                cfg[OVC_FILTER_RESONANCE] = ol::core::scale(40, 0, 127, 0, 1, 1);
+                oracle_voice_config(vref.of(v), vref.slot[v], cfg);
+            }
+            vref.event(2, 1, 60);
+        }
+        if (t == 5 * B) vref.event(0, 0, 48);
+        const std::vector<float> f = vref.frame();
+        float s = 0.f;
+        for (float x : f) s += x;
+        mr[t] = s;
+    }
+    EXPECT_TRUE(close_delayed(m, mr, F, "firmware voices (members before Init)"));
 }
 
 /* ol::fx::ChorusFx<2> (stereo) and <1> (mono: L = R = x, out = L) against the chorus oracle. */

@@ -58,7 +58,7 @@ def test_library_has_gfx950_code_object():
 
 def test_abi_version_and_kind_info():
     lib = ofx.load()
-    assert lib.olfx_abi_version() == 1
+    assert lib.olfx_abi_version() == 2
     info = ofx.kind_info(ofx.KIND_DATTORRO)
     assert (info.n_params, info.in_channels, info.out_channels) == (7, 2, 2)
     # 42,368 ring floats + 3 recursive scalars + 7 coefficients per instance

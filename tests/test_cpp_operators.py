@@ -79,12 +79,13 @@ def test_ref_surface_compiles_against_reference_headers_and_fails_loudly_without
 @pytest.mark.gpu
 def test_ref_surface_on_gpu():
     """Reference-typed classes on the GPU: Polyvoice / VoiceMap sums, Voice gate / pitch calls,
-    FxRack<2>(DelayFx&, ReverbFx&, FilterFx&) controls, ChorusFx<1|2>, vs the oracle one block late."""
+    FxRack<2>(DelayFx&, ReverbFx&, FilterFx&) controls, ChorusFx<1|2>, vs the oracle one block late; the
+    Daisy firmware's audio callback verbatim over standalone DelayFx<1> / ReverbFx<2> / FilterFx<2>."""
     _build_ref()
     r = subprocess.run([REF_BIN], capture_output=True, text=True, timeout=600)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "5 tests, 0 failures" in r.stdout
+    assert "6 tests, 0 failures" in r.stdout
 
 
 def test_ref_header_standalone_without_gpu():
