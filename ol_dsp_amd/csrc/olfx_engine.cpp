@@ -353,7 +353,7 @@ struct olfx_engine {
     uint32_t block = 0;
     float sr = 48000.f;
     hipStream_t stream = nullptr;
-    hipEvent_t done = nullptr;            // recorded after each olfx_process's work, on its stream
+    hipStream_t copy_stream = nullptr;    // copies of large control packets
     uint64_t frames = 0;
     std::string err;
 
@@ -370,15 +370,29 @@ struct olfx_engine {
     // control packets: a block's changed coefficients and folded note events, in pinned host
     // slots the block's kernels read (submit_control).  A slot is rewritten only after the
     // kernels that read it are done (consumed).
-    static constexpr int kSlots = 4;
+    // 16 slots in groups of 4: one `consumed` marker per group (each marker is a command-processor
+    // packet between two blocks' kernels), recorded after the group's last packet or when the
+    // caller switches streams; a slot's guard is its group's marker
+    static constexpr int kSlots = 16, kGroup = 4, kBig = 2;
+    static constexpr size_t kCopyBytes = 64 * 1024;   // packets from this size on are copied
+    size_t copy_bytes = kCopyBytes;                  // OLFX_COPY_BYTES overrides (A/B diagnostic)
     struct Slot {
-        uint32_t *h = nullptr, *d = nullptr;
-        bool d_owned = false;
-        size_t cap = 0;                   // words
+        uint32_t *h = nullptr, *hd = nullptr;   // pinned host half and its device address
+        uint32_t *d = nullptr;                  // device half (large packets), allocated on first need
+        size_t cap = 0, dcap = 0;               // words
         hipEvent_t copied = nullptr, consumed = nullptr;
+        hipEvent_t guard = nullptr;             // the marker after this slot's last readers
         bool used = false;
-    } slot[kSlots];
-    int slot_next = 0;
+    } slot[kSlots], big[kBig];                  // small packets (zero-copy) / large ones (copied)
+    int slot_next = 0, big_next = 0;
+    template <class F>
+    void each_slot(F &&f) {
+        for (Slot &x : slot) f(x);
+        for (Slot &x : big) f(x);
+    }
+    int pending[kGroup] = {};                   // slots used since the last marker, all on pending_stream
+    int n_pending = 0;
+    hipStream_t pending_stream = nullptr;
     std::vector<int32_t> ev_slot;         // voice -> its record in `folded` during fold_events, else -1
     struct Folded { uint32_t inst, op, freq, pad; };
     std::vector<Folded> folded, ev_sorted;
@@ -387,8 +401,6 @@ struct olfx_engine {
     // OLFX_TRACE_CONTROL=1 (read at create): host time of each control-path step, summed and
     // printed to stderr at destroy (tracing)
     bool trace = false;
-    int ctl_mode = 2;                     // OLFX_CTL_MODE (A/B diagnostic): 1 copy on the caller's stream,
-                                          // 2 pinned host memory read by the kernels
     double tr[6] = {0, 0, 0, 0, 0, 0};
     uint64_t tr_calls = 0;
 
@@ -603,6 +615,65 @@ void fold_events(olfx_engine *e) {
     for (const olfx_engine::Folded &r : e->folded) e->ev_sorted[e->ev_fill[r.inst >> 6]++] = r;
 }
 
+// Record one marker after the pending slots' kernels (on their stream) and make it their guard.
+hipError_t flush_markers(olfx_engine *e) {
+    if (!e->n_pending) return hipSuccess;
+    hipEvent_t m = e->slot[e->pending[e->n_pending - 1]].consumed;
+    const hipError_t r = hipEventRecord(m, e->pending_stream);
+    for (int k = 0; k < e->n_pending; ++k) e->slot[e->pending[k]].guard = r == hipSuccess ? m : nullptr;
+    e->n_pending = 0;
+    return r;
+}
+
+// A block's kernels that read slot `sl` are queued on `s`: a big slot gets its own marker, a small
+// one joins the pending group.
+hipError_t slot_queued(olfx_engine *e, olfx_engine::Slot *sl, hipStream_t s) {
+    if (sl >= e->big && sl < e->big + olfx_engine::kBig) {
+        const hipError_t r = hipEventRecord(sl->consumed, s);
+        sl->guard = r == hipSuccess ? sl->consumed : nullptr;
+        return r;
+    }
+    hipError_t r = hipSuccess;
+    if (e->n_pending && e->pending_stream != s) r = flush_markers(e);
+    e->pending[e->n_pending++] = (int)(sl - e->slot);
+    e->pending_stream = s;
+    if (e->n_pending == olfx_engine::kGroup) {
+        const hipError_t r2 = flush_markers(e);
+        if (r == hipSuccess) r = r2;
+    }
+    return r;
+}
+
+// A slot's pinned half (and, for copied packets, its device half) of at least `words` words.
+int grow_slot(olfx_engine *e, olfx_engine::Slot &sl, size_t words, bool device_half) {
+    if (sl.cap < words) {
+        if (sl.h) (void)hipHostFree(sl.h);
+        sl.h = nullptr; sl.hd = nullptr; sl.cap = 0;
+        const size_t cap = std::max<size_t>(words, 4096);
+        HIPCHK(e, hipHostMalloc((void **)&sl.h, cap * 4, hipHostMallocDefault));
+        void *dp = nullptr;
+        HIPCHK(e, hipHostGetDevicePointer(&dp, sl.h, 0));
+        sl.hd = (uint32_t *)dp;
+        sl.cap = cap;
+    }
+    if (device_half && sl.dcap < sl.cap) {
+        if (sl.d) (void)hipFree(sl.d);
+        sl.d = nullptr; sl.dcap = 0;
+        HIPCHK(e, hipMalloc((void **)&sl.d, sl.cap * 4));
+        sl.dcap = sl.cap;
+    }
+    return OLFX_OK;
+}
+
+// The largest control packet an engine can produce: every instance's coefficients and, for voices,
+// an event for every voice (submit_control's layout, rounded up).
+size_t max_packet_words(const olfx_engine *e) {
+    CoefScatterArgs ca{};
+    const size_t n = e->n, W = coef_segments(e, &ca);
+    const size_t ev = is_voice_kind(e->kind) ? (n + 63) / 64 + 1 + 4 * n : 0;
+    return n + W * n + ev + 16;
+}
+
 // This block's control packet -- the changed instances' coefficient records and the folded note
 // events -- in a pinned host slot that the block's kernels read directly over the host link
 // (zero-copy: no copy command, no second stream, no host wait on the device).  The coefficients are
@@ -640,28 +711,25 @@ int submit_control(olfx_engine *e, hipStream_t s, VoiceArgs *va, olfx_engine::Sl
     const size_t o_ev = up4(o_off + (mev ? groups + 1 : 0));
     const size_t words = o_ev + 4 * mev;
 
-    olfx_engine::Slot &sl = e->slot[e->slot_next];
-    e->slot_next = (e->slot_next + 1) % olfx_engine::kSlots;
-    const int mode = e->ctl_mode;
-    if (sl.used) HIPCHK(e, hipEventSynchronize(mode == 2 ? sl.consumed : sl.copied));   // the host half is free
-    lap(1);
-    if (sl.cap < words) {
-        if (sl.used) HIPCHK(e, hipEventSynchronize(sl.consumed));  // the device half too
-        if (sl.h) (void)hipHostFree(sl.h);
-        if (sl.d && sl.d_owned) (void)hipFree(sl.d);
-        sl.h = nullptr; sl.d = nullptr; sl.cap = 0; sl.used = false; sl.d_owned = false;
-        const size_t cap = std::max<size_t>(words + words / 2, 4096);
-        HIPCHK(e, hipHostMalloc((void **)&sl.h, cap * 4, hipHostMallocDefault));
-        if (mode == 2) {         // the kernels read the pinned host memory
-            void *dp = nullptr;
-            HIPCHK(e, hipHostGetDevicePointer(&dp, sl.h, 0));
-            sl.d = (uint32_t *)dp;
-        } else {
-            HIPCHK(e, hipMalloc((void **)&sl.d, cap * 4));
-            sl.d_owned = true;
-        }
-        sl.cap = cap;
+    // Delivery: a small packet (a block's CCs / notes) is read by the kernels straight from a pinned
+    // slot -- no copy command: ~2 us of host time, a host-link round trip or two inside the kernel.
+    // A large one (the first block's full upload, an all-voices note-off) goes to one of two big
+    // slots and is copied into its device half on the engine's copy stream, which the caller's
+    // stream waits for: ~20 us of host API time, but no 512-KB read over the host link on the
+    // kernel's critical path.
+    const bool copy = words * 4 >= e->copy_bytes;
+    olfx_engine::Slot &sl = copy ? e->big[e->big_next] : e->slot[e->slot_next];
+    if (copy) e->big_next = (e->big_next + 1) % olfx_engine::kBig;
+    else e->slot_next = (e->slot_next + 1) % olfx_engine::kSlots;
+    // the slot is free once the kernels that read it are done (both halves)
+    if (sl.used) {
+        if (!sl.guard) HIPCHK(e, flush_markers(e));
+        if (sl.guard) HIPCHK(e, hipEventSynchronize(sl.guard));
+        else HIPCHK(e, hipDeviceSynchronize());     // its marker failed to record: wait for everything
     }
+    lap(1);
+    if (const int rc = grow_slot(e, sl, words, copy)) return rc;
+    uint32_t *const dev = copy ? sl.d : sl.hd;      // what the kernels read
     lap(2);
     // coefficient records, field-major [W][m]
     uint32_t *val = sl.h + o_val;
@@ -679,26 +747,30 @@ int submit_control(olfx_engine *e, hipStream_t s, VoiceArgs *va, olfx_engine::Sl
         std::memcpy(sl.h + o_off, e->ev_off.data(), (groups + 1) * 4);
         std::memcpy(sl.h + o_ev, e->ev_sorted.data(), mev * 16);
     }
-    if (mode == 2) {
-        std::atomic_thread_fence(std::memory_order_seq_cst);     // the packet's stores before the launch
+    if (copy) {
+        // the copy stream waits for nothing on the device: the host made sure above that the slot's
+        // previous readers are done (a device-side wait there serialised the copy behind them)
+        HIPCHK(e, hipMemcpyAsync(sl.d, sl.h, words * 4, hipMemcpyHostToDevice, e->copy_stream));
+        HIPCHK(e, hipEventRecord(sl.copied, e->copy_stream));
+        HIPCHK(e, hipStreamWaitEvent(s, sl.copied, 0));
     } else {
-        HIPCHK(e, hipMemcpyAsync(sl.d, sl.h, words * 4, hipMemcpyHostToDevice, s));
-        HIPCHK(e, hipEventRecord(sl.copied, s));
+        std::atomic_thread_fence(std::memory_order_seq_cst);     // the packet's stores before the launch
     }
     sl.used = true;
+    sl.guard = nullptr;
     *used_slot = &sl;
     lap(4);
     if (m) {
-        ca.inst = dense ? nullptr : sl.d + o_inst;
-        ca.val = sl.d + o_val;
+        ca.inst = dense ? nullptr : dev + o_inst;
+        ca.val = dev + o_val;
         ca.m = (uint32_t)m;
         ca.W = W;
         const hipError_t r = launch_coef_scatter(ca, s);
         if (r != hipSuccess) return e->hip_fail(r, "coefficient scatter launch");
     }
     if (mev) {
-        va->ev_off = sl.d + o_off;
-        va->ev = reinterpret_cast<const uint4 *>(sl.d + o_ev);
+        va->ev_off = dev + o_off;
+        va->ev = reinterpret_cast<const uint4 *>(dev + o_ev);
     }
     lap(5);
     return OLFX_OK;
@@ -706,8 +778,9 @@ int submit_control(olfx_engine *e, hipStream_t s, VoiceArgs *va, olfx_engine::Sl
 
 int init_state(olfx_engine *e) {
     // all of the engine's earlier work (on any stream) is done: control slots included
-    for (olfx_engine::Slot &sl : e->slot)
-        if (sl.used) HIPCHK(e, hipEventSynchronize(sl.consumed));
+    HIPCHK(e, hipDeviceSynchronize());
+    e->n_pending = 0;
+    e->each_slot([](olfx_engine::Slot &sl) { sl.used = false; sl.guard = nullptr; });
     HIPCHK(e, hipMemsetAsync(e->d_mem, 0, e->d_bytes, e->stream));
     // voices: daisysp Oscillator::Init phase 0; Svf::Init states 0; Adsr idle; freq_ = 0
     // (SynthVoice.h:276); Port z1 = 0 -- all zeros
@@ -964,18 +1037,19 @@ int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32
     e->sr = sample_rate;
     e->n_params = n_params_of(kind);
     e->trace = std::getenv("OLFX_TRACE_CONTROL") && std::getenv("OLFX_TRACE_CONTROL")[0] == '1';
-    if (const char *m = std::getenv("OLFX_CTL_MODE")) e->ctl_mode = std::atoi(m) == 1 ? 1 : 2;
+    if (const char *cb = std::getenv("OLFX_COPY_BYTES"))
+        e->copy_bytes = std::min<size_t>((size_t)std::strtoull(cb, nullptr, 10), olfx_engine::kCopyBytes);
     chorus_sizes(sample_rate, &e->psize, &e->csize);
     e->n_dt = kind == OLFX_KIND_CHAIN ? (n_inst + 63u) & ~63u : n_inst;
 
     hipError_t r = hipSetDevice(device);
     if (r == hipSuccess) r = hipDeviceGetAttribute(&e->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
-    if (r == hipSuccess) r = hipEventCreateWithFlags(&e->done, hipEventDisableTiming);
-    for (olfx_engine::Slot &sl : e->slot) {
-        if (r == hipSuccess) r = hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming);
-        if (r == hipSuccess) r = hipEventCreateWithFlags(&sl.consumed, hipEventDisableTiming);
-    }
+    if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking);
+    e->each_slot([&](olfx_engine::Slot &x) {
+        if (r == hipSuccess) r = hipEventCreateWithFlags(&x.copied, hipEventDisableTiming);
+        if (r == hipSuccess) r = hipEventCreateWithFlags(&x.consumed, hipEventDisableTiming);
+    });
     if (r != hipSuccess) {
         int rc = e->hip_fail(r, "olfx_create: stream / events");
         olfx_destroy(e);
@@ -1055,6 +1129,15 @@ int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32
         e->vc_coef = (float *)(base + o_vc_c);
     }
     int rc = init_state(e);
+    // slots allocated now, so that no block -- an all-voices note-off in the middle of a stream,
+    // say -- pays a pinned / device allocation: the small ones at the copy threshold, the big ones
+    // for the largest packet this engine can produce (up to 256 MiB each; larger on first need)
+    const size_t maxw = max_packet_words(e);
+    for (olfx_engine::Slot &sl : e->slot)
+        if (!rc) rc = grow_slot(e, sl, olfx_engine::kCopyBytes / 4, false);
+    if (maxw * 4 >= e->copy_bytes && maxw * 4 <= ((size_t)256 << 20))
+        for (olfx_engine::Slot &sl : e->big)
+            if (!rc) rc = grow_slot(e, sl, maxw, true);
     if (rc) {
         olfx_destroy(e);
         return rc;
@@ -1072,19 +1155,17 @@ int olfx_destroy(olfx_engine *e) {
                      e->tr[2] / e->tr_calls, e->tr[3] / e->tr_calls, e->tr[4] / e->tr_calls, e->tr[5] / e->tr_calls);
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    if (e->done) (void)hipEventSynchronize(e->done);          // the last block, on the caller's stream
+    // the engine's work may sit on any caller stream: wait for the device (no per-call marker on
+    // the caller's stream -- each one is a command-processor packet between two blocks' kernels)
+    (void)hipDeviceSynchronize();
     if (e->mix_done) (void)hipEventSynchronize(e->mix_done);
-    for (olfx_engine::Slot &sl : e->slot) {
-        if (sl.used) {
-            (void)hipEventSynchronize(sl.copied);
-            (void)hipEventSynchronize(sl.consumed);
-        }
+    e->each_slot([](olfx_engine::Slot &sl) {
         if (sl.h) (void)hipHostFree(sl.h);
-        if (sl.d && sl.d_owned) (void)hipFree(sl.d);
+        if (sl.d) (void)hipFree(sl.d);
         if (sl.copied) (void)hipEventDestroy(sl.copied);
         if (sl.consumed) (void)hipEventDestroy(sl.consumed);
-    }
-    if (e->done) (void)hipEventDestroy(e->done);
+    });
+    if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
     if (e->tile_in) (void)hipFree(e->tile_in);
     if (e->tile_out) (void)hipFree(e->tile_out);
     if (e->d_mem) (void)hipFree(e->d_mem);
@@ -1103,7 +1184,7 @@ int olfx_reset(olfx_engine *e) {
     if (!e) return OLFX_E_ARG;
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    HIPCHK(e, hipEventSynchronize(e->done));                    // the last block, on any stream
+    HIPCHK(e, hipDeviceSynchronize());                          // the last block, on any stream
     return init_state(e);
 }
 
@@ -1361,7 +1442,7 @@ int olfx_process(olfx_engine *e, const float *in, float *out, uint32_t n_frames,
     // the slot is free again once whatever was queued on `s` (the scatter, the kernels) is done --
     // recorded on the error paths too, so a later block never overwrites a packet still being read
     if (sl) {
-        const hipError_t r = hipEventRecord(sl->consumed, s);
+        const hipError_t r = slot_queued(e, sl, s);
         if (!rc && r != hipSuccess) rc = e->hip_fail(r, "hipEventRecord(consumed)");
     }
     if (rc) return rc;
@@ -1370,7 +1451,6 @@ int olfx_process(olfx_engine *e, const float *in, float *out, uint32_t n_frames,
         HIPCHK(e, hipStreamSynchronize(s));
         std::memcpy(out, e->h_out, fout * 4);
     }
-    HIPCHK(e, hipEventRecord(e->done, s));
     return OLFX_OK;
 }
 

@@ -144,9 +144,11 @@ int run_block(Generation *g) {
     if (rc) return engine_fail(g, rc, "olfx_process");
     g->complete.store(0, std::memory_order_relaxed);
     g->filling.store(false, std::memory_order_relaxed);
-    for (olfx_sample *m : g->members)
-        if (m) m->pos.store(0, std::memory_order_relaxed);
+    // publish the new block count first, then each member's pos = 0 with release: a member that
+    // reads its pos 0 (acquire) also sees the new count and this run's outputs
     g->blocks.store(b + 1, std::memory_order_release);
+    for (olfx_sample *m : g->members)
+        if (m) m->pos.store(0, std::memory_order_release);
     return apply_pending(g);
 }
 
@@ -283,7 +285,9 @@ int olfx_sample_process(olfx_sample *s, const float *in, float *out) {
             if (rc) return rc;
         }
     }
-    const uint32_t pos = s->pos.load(std::memory_order_relaxed);
+    // pos first (acquire, pairs with run_block's release of pos = 0), then the block count: a reset
+    // pos is never seen with the previous count (the output buffer of the wrong parity)
+    const uint32_t pos = s->pos.load(std::memory_order_acquire);
     const uint64_t blocks = g->blocks.load(std::memory_order_acquire);
     if (pos == g->block) {
         char buf[256];

@@ -42,7 +42,7 @@ for m in "$@"; do
       step bench_ctl 600 python bench.py --steps 20 --warmup 5 --workload voice --also voice_events,chain,chain_cc \
           --cpu-seconds 0 ;;
     ctl_ab)   # control-packet delivery A/B (OLFX_CTL_MODE 1: copy on the stream, 2: zero-copy)
-      for cm in 2 1; do
+      for cm in ${CTL_MODES:-0}; do
         step "pytest_ctl_m$cm" 600 env OLFX_CTL_MODE=$cm python -u -m pytest tests/test_gpu_control.py -m gpu -x -q \
             -p no:cacheprovider --timeout 300 --timeout-method thread -k "not tiled"
         step "bench_ctl_m$cm" 600 env OLFX_CTL_MODE=$cm OLFX_TRACE_CONTROL=1 python bench.py --steps 20 --warmup 5 \
