@@ -118,8 +118,8 @@ int main() {
         for (uint32_t k = 0; t0 < F; ++k) {
             const uint32_t m = std::min(sizes[k % 8], F - t0);
             std::vector<float> xb(2 * (size_t)m * n), yb(xb.size()), xi(xb.size()), yi(xb.size());
-            for (uint32_t c = 0; c < 2; ++c)
-                std::memcpy(&xb[(size_t)c * m * n], &x[((size_t)c * F + t0) * n], (size_t)m * n * 4);
+            for (uint32_t c = 0; c < 2 && m; ++c)    // (a zero-frame callback copies nothing)
+                std::memcpy(xb.data() + (size_t)c * m * n, x.data() + ((size_t)c * F + t0) * n, (size_t)m * n * 4);
             for (uint32_t f = 0; f < m; ++f)          // [f][i][c]
                 for (uint32_t i = 0; i < n; ++i)
                     for (uint32_t c = 0; c < 2; ++c) xi[((size_t)f * n + i) * 2 + c] = xb[((size_t)c * m + f) * n + i];
