@@ -45,23 +45,27 @@ struct PlanL {
     bool okA, okB;
 };
 
+// 64-bit phasors (2^64 = one cycle): the float phase is the top 24 bits of the high word, exact
+__device__ __forceinline__ float unit24h(uint64_t acc) { return unit24((uint32_t)(acc >> 32)); }
+constexpr uint64_t kHalfCycle = 0x8000000000000000ull;
+
 template <int kWin>
-__device__ __forceinline__ PlanL plan_chunk_l(uint32_t lfo_acc, uint32_t lfo_inc, uint32_t lfo_off, uint32_t ps_acc,
-                                              uint32_t ps_inc, int C, float D, float W, float pmax, float cmax,
+__device__ __forceinline__ PlanL plan_chunk_l(uint64_t lfo_acc, uint64_t lfo_inc, uint64_t lfo_off, uint64_t ps_acc,
+                                              uint64_t ps_inc, int C, float D, float W, float pmax, float cmax,
                                               bool full) {
     PlanL p;
     const uint32_t last = (uint32_t)(C - 1);
     // pitch taps: the floor delay is non-decreasing over the chunk unless the phasor wraps
     {
-        const uint32_t a0 = ps_acc, a1 = ps_acc + last * ps_inc;
-        const int d0 = floor_delay(unit24(a0) * W, 1.0f, pmax), d1 = floor_delay(unit24(a1) * W, 1.0f, pmax);
+        const uint64_t a0 = ps_acc, a1 = ps_acc + last * ps_inc;
+        const int d0 = floor_delay(unit24h(a0) * W, 1.0f, pmax), d1 = floor_delay(unit24h(a1) * W, 1.0f, pmax);
         const int lo = -d1 - 1, hi = (int)last - d0;
         p.sA = lo & ~3;
         p.okA = a1 >= a0 && hi - p.sA < kWin;
     }
     {
-        const uint32_t a0 = ps_acc + 0x80000000u, a1 = a0 + last * ps_inc;
-        const int d0 = floor_delay(unit24(a0) * W, 1.0f, pmax), d1 = floor_delay(unit24(a1) * W, 1.0f, pmax);
+        const uint64_t a0 = ps_acc + kHalfCycle, a1 = a0 + last * ps_inc;
+        const int d0 = floor_delay(unit24h(a0) * W, 1.0f, pmax), d1 = floor_delay(unit24h(a1) * W, 1.0f, pmax);
         const int lo = -d1 - 1, hi = (int)last - d0;
         p.sB = lo & ~3;
         p.okB = a1 >= a0 && hi - p.sB < kWin;
@@ -72,8 +76,8 @@ __device__ __forceinline__ PlanL plan_chunk_l(uint32_t lfo_acc, uint32_t lfo_inc
     // frame's floor delay, and those two differ by at most one (|d'| <= 0.038 frame/frame)
     p.sC = 0; p.hiC = 0;
     if (full) {
-        const float e0 = cos2pi(unit24(lfo_acc + lfo_off)) * D + D;
-        const float e1 = cos2pi(unit24(lfo_acc + last * lfo_inc + lfo_off)) * D + D;
+        const float e0 = cos2pi(unit24h(lfo_acc + lfo_off)) * D + D;
+        const float e1 = cos2pi(unit24h(lfo_acc + last * lfo_inc + lfo_off)) * D + D;
         const int dhi = floor_delay(fmaxf(e0, e1) + 0.01f, 0.0f, cmax);
         const int dlo = floor_delay(fminf(e0, e1) - 0.01f, 0.0f, cmax);
         p.sC = (-dhi - 1) & ~3;
@@ -95,9 +99,9 @@ struct ChStageL {
 
     uint32_t lane, j, ch, inst0, n, i;
     bool valid;
-    uint32_t lfo_inc, lfo_off, ps_inc;
+    uint64_t lfo_inc, lfo_off, ps_inc;
     float D, W, b0, b1, b2, a1, a2, mix, dry;
-    uint32_t lfo_acc, ps_acc;
+    uint64_t lfo_acc, ps_acc;
     float z1, z2;
     uint32_t pmask, cmask, pshift, cshift;   // ring sizes are powers of two: instance offset = i << shift
     float pmax, cmax;
@@ -118,9 +122,9 @@ struct ChStageL {
         const uint32_t i_raw = inst0 + j;
         valid = i_raw < n;
         i = valid ? i_raw : n - 1;
-        lfo_inc = a.coef[CHC_LFO_INC * n + i];
-        lfo_off = a.coef[CHC_LFO_OFF * n + i];
-        ps_inc = a.coef[CHC_PS_INC * n + i];
+        lfo_inc = word64(a.coef[CHC_LFO_INC * n + i], a.coef[CHC_LFO_INC_LO * n + i]);
+        lfo_off = word64(a.coef[CHC_LFO_OFF * n + i], a.coef[CHC_LFO_OFF_LO * n + i]);
+        ps_inc = word64(a.coef[CHC_PS_INC * n + i], a.coef[CHC_PS_INC_LO * n + i]);
         D = __uint_as_float(a.coef[CHC_DEPTH * n + i]);
         W = __uint_as_float(a.coef[CHC_WINDOW * n + i]);
         b0 = __uint_as_float(a.coef[CHC_B0 * n + i]);
@@ -130,8 +134,8 @@ struct ChStageL {
         a2 = __uint_as_float(a.coef[CHC_A2 * n + i]);
         mix = __uint_as_float(a.coef[CHC_MIX * n + i]);
         dry = __uint_as_float(a.coef[CHC_DRY * n + i]);
-        lfo_acc = a.state[CHS_LFO_ACC * n + i];
-        ps_acc = a.state[CHS_PS_ACC * n + i];
+        lfo_acc = word64(a.state[CHS_LFO_ACC * n + i], a.state[CHS_LFO_LO * n + i]);
+        ps_acc = word64(a.state[CHS_PS_ACC * n + i], a.state[CHS_PS_LO * n + i]);
         z1 = __uint_as_float(a.state[(ch ? CHS_Z1R : CHS_Z1L) * n + i]);
         z2 = __uint_as_float(a.state[(ch ? CHS_Z2R : CHS_Z2L) * n + i]);
         pmask = a.psize - 1u; cmask = a.csize - 1u;
@@ -146,6 +150,8 @@ struct ChStageL {
         strag = 0.f;
         strag_slot = kWin;
     }
+
+    __device__ __forceinline__ static uint64_t word64(uint32_t hi, uint32_t lo) { return ((uint64_t)hi << 32) | lo; }
 
     // a window slot, or the junk slot kWin when the position lies outside the window: patches
     // write unconditionally (a select, no exec-masked block and branch per position)
@@ -284,7 +290,7 @@ struct ChStageL {
     template <int PAR>
     __device__ __forceinline__ void stores_and_next(const float (&psv)[kChunk], const float (&x)[kChunk],
                                                     const float (&xn)[kChunk], uint32_t w0, int C, int Cn,
-                                                    uint32_t lfo0, uint32_t ps0) {
+                                                    uint64_t lfo0, uint64_t ps0) {
         if (FULL) {
             stage_run(psv, kPsvBase);
             coop_store(false, kPsvBase, w0, C);
@@ -296,7 +302,7 @@ struct ChStageL {
             stage_run(xn, 0);
             coop_store(true, 0, w0 + (uint32_t)C, Cn);
         }
-        pl = plan_chunk_l<kWin>(lfo0 + (uint32_t)C * lfo_inc, lfo_inc, lfo_off, ps0 + (uint32_t)C * ps_inc,
+        pl = plan_chunk_l<kWin>(lfo0 + (uint64_t)C * lfo_inc, lfo_inc, lfo_off, ps0 + (uint64_t)C * ps_inc,
                                 ps_inc, Cn > 0 ? Cn : 4, D, W, pmax, cmax, FULL);
         // the line loads below read positions the stores above just wrote (other lanes of this
         // wave): vector memory operations of a wave reach the L1/L2 in issue order, as for the
@@ -322,7 +328,7 @@ struct ChStageL {
         j = lane >> 1;
         ch = lane & 1u;
         const uint32_t w0 = wpos;
-        const uint32_t lfo0 = lfo_acc, ps0 = ps_acc;     // the phasors at the chunk's first frame
+        const uint64_t lfo0 = lfo_acc, ps0 = ps_acc;     // the phasors at the chunk's first frame
         const PlanL cur = pl;
         float psv[kChunk];
         float *wP0 = region + 0 * kSlots * kRow + lane;
@@ -373,21 +379,22 @@ struct ChStageL {
             //     never reads a position newer than its own, so writing them all first is the same
             //     as writing each just before its frame;
             //  (C, the chorus tap, follows the ring stores and chunk c+1's line loads below)
-            // p W == (acc >> 8) (W 2^-24) exactly (scaling by a power of two is exact)
+            // p W == (hi >> 8) (W 2^-24) exactly (scaling by a power of two is exact)
             const float Ws = W * 5.9604644775390625e-8f;
             float gA0 = 0.f, gA1 = 0.f, gB0 = 0.f, gB1 = 0.f;
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) {
                 if ((k & 1) == 0) {
                     // gain arguments (p - 1/2)/2 lie in [-1/4, 1/4): cos2pi_q == cos2pi there
-                    const uint32_t pa = ps_acc + ch * ps_inc;
-                    const float m_gA = cos2pi_q((unit24(pa) - 0.5f) * 0.5f);
-                    const float m_gB = cos2pi_q((unit24(pa + 0x80000000u) - 0.5f) * 0.5f);
+                    const uint64_t pa = ps_acc + (ch ? ps_inc : 0ull);
+                    const float m_gA = cos2pi_q((unit24h(pa) - 0.5f) * 0.5f);
+                    const float m_gB = cos2pi_q((unit24h(pa + kHalfCycle) - 0.5f) * 0.5f);
                     gA0 = pair_even(m_gA); gA1 = pair_odd(m_gA);
                     gB0 = pair_even(m_gB); gB1 = pair_odd(m_gB);
                 }
-                const float d0 = (float)(ps_acc >> 8) * Ws;
-                const float d1 = (float)((ps_acc + 0x80000000u) >> 8) * Ws;
+                const uint32_t ph = (uint32_t)(ps_acc >> 32);
+                const float d0 = (float)(ph >> 8) * Ws;
+                const float d1 = (float)((ph + 0x80000000u) >> 8) * Ws;
                 ps_acc += ps_inc;
                 int di; float fr;
                 split_delay3(d0, 1.0f, pmax, di, fr);
@@ -419,10 +426,10 @@ struct ChStageL {
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) {
                 if ((k & 1) == 0) {
-                    const uint32_t la = lfo_acc + ch * lfo_inc, pa = ps_acc + ch * ps_inc;
-                    const float m_lfo = cos2pi(unit24(la + lfo_off));
-                    const float m_gA = cos2pi((unit24(pa) - 0.5f) * 0.5f);
-                    const float m_gB = cos2pi((unit24(pa + 0x80000000u) - 0.5f) * 0.5f);
+                    const uint64_t la = lfo_acc + (ch ? lfo_inc : 0ull), pa = ps_acc + (ch ? ps_inc : 0ull);
+                    const float m_lfo = cos2pi(unit24h(la + lfo_off));
+                    const float m_gA = cos2pi((unit24h(pa) - 0.5f) * 0.5f);
+                    const float m_gB = cos2pi((unit24h(pa + kHalfCycle) - 0.5f) * 0.5f);
                     const float o_lfo = swap_pair(m_lfo), o_gA = swap_pair(m_gA), o_gB = swap_pair(m_gB);
                     pl_lfo[0] = ch ? o_lfo : m_lfo; pl_lfo[1] = ch ? m_lfo : o_lfo;
                     pl_gA[0] = ch ? o_gA : m_gA;    pl_gA[1] = ch ? m_gA : o_gA;
@@ -431,8 +438,8 @@ struct ChStageL {
                 if (k >= C) { psv[k] = 0.f; continue; }
                 const float lfo = pl_lfo[k & 1];
                 const float dch = lfo * D + D;
-                const float p0 = unit24(ps_acc);
-                const float p1 = unit24(ps_acc + 0x80000000u);
+                const float p0 = unit24h(ps_acc);
+                const float p1 = unit24h(ps_acc + kHalfCycle);
                 const float gA = pl_gA[k & 1];
                 const float gB = pl_gB[k & 1];
                 lfo_acc += lfo_inc;
@@ -482,7 +489,7 @@ struct ChStageL {
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) {
                     if ((k & 1) == 0) {
-                        const float m_lfo = cos2pi(unit24(lfo_acc + ch * lfo_inc + lfo_off));
+                        const float m_lfo = cos2pi(unit24h(lfo_acc + (ch ? lfo_inc : 0ull) + lfo_off));
                         l0 = pair_even(m_lfo); l1 = pair_odd(m_lfo);
                     }
                     const float dch = ((k & 1) ? l1 : l0) * D + D;
@@ -497,7 +504,7 @@ struct ChStageL {
                     sink(k, x[k] * dry + lp * mix);
                 }
             } else {
-                lfo_acc += (uint32_t)kChunk * lfo_inc;
+                lfo_acc += (uint64_t)kChunk * lfo_inc;
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) sink(k, psv[k]);
             }
@@ -512,8 +519,10 @@ struct ChStageL {
     __device__ __forceinline__ void finish(const ChorusArgs &a) const {
         if (!valid) return;
         if (ch == 0) {
-            a.state[CHS_LFO_ACC * n + i] = lfo_acc;
-            a.state[CHS_PS_ACC * n + i] = ps_acc;
+            a.state[CHS_LFO_ACC * n + i] = (uint32_t)(lfo_acc >> 32);
+            a.state[CHS_LFO_LO * n + i] = (uint32_t)lfo_acc;
+            a.state[CHS_PS_ACC * n + i] = (uint32_t)(ps_acc >> 32);
+            a.state[CHS_PS_LO * n + i] = (uint32_t)ps_acc;
         }
         a.state[(ch ? CHS_Z1R : CHS_Z1L) * n + i] = __float_as_uint(z1);
         a.state[(ch ? CHS_Z2R : CHS_Z2L) * n + i] = __float_as_uint(z2);

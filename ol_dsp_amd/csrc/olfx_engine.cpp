@@ -56,10 +56,11 @@ uint32_t pow2_at_least(uint32_t x) {
 
 float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
-uint32_t phase_inc_u32(double hz, double sr) {
-    double v = std::floor(hz / sr * 4294967296.0 + 0.5);
-    if (v < 0) v = 0;
-    return (uint32_t)(uint64_t)v;
+// a fraction of a cycle in [0, 1] as 64-bit fixed point (2^64 = one cycle); 1.0 wraps to 0
+uint64_t fix64(double cycles) {
+    constexpr double kTwo64 = 18446744073709551616.0;
+    const double v = std::floor(cycles * kTwo64 + 0.5);
+    return v <= 0 ? 0u : (v >= kTwo64 ? (uint64_t)(v - kTwo64) : (uint64_t)v);
 }
 
 uint32_t as_u32(float f) {
@@ -205,9 +206,14 @@ void derive_chorus(const float *p, double sr, uint32_t *c) {
     const double rate_hz = 0.01 + rate * (0.5 - 0.01);           // scale 0 1 0.01 0.5 (:3935)
     const double depth_ms = 1.0 + depth * (12.0 - 1.0);          // scale 0 1 1 12 1   (:3436)
     const double fc = 300.0 + cutoff * (15000.0 - 300.0);         // scale 0 1 300 15000 1 (:2242)
-    c[CHC_LFO_INC] = phase_inc_u32(rate_hz, sr);
-    c[CHC_LFO_OFF] = (uint32_t)(uint64_t)std::floor(phase * 4294967296.0 + 0.5);  // 1.0 wraps to 0
-    c[CHC_PS_INC] = phase_inc_u32(pitch, sr);
+    // 64-bit phasors: the increment rounding drifts a phase by < 2^-64 cycle per sample
+    const uint64_t lfo_inc = fix64(rate_hz / sr), lfo_off = fix64(phase), ps_inc = fix64(pitch / sr);
+    c[CHC_LFO_INC] = (uint32_t)(lfo_inc >> 32);
+    c[CHC_LFO_INC_LO] = (uint32_t)lfo_inc;
+    c[CHC_LFO_OFF] = (uint32_t)(lfo_off >> 32);                   // phase 1.0 wraps to 0
+    c[CHC_LFO_OFF_LO] = (uint32_t)lfo_off;
+    c[CHC_PS_INC] = (uint32_t)(ps_inc >> 32);
+    c[CHC_PS_INC_LO] = (uint32_t)ps_inc;
     c[CHC_DEPTH] = as_u32((float)(depth_ms * sr / 1000.0));       // mstosamps (:3897)
     c[CHC_WINDOW] = as_u32((float)(window * sr / 1000.0));        // mstosamps(window)
     // lores~ -> RBJ biquad low-pass, Q = 1/sqrt(2) + 20 q^3 (declared)

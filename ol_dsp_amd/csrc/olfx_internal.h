@@ -109,19 +109,22 @@ OLFX_HD float cos2pi(float x) {
 // modulated per instance: each lane streams through its own ring.
 // ----------------------------------------------------------------------------------------------
 enum {
-    CHC_LFO_INC = 0,    // u32 phase increment of cycle~ (2^32 = one cycle)
-    CHC_LFO_OFF,        // u32 phase offset of cycle~
-    CHC_PS_INC,         // u32 phase increment of the pitch-shifter phasor
+    // phasors are 64-bit fixed point (2^64 = one cycle), stored as a high and a low word
+    CHC_LFO_INC = 0,    // high word of cycle~'s phase increment
+    CHC_LFO_OFF,        // high word of cycle~'s phase offset
+    CHC_PS_INC,         // high word of the pitch-shifter phasor's increment
     CHC_DEPTH,          // D = mstosamps(1 + 11 depth)       (float)
     CHC_WINDOW,         // W = mstosamps(window)             (float)
     CHC_B0, CHC_B1, CHC_B2, CHC_A1, CHC_A2,   // lores~ (RBJ biquad LP, normalised by a0)
     CHC_MIX, CHC_DRY,   // mix, 1 - mix
+    CHC_LFO_INC_LO, CHC_LFO_OFF_LO, CHC_PS_INC_LO,   // low words of the three above
     CHC_N
 };
 enum {
-    CHS_LFO_ACC = 0,    // u32
-    CHS_PS_ACC,         // u32
+    CHS_LFO_ACC = 0,    // high word of cycle~'s 64-bit phase
+    CHS_PS_ACC,         // high word of the pitch-shifter's 64-bit phase
     CHS_Z1L, CHS_Z2L, CHS_Z1R, CHS_Z2R,   // biquad TDF-II state per channel
+    CHS_LFO_LO, CHS_PS_LO,                // low words of the two phases
     CHS_N
 };
 

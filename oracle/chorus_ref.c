@@ -10,7 +10,8 @@
  * covers them.  This file restates the patch dataflow exactly as written (per-object citations
  * below) with the build's declared spec choices:
  *   - fp32 arithmetic (gen~/RNBO compute in double);
- *   - phasors as 32-bit fixed-point accumulators, 24-bit fraction -> float;
+ *   - phasors as 64-bit fixed-point accumulators (2^64 = one cycle; the increment rounding drifts a
+ *     phase by < 2^-64 cycle per sample), their top 24 bits -> the float phase (exact);
  *   - cos(2 pi x) by a fixed polynomial (cos2pi below), standing in for cycle~'s wavetable and
  *     gen~'s cos;
  *   - gen Delay.read: linear interpolation, delay clamped to [1, size-2] (read before write);
@@ -38,13 +39,17 @@ static float clampf_(float x, float lo, float hi) { return x < lo ? lo : (x > hi
 
 static uint32_t pow2ge(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; return p; }
 
-static uint32_t fix_inc(double hz, double sr)
+#define TWO64 18446744073709551616.0
+
+/* a fraction of a cycle [0, 1] as 64-bit fixed point; 1.0 (and anything rounding to it) wraps to 0 */
+static uint64_t fix64(double cycles)
 {
-    double v = floor(hz / sr * 4294967296.0 + 0.5);
-    return v < 0 ? 0u : (uint32_t)(uint64_t)v;
+    const double v = floor(cycles * TWO64 + 0.5);
+    return v <= 0 ? 0u : (v >= TWO64 ? (uint64_t)(v - TWO64) : (uint64_t)v);
 }
 
-static float unit24(uint32_t acc) { return (float)(acc >> 8) * 5.9604644775390625e-8f; }
+/* the float phase of a 64-bit accumulator: its top 24 bits, exact in fp32 */
+static float unit24(uint64_t acc) { return (float)((uint32_t)(acc >> 32) >> 8) * 5.9604644775390625e-8f; }
 
 /* cos(2 pi x): reduce to b in [0, 1/4] (exact), one Taylor polynomial of cos to theta^14 on
    [0, pi/2]; same operations in the same order as the GPU (spec choice) */
@@ -64,12 +69,12 @@ float oracle_cos2pi(float x)
 }
 
 typedef struct {
-    uint32_t lfo_inc, lfo_off, ps_inc;
+    uint64_t lfo_inc, lfo_off, ps_inc;
     float D, W, b0, b1, b2, a1, a2, mix, dry;
 } chcoef_t;
 
 typedef struct {
-    uint32_t lfo_acc, ps_acc;
+    uint64_t lfo_acc, ps_acc;
     float z1[2], z2[2];
     float *pring[2], *cring[2];
 } chstate_t;
@@ -98,9 +103,9 @@ static void derive(const float *p, double sr, chcoef_t *c)
     const double rate_hz = 0.01 + rate * (0.5 - 0.01);
     const double depth_ms = 1.0 + depth * (12.0 - 1.0);
     const double fc = 300.0 + cutoff * (15000.0 - 300.0);
-    c->lfo_inc = fix_inc(rate_hz, sr);
-    c->lfo_off = (uint32_t)(uint64_t)floor(phase * 4294967296.0 + 0.5);
-    c->ps_inc = fix_inc(pitch, sr);
+    c->lfo_inc = fix64(rate_hz / sr);
+    c->lfo_off = fix64(phase);                 /* phase 1.0 wraps to 0: L and R share the LFO */
+    c->ps_inc = fix64(pitch / sr);
     c->D = (float)(depth_ms * sr / 1000.0);
     c->W = (float)(window * sr / 1000.0);
     const double Q = 0.70710678118654752 + 20.0 * q * q * q;
@@ -186,7 +191,7 @@ static void chorus_frame(const oracle_chorus *o, const chcoef_t *k, chstate_t *s
     s->lfo_acc += k->lfo_inc;
     const float dch = lfo * k->D + k->D;
     const float p0 = unit24(s->ps_acc);
-    const float p1 = unit24(s->ps_acc + 0x80000000u);
+    const float p1 = unit24(s->ps_acc + 0x8000000000000000ull);
     s->ps_acc += k->ps_inc;
     const float g0 = oracle_cos2pi((p0 - 0.5f) * 0.5f);
     const float g1 = oracle_cos2pi((p1 - 0.5f) * 0.5f);

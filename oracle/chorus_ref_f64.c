@@ -41,9 +41,9 @@ struct oracle_chorus64 {
     double *params;            /* [n][OCH_NPARAMS] */
 };
 
-/* quantize = 1: phasor increments rounded to the fp32 spec's 32-bit fixed point (chorus_ref.c
-   fix_inc), so the remaining deviation is the fp32 arithmetic alone */
-static double q32(double inc) { return floor(inc * 4294967296.0 + 0.5) / 4294967296.0; }
+/* quantize = 1: phasor increments rounded to the fp32 spec's 64-bit fixed point (chorus_ref.c
+   fix64), so the remaining deviation is the fp32 arithmetic alone */
+static double q64(double inc) { return floor(inc * 18446744073709551616.0 + 0.5) / 18446744073709551616.0; }
 
 static void derive64(const double *p, double sr, int quantize, ch64_t *c)
 {
@@ -57,7 +57,7 @@ static void derive64(const double *p, double sr, int quantize, ch64_t *c)
     c->lfo_off = clampd(p[OCH_PHASE], 0.0, 1.0);
     c->lfo_inc = (0.01 + rate * (0.5 - 0.01)) / sr;          /* scale 0 1 0.01 0.5, :3935 */
     c->ps_inc = pitch / sr;
-    if (quantize) { c->lfo_inc = q32(c->lfo_inc); c->ps_inc = q32(c->ps_inc); }
+    if (quantize) { c->lfo_inc = q64(c->lfo_inc); c->ps_inc = q64(c->ps_inc); }
     c->D = (1.0 + depth * (12.0 - 1.0)) * sr / 1000.0;       /* mstosamps(scale 0 1 1 12), :3436 */
     c->W = window * sr / 1000.0;
     const double fc = 300.0 + cutoff * (15000.0 - 300.0);    /* :2242 */

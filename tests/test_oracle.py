@@ -145,13 +145,14 @@ def test_chorus_frozen_golden(golden, key, mode):
 
 @pytest.mark.parametrize("key,mode", [("chorus", 0), ("pitchshift", 1)])
 def test_chorus_fp32_deviation_from_double(golden, key, mode):
-    """The spec's declared deviation (fp32 arithmetic, 32-bit fixed-point phasors) MEASURED against
+    """The spec's declared deviation (fp32 arithmetic, 64-bit fixed-point phasors) MEASURED against
     the same graph in double precision with double phasors (gen~ / RNBO arithmetic,
     oracle/chorus_ref_f64.c) on the golden inputs (6 instances x 6,000 frames of white noise).
-    Measured: chorus max |d| / max(|ref|, rms) 1.51e-3 (SNR 77.5 dB), pitch-shift 4.2e-4 (82.3 dB);
-    with the double restatement's increments rounded to the spec's fixed point, 1.8e-4 / 1.4e-4
-    (93.7 / 93.4 dB): the increment rounding (LFO phase drift over time) dominates.  Parity stays
-    unpinned (RNBO / genlib absent); this bounds only the arithmetic."""
+    Measured (round 3, 64-bit phasors): chorus max |d| / max(|ref|, rms) 1.58e-4 (SNR 93.5 dB),
+    pitch-shift 1.29e-4 (93.3 dB) -- the fp32 arithmetic alone: rounding the double restatement's
+    increments to the spec's fixed point changes nothing measurable.  (Round 2's 32-bit phasor
+    increments drifted the LFO phase: 1.51e-3 / 4.2e-4.)  Parity stays unpinned (RNBO / genlib
+    absent); this bounds only the arithmetic."""
     g = golden[key]
     p = np.asarray(g["params"], np.float32)
     x = noise_block(g["n"], g["frames"], g["input_base"])
@@ -169,9 +170,9 @@ def test_chorus_fp32_deviation_from_double(golden, key, mode):
         snr = float(10 * np.log10(np.sum(yb ** 2) / np.sum(d ** 2)))
         out[q] = (rel, snr)
         print(f"{key} {'fixed-point increments' if q else 'double increments'}: rel {rel:.3g}, SNR {snr:.1f} dB")
-    assert out[0][0] <= 2e-3 and out[0][1] >= 75.0
-    assert out[2][0] <= 2.5e-4 and out[2][1] >= 90.0
-    assert out[2][0] < out[0][0]
+    for q in (0, 2):
+        assert out[q][0] <= 2e-4 and out[q][1] >= 90.0
+    assert abs(out[0][0] - out[2][0]) <= 0.1 * out[2][0]
 
 
 def test_cos2pi_accuracy():
