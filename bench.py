@@ -471,8 +471,9 @@ def main():
                                                 "cpu_baseline", "output_checksum", "output_nonfinite_rank0") if k in r}
             base = EVENT_FREE.get(name)
             bkey = base if base != "chain" else "chain_16384"
-            if base and bkey in also_res:   # the control leg's cost against its event-free twin
-                b = also_res[bkey]
+            # the control leg's cost against its event-free twin (an `also` leg or the main workload)
+            b = also_res.get(bkey) or (main_res if base == args.workload else None)
+            if base and b is not None:
                 also_res[key]["control"].update({
                     "event_free_kernel_ms": b["roofline"]["kernel_ms"], "event_free_ms_per_step": b["ms_per_step"],
                     "kernel_ms_ratio": r["roofline"]["kernel_ms"] / b["roofline"]["kernel_ms"],

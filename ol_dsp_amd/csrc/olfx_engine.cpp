@@ -401,8 +401,10 @@ struct olfx_engine {
     hipStream_t pending_stream = nullptr;
     std::vector<int32_t> ev_slot;         // voice -> its record in `folded` during fold_events, else -1
     struct Folded { uint32_t inst, op, freq, pad; };
-    std::vector<Folded> folded, ev_sorted;
-    std::vector<uint32_t> ev_off, ev_fill;   // per-workgroup offsets of ev_sorted
+    std::vector<Folded> folded;
+    // per workgroup: records, first overflow record (crowded groups), records written so far
+    std::vector<uint32_t> ev_count, ev_more, ev_fill;
+    uint32_t n_more = 0;                  // overflow records
     std::vector<uint32_t> h_words;        // scratch for a record
     // OLFX_TRACE_CONTROL=1 (read at create): host time of each control-path step, summed and
     // printed to stderr at destroy (tracing)
@@ -607,18 +609,42 @@ void fold_events(olfx_engine *e) {
         }
     }
     e->events.clear();
-    // bucket the records by workgroup (64 voices), a counting sort: ev_off[g] .. ev_off[g+1] are
-    // group g's records (any order inside a group: a lane finds its voice's record by slot)
+    // records per workgroup (64 voices); crowded workgroups (more than kVevCap records) get a run
+    // of the overflow list each, in group order
     const uint32_t groups = (e->n + 63u) / 64u;
-    e->ev_off.assign(groups + 1, 0u);
+    e->ev_count.assign(groups, 0u);
     for (const olfx_engine::Folded &r : e->folded) {
-        e->ev_off[(r.inst >> 6) + 1]++;
+        e->ev_count[r.inst >> 6]++;
         e->ev_slot[r.inst] = -1;
     }
-    for (uint32_t g = 0; g < groups; ++g) e->ev_off[g + 1] += e->ev_off[g];
-    e->ev_sorted.resize(e->folded.size());
-    e->ev_fill.assign(e->ev_off.begin(), e->ev_off.end() - 1);
-    for (const olfx_engine::Folded &r : e->folded) e->ev_sorted[e->ev_fill[r.inst >> 6]++] = r;
+    e->ev_more.assign(groups, 0u);
+    e->n_more = 0;
+    for (uint32_t g = 0; g < groups; ++g)
+        if (e->ev_count[g] > kVevCap) {
+            e->ev_more[g] = e->n_more;
+            e->n_more += e->ev_count[g];
+        }
+}
+
+// The folded records into a packet's event section (VoiceArgs::ev layout, olfx_internal.h):
+// `fix` = [groups][kVevCap] 8-B slots, then the overflow list.
+void write_events(olfx_engine *e, uint32_t *fix) {
+    const uint32_t groups = (e->n + 63u) / 64u;
+    std::memset(fix, 0, (size_t)groups * kVevCap * 8);
+    uint32_t *more = fix + (size_t)groups * kVevCap * 2;
+    e->ev_fill.assign(groups, 0u);
+    for (const olfx_engine::Folded &r : e->folded) {
+        const uint32_t g = r.inst >> 6;
+        const uint32_t k = e->ev_fill[g]++;
+        uint32_t *rec = e->ev_count[g] <= kVevCap ? fix + 2 * ((size_t)g * kVevCap + k) : more + 2 * ((size_t)e->ev_more[g] + k);
+        rec[0] = (r.inst & 63u) | r.op << 8;
+        rec[1] = r.freq;
+    }
+    for (uint32_t g = 0; g < groups; ++g)
+        if (e->ev_count[g] > kVevCap) {
+            fix[2 * (size_t)g * kVevCap] = VEV_MORE << 8 | e->ev_count[g] << 16;
+            fix[2 * (size_t)g * kVevCap + 1] = e->ev_more[g];
+        }
 }
 
 // Record one marker after the pending slots' kernels (on their stream) and make it their guard.
@@ -676,7 +702,7 @@ int grow_slot(olfx_engine *e, olfx_engine::Slot &sl, size_t words, bool device_h
 size_t max_packet_words(const olfx_engine *e) {
     CoefScatterArgs ca{};
     const size_t n = e->n, W = coef_segments(e, &ca);
-    const size_t ev = is_voice_kind(e->kind) ? (n + 63) / 64 + 1 + 4 * n : 0;
+    const size_t ev = is_voice_kind(e->kind) ? 2 * ((n + 63) / 64 * kVevCap + n) : 0;
     return n + W * n + ev + 16;
 }
 
@@ -686,8 +712,8 @@ size_t max_packet_words(const olfx_engine *e) {
 // scattered on `s` ahead of the block's kernel; the voice kernel reads its events itself.  A slot is
 // rewritten only after the kernels that read it are done (its `consumed` event, recorded by the
 // caller after them: *used_slot).  Packet layout (u32 words, 16-B aligned sections): instance list
-// (absent when every instance changed) | coefficient records [W][m] | event offsets [groups + 1] |
-// event records [mev][4].
+// (absent when every instance changed) | coefficient records [W][m] | event slots [groups][kVevCap]
+// and the overflow list, 8-B records (write_events).
 int submit_control(olfx_engine *e, hipStream_t s, VoiceArgs *va, olfx_engine::Slot **used_slot) {
     *used_slot = nullptr;
     const bool voice = is_voice_kind(e->kind);
@@ -704,7 +730,6 @@ int submit_control(olfx_engine *e, hipStream_t s, VoiceArgs *va, olfx_engine::Sl
     e->tr_calls++;
     const bool evs = voice && !e->events.empty();
     if (evs) fold_events(e);
-    const size_t mev = evs ? e->ev_sorted.size() : 0;
     lap(0);
     CoefScatterArgs ca{};
     const uint32_t W = coef_segments(e, &ca);
@@ -713,9 +738,8 @@ int submit_control(olfx_engine *e, hipStream_t s, VoiceArgs *va, olfx_engine::Sl
     auto up4 = [](size_t x) { return (x + 3) & ~(size_t)3; };
     const size_t o_inst = 0;
     const size_t o_val = o_inst + (dense ? 0 : up4(m));
-    const size_t o_off = up4(o_val + (size_t)W * m);
-    const size_t o_ev = up4(o_off + (mev ? groups + 1 : 0));
-    const size_t words = o_ev + 4 * mev;
+    const size_t o_ev = up4(o_val + (size_t)W * m);
+    const size_t words = o_ev + (evs ? 2 * ((size_t)groups * kVevCap + e->n_more) : 0);
 
     // Delivery: a small packet (a block's CCs / notes) is read by the kernels straight from a pinned
     // slot -- no copy command: ~2 us of host time, a host-link round trip or two inside the kernel.
@@ -749,10 +773,7 @@ int submit_control(olfx_engine *e, hipStream_t s, VoiceArgs *va, olfx_engine::Sl
     for (const uint32_t i : e->dirty_list) e->dirty_mark[i] = 0;
     e->dirty_list.clear();
     lap(3);
-    if (mev) {
-        std::memcpy(sl.h + o_off, e->ev_off.data(), (groups + 1) * 4);
-        std::memcpy(sl.h + o_ev, e->ev_sorted.data(), mev * 16);
-    }
+    if (evs) write_events(e, sl.h + o_ev);
     if (copy) {
         // the copy stream waits for nothing on the device: the host made sure above that the slot's
         // previous readers are done (a device-side wait there serialised the copy behind them)
@@ -774,9 +795,9 @@ int submit_control(olfx_engine *e, hipStream_t s, VoiceArgs *va, olfx_engine::Sl
         const hipError_t r = launch_coef_scatter(ca, s);
         if (r != hipSuccess) return e->hip_fail(r, "coefficient scatter launch");
     }
-    if (mev) {
-        va->ev_off = dev + o_off;
-        va->ev = reinterpret_cast<const uint4 *>(dev + o_ev);
+    if (evs) {
+        va->ev = reinterpret_cast<const uint2 *>(dev + o_ev);
+        va->ev_more = va->ev + (size_t)groups * kVevCap;
     }
     lap(5);
     return OLFX_OK;
@@ -887,7 +908,7 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, uin
         a.n = e->n;
         a.n_frames = n_frames;
         a.moog = e->kind == OLFX_KIND_VOICE_MOOG;
-        a.ev_off = ev.ev_off;
+        a.ev_more = ev.ev_more;
         a.ev = ev.ev;
         r = launch_voice(a, s);
         break;

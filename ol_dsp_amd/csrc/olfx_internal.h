@@ -180,8 +180,15 @@ enum : uint32_t {
     VEV_GATE_SET = 1u,          // gate := VEV_GATE_ON bit (NoteOn / GateOn / NoteOff / GateOff)
     VEV_GATE_ON = 2u,
     VEV_RETRIGGER = 4u,         // Adsr::Retrigger(true) on both envelopes: mode ATTACK, x = 0
-    VEV_FREQ = 8u,              // freq_ := rec.z (mtof(note) for NoteOn, SetFrequency's Hz)
+    VEV_FREQ = 8u,              // freq_ := the record's frequency (mtof(note) for NoteOn, SetFrequency's Hz)
+    VEV_MORE = 0x80u,           // (slot 0 of a crowded workgroup) its records are in the overflow list
 };
+// Event records, 8 B: x = (voice & 63) | VEV_* ops << 8, y = frequency bits; x = 0 is an empty slot.
+// Workgroup g (64 voices) owns the kVevCap fixed slots ev[g kVevCap ..]: the kernel reads them in
+// one host-link round trip without first reading where they are.  A workgroup with more than
+// kVevCap records puts them all in the overflow list and marks slot 0:
+// x = VEV_MORE << 8 | count << 16, y = first record in ev_more (a second round trip, for it only).
+constexpr uint32_t kVevCap = 4;
 
 struct VoiceArgs {
     float *state;               // [VCS_N][n], MoogFilter voices [VCS_N_MOOG][n]
@@ -189,10 +196,9 @@ struct VoiceArgs {
     float *out;                 // [1][n_frames][n]
     uint32_t n, n_frames;
     uint32_t moog;              // 1: daisysp::LadderFilter (MoogFilter) in place of the Svf
-    // this block's events (nullptr: none): workgroup g's records are ev[ev_off[g] .. ev_off[g+1]),
-    // sorted by voice, at most one per voice: (voice, VEV_* ops, frequency bits, 0)
-    const uint32_t *ev_off;     // [n_groups + 1], n_groups = ceil(n / 64)
-    const uint4 *ev;
+    // this block's events (nullptr: none), at most one record per voice (kVevCap above)
+    const uint2 *ev;            // [n_groups][kVevCap] fixed slots, n_groups = ceil(n / 64)
+    const uint2 *ev_more;       // overflow list
 };
 
 // Coefficient records of the instances whose parameters changed (olfx_engine.cpp upload_params):

@@ -69,29 +69,43 @@ struct Ladder {
     float z0[4], z1[4], old;
 };
 
-// The block's folded note events (VoiceArgs::ev, VEV_*) of this lane's voice: the wave stages its
-// workgroup's records (at most 64, one per voice) into its own 64 LDS slots, slot = voice within the
-// group, and each lane reads its own.  `me` is the lane's voice within the group (dead lanes of the
-// last group mirror voice n-1, so they read its slot too).  No events: one uniform test.
+// The block's folded note events (VoiceArgs::ev, VEV_*) of this lane's voice: the wave reads its
+// workgroup's fixed slots (lanes 0 .. kVevCap-1, one host-link round trip; a crowded workgroup's
+// overflow list is a second one), stages the records into its own 64 LDS slots, slot = voice within
+// the group, and each lane reads its own.  `me` is the lane's voice within the group (dead lanes of
+// the last group mirror voice n-1, so they read its slot too).  No events: one uniform test.
 struct VoiceEv {
     uint32_t op;
     float freq;
 };
 __device__ __forceinline__ VoiceEv voice_event(const VoiceArgs &a, uint2 *slot, uint32_t lane, uint32_t me) {
     VoiceEv r{0u, 0.0f};
-    if (!a.ev_off) return r;
-    const uint32_t lo = a.ev_off[blockIdx.x], hi = a.ev_off[blockIdx.x + 1];
-    if (lo == hi) return r;
+    if (!a.ev) return r;
+    uint2 e = make_uint2(0u, 0u);
+    if (lane < kVevCap) e = a.ev[blockIdx.x * kVevCap + lane];
     slot[lane] = make_uint2(0u, 0u);
-    if (lo + lane < hi) {
-        const uint4 e = a.ev[lo + lane];
-        slot[e.x & 63u] = make_uint2(e.y, e.z);
+    const uint32_t head = __builtin_amdgcn_readfirstlane(e.x);
+    if ((head >> 8) & VEV_MORE) {
+        const uint32_t cnt = head >> 16, first = __builtin_amdgcn_readfirstlane(e.y);
+        e = make_uint2(0u, 0u);
+        if (lane < cnt) e = a.ev_more[first + lane];
     }
+    if (e.x >> 8) slot[e.x & 63u] = make_uint2(e.x >> 8, e.y);
     // one wave writes and reads its slots: LDS operations of a wave complete in order; the fences
     // keep the compiler from moving the read above the other lanes' writes
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint2 v = slot[me];
+    r.op = v.x;
+    r.freq = __uint_as_float(v.y);
+    return r;
+}
+
+// Another wave's view of slots voice_event staged, after a workgroup barrier.
+__device__ __forceinline__ VoiceEv staged_event(const VoiceArgs &a, const uint2 *slot, uint32_t me) {
+    VoiceEv r{0u, 0.0f};
+    if (!a.ev) return r;
     const uint2 v = slot[me];
     r.op = v.x;
     r.freq = __uint_as_float(v.y);
@@ -217,15 +231,17 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
     // ---------------- amp and/or cutoff roles (compile-time role flags: straight-line chunks) ----------------
     auto feed = [&](auto amp_c, auto cut_c) {
         constexpr bool AMP = decltype(amp_c)::value, CUT = decltype(cut_c)::value;
-        // the block's note events first (one feed wave per workgroup applies them)
-        const VoiceEv ev = voice_event(a, evslot, lane, me);
+        // the block's note events first (one feed wave per workgroup applies them); the state loads
+        // are issued before the event read, so their latency hides under its host-link round trip
         uint32_t flags0 = __float_as_uint(s[VCS_FLAGS * n + i]);
         float xa0 = s[VCS_ENVA_X * n + i], xf0 = s[VCS_ENVF_X * n + i];
+        const float freq_s = s[VCS_FREQ * n + i];
+        const VoiceEv ev = voice_event(a, evslot, lane, me);
         apply_gate_events(ev, flags0, xa0, xf0);
         const bool gate = (flags0 >> 8) & 1u;
         const float amp_amt = c[VCC_AMP_AMT * n + i], port_c = c[VCC_PORT_COEF * n + i];
         const float inv_sr = c[VCC_INV_SR * n + i];
-        const float freq = (ev.op & VEV_FREQ) ? ev.freq : s[VCS_FREQ * n + i];
+        const float freq = (ev.op & VEV_FREQ) ? ev.freq : freq_s;
         const float cutoff = c[VCC_CUTOFF * n + i], fenv_amt = c[VCC_FENV_AMT * n + i];
         // ladder: drive_scaled (VCC_DRIVE), 1/(4 sr) (VCC_FC_MAX)
         const float drive = c[VCC_DRIVE * n + i];
@@ -369,7 +385,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     __shared__ float2 eq[2][kVcChunk][64];      // ENV -> OSC, FREQ: (amp, fc_in)
     __shared__ float2 sq[2][kVcChunk][64];      // OSC -> FILT: (src, amp)
     __shared__ float2 fdq[2][kVcChunk][64];     // FREQ -> FILT: (fq, damp)
-    __shared__ uint2 evslot[2][64];             // ENV's and OSC's staging of the block's events
+    __shared__ uint2 evslot[64];                // ENV's staging of the block's events (OSC reads it)
     const uint32_t n = a.n;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -388,10 +404,11 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
 
     if (role == 0) {
         // ---- ENV (SynthVoice.h:42,46-47): the amp and filter Adsr, the cutoff sum ----
-        // the block's gate events first (NoteOn / GateOn / NoteOff / GateOff)
-        const VoiceEv ev = voice_event(a, evslot[0], lane, me);
+        // the block's gate events first (NoteOn / GateOn / NoteOff / GateOff); the state loads are
+        // issued before the event read, so their latency hides under its host-link round trip
         uint32_t flags0 = __float_as_uint(s[VCS_FLAGS * n + i]);
         float xa0 = s[VCS_ENVA_X * n + i], xf0 = s[VCS_ENVF_X * n + i];
+        const VoiceEv ev = voice_event(a, evslot, lane, me);
         apply_gate_events(ev, flags0, xa0, xf0);
         const bool gate = (flags0 >> 8) & 1u;
         bool gprev_a = (flags0 >> 6) & 1u, gprev_f = (flags0 >> 7) & 1u;
@@ -444,14 +461,20 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     } else if (role == 1) {
         // ---- OSC (SynthVoice.h:44-45): Port::Process, Oscillator::SetFreq / Process, WAVE_POLYBLEP_SAW,
         //      amp 0.5 ----
-        // the block's pitch events (NoteOn: mtof(note), SetFrequency: Hz) first
-        const VoiceEv ev = voice_event(a, evslot[1], lane, me);
         const float port_c = c[VCC_PORT_COEF * n + i];
         const float inv_sr = c[VCC_INV_SR * n + i];
-        const float freq = (ev.op & VEV_FREQ) ? ev.freq : s[VCS_FREQ * n + i];
-        if (ev.op & VEV_FREQ) s[VCS_FREQ * n + i] = freq;
+        float freq = s[VCS_FREQ * n + i];
         float phase = s[VCS_PHASE * n + i], port_z = s[VCS_PORT_Z * n + i];
         for (uint32_t k = 0; k < nsteps; ++k) {
+            if (k == 1) {
+                // the block's pitch events (NoteOn: mtof(note), SetFrequency: Hz), staged by ENV
+                // before the first barrier; OSC's first chunk is step 1
+                const VoiceEv ev = staged_event(a, evslot, me);
+                if (ev.op & VEV_FREQ) {
+                    freq = ev.freq;
+                    s[VCS_FREQ * n + i] = freq;
+                }
+            }
             if (k >= 1 && k + 1 < nsteps) {
                 const float2 *qi = &eq[(k - 1) & 1][0][lane];
                 float2 *qo = &sq[(k - 1) & 1][0][lane];
