@@ -17,14 +17,19 @@
 // interleaved [n][48000][2]: both channels share the delay, so one window load serves both.
 //
 // Mapping (as chorus_stage.h): lane = (instance j of the wave, channel), a wave = 32 instances x
-// 2 channels.  The block runs in 16-frame chunks.  A chunk's reads fall in a window of 20
-// positions starting at (t0 - D - 1) rounded down to even: 10 x 16-B stereo pieces per
-// instance, loaded cooperatively one chunk ahead and de-interleaved into LDS as [slot][lane]
-// (conflict-free per-frame reads).  The chunk's writes leave as one 128-B stereo run per
-// instance (8 lanes x 16 B) from LDS staging.  Delays shorter than a chunk read positions the
-// chunk itself writes: every written sample also goes into the window (a junk slot when it falls
-// outside), and positions the next window needs before they reach the ring are patched in from
-// registers -- so every delay 0..47999 takes the same branch-free path.
+// 2 channels.  The block runs in 16-frame chunks.  A chunk's reads (frame k at t + k - D and one
+// below) fall in a window of 18 positions from s = (t - D - 1) rounded down to even, de-interleaved
+// into LDS as [slot][lane] (conflict-free per-frame reads).  LINE CARRY (v3): s is even, so the
+// window lies in the two 128-B stereo lines L = s / 16 and L + 1 (s mod 16 <= 14); D is fixed
+// within a block, so the next chunk's window is lines L + 1 and L + 2.  Each chunk loads only its
+// successor's new line (cooperatively, one chunk ahead) and carries the other in registers:
+// 8 B read per stereo frame, the algorithmic figure (v2 loaded 10 overlapping 16-B pieces per
+// chunk: 23.8 B/frame measured).  The chunk's writes leave as one 128-B stereo run per instance
+// (8 lanes x 16 B) from LDS staging.  Delays shorter than a chunk read positions the chunk itself
+// writes: every written sample also goes into the window (a junk slot when it falls outside).  A
+// carried line was loaded two chunks back, a new one a chunk back, each after the stores of the
+// chunks before it: the last two chunks' writes are patched in from registers -- so every delay
+// 0..47999 takes the same branch-free path.
 // Bound: HBM (32 B per stereo frame: ring write 8 + ring read 8 + I/O 16).
 #include <type_traits>
 #include <utility>
@@ -37,7 +42,7 @@ namespace {
 
 constexpr int kFrThreads = 256;
 constexpr int kFrChunk = 16;
-constexpr int kFrWin = 20;                          // positions per window (10 stereo pieces)
+constexpr int kFrWin = 20;                          // window slots (18 read) staged from two lines
 constexpr int kFrSlots = kFrWin + 1;                // + junk slot
 constexpr int kFrStride = 36;                       // staging floats per instance (32 + pad)
 constexpr int kFrRegion = kFrSlots * 64 + 32 * kFrStride;   // floats of LDS per wave
@@ -86,7 +91,7 @@ __device__ __forceinline__ uint32_t wrap48k(int64_t p) {
 // same lanes and ticks, with per-instance selects of what each lane outputs.  Engines of racks only
 // (topologies 0 / 1) run COMP = false, the rack's own instruction stream.
 template <bool COMP>
-__global__ __launch_bounds__(kFrThreads) void fxrack_block_v2(FxRackArgs a) {
+__global__ __launch_bounds__(kFrThreads) void fxrack_block_v3(FxRackArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const uint32_t tid = threadIdx.x;
     const uint32_t wib = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
@@ -145,41 +150,52 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v2(FxRackArgs a) {
     float *stage = win + kFrSlots * 64;                 // [32][kFrStride]
 
     // window of the chunk starting at t: first position (t - D - 1) rounded down to even, as an
-    // offset from t (the ring position of t is (a.t0 + f0) mod 48000)
+    // offset from t -- the same for every chunk (t is even)
     auto rel_of = [&](uint32_t t) { return (int)(((int64_t)t - (int64_t)D - 1) & ~(int64_t)1) - (int)t; };
-    // cooperative window load: piece P = r * 64 + lane of 320 -> piece m = P / 32 of instance
-    // jj = P % 32 (instances innermost).  A ds_write_b64 lane group (16 contiguous lanes) then
-    // stages one piece of 16 instances: 16 distinct bank pairs, conflict-free.  (Pieces innermost,
-    // m = P % 10, put up to ten pieces of one instance -- one bank pair -- in a group.)
-    auto piece_inst = [&](int) { return lane & 31u; };
-    auto piece_idx = [&](int r) { return (uint32_t)r * 2u + (lane >> 5); };
-    float4 v[5];
-    auto load_window = [&](uint32_t t) {
+    // Cooperative line loads: piece P = r * 64 + lane of 256 -> piece m = 2 r + lane / 32 (16 B:
+    // positions 2m, 2m + 1 of the line) of instance jj = lane % 32 (instances innermost: a
+    // ds_write_b64 lane group of 16 contiguous lanes stages one piece of 16 instances, 16 distinct
+    // bank pairs, conflict-free).  Every part of a lane serves the same instance jj, whose window
+    // start (ring position, wrapped) comes from lane 2 jj once per launch.
+    const uint32_t jj = lane & 31u;
+    const uint32_t oj = min(inst0 + jj, n - 1) - inst0;      // ring within the wave's descriptor
+    const uint32_t spos = (uint32_t)__builtin_amdgcn_ds_bpermute(
+        (int)(jj << 3), (int)wrap48k(((int64_t)a.t0 - (int64_t)D - 1) & ~(int64_t)1));
+    const uint32_t so15 = spos & 15u;                   // window start within its line (even)
+    uint32_t lcur = spos >> 4;                          // line L of the current chunk (instance jj)
+    constexpr uint32_t kLines = kFrMaxDelay / 16u;      // 3000 lines per ring: wraps at a line edge
+    float4 lo[4], nx[4];                                // lines L (carried) and L + 1 (loaded a chunk back)
+    auto load_line = [&](float4 (&dst)[4], uint32_t line) {
 #pragma unroll
-        for (int r = 0; r < 5; ++r) {
-            const uint32_t jj = piece_inst(r), m = piece_idx(r);
-            const int rel = __builtin_amdgcn_ds_bpermute((int)(jj << 3), rel_of(t));   // lane 2 jj
-            const uint32_t oj = min(inst0 + jj, n - 1) - inst0;   // ring within the wave's descriptor
-            const uint32_t pos = wrap48k((int64_t)t + rel + 2 * (int)m);
-            v[r] = ch::ld4(rR, oj * kRing + pos * 8u);
-        }
+        for (int r = 0; r < 4; ++r)
+            dst[r] = ch::ld4(rR, oj * kRing + line * 128u + ((uint32_t)r * 2u + (lane >> 5)) * 16u);
     };
-    auto stage_window = [&]() {
+    auto next_line = [&](uint32_t l) { return l + 1u == kLines ? 0u : l + 1u; };
+    auto stage_lines = [&]() {
 #pragma unroll
-        for (int r = 0; r < 5; ++r) {
-            const uint32_t jj = piece_inst(r), m = piece_idx(r);
-            float *p = win + 2u * m * 64u + 2u * jj;
-            *(float2 *)p = make_float2(v[r].x, v[r].y);
-            *(float2 *)(p + 64) = make_float2(v[r].z, v[r].w);
+        for (int r = 0; r < 4; ++r) {
+            const int m = r * 2 + (int)(lane >> 5);
+            const int slo = 2 * m - (int)so15, shi = slo + 16;   // slots of the piece in L, L + 1
+            if (slo >= 0) {
+                float *p = win + (uint32_t)slo * 64u + 2u * jj;
+                *(float2 *)p = make_float2(lo[r].x, lo[r].y);
+                *(float2 *)(p + 64) = make_float2(lo[r].z, lo[r].w);
+            }
+            if (shi < kFrWin) {                         // shi + 1 <= kFrWin: the junk slot at most
+                float *p = win + (uint32_t)shi * 64u + 2u * jj;
+                *(float2 *)p = make_float2(nx[r].x, nx[r].y);
+                *(float2 *)(p + 64) = make_float2(nx[r].z, nx[r].w);
+            }
         }
     };
 
-    float x[kFrChunk], xn[kFrChunk], y[kFrChunk];
+    float x[kFrChunk], xn[kFrChunk], y[kFrChunk], y2[kFrChunk];
     const uint32_t t00 = a.t0;                          // ring position of frame 0
     int C = (int)min((uint32_t)kFrChunk, nf);
 #pragma unroll
     for (int k = 0; k < kFrChunk; ++k) x[k] = k < C ? ch::ld1(rIn, io_v, (uint32_t)k * frame_b) : 0.f;
-    load_window(t00);
+    load_line(lo, lcur);
+    load_line(nx, next_line(lcur));
     // A chunk's stores (ring run and outputs) are issued at the start of the NEXT chunk, ahead of
     // that chunk's loads: the compiler drains vmcnt to 0 at the loop head (the loop carries
     // in-flight loads), so every memory operation should be issued early in the iteration, where
@@ -204,9 +220,16 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v2(FxRackArgs a) {
         const int Cn = f0 + kFrChunk < nf ? (int)min((uint32_t)kFrChunk, nf - f0 - kFrChunk) : 0;
         const uint32_t t = t00 + f0;                    // chunk's first position, unreduced
         const int rel = rel_of(t);
-        // ---- 1. this chunk's window -> LDS (loaded one chunk ahead), patched with the previous
-        //         chunk's writes that had not reached the ring when it was loaded ----
-        stage_window();
+        // ---- 1. this chunk's window -> LDS from its two lines, patched with the last two chunks'
+        //         writes: line L was loaded before chunk c-2's stores, L + 1 before chunk c-1's ----
+        stage_lines();
+        if (f0 >= 2u * kFrChunk) {
+#pragma unroll
+            for (int k = 0; k < kFrChunk; ++k) {
+                const int s = k - 2 * kFrChunk - rel;   // slot of position t - 32 + k
+                if (s >= 0 && s < kFrWin) wcol[s * 64] = y2[k];
+            }
+        }
         if (f0 > 0) {
 #pragma unroll
             for (int k = 0; k < kFrChunk; ++k) {
@@ -215,13 +238,18 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v2(FxRackArgs a) {
             }
         }
         if (f0 > 0) flush(f0 - kFrChunk, kFrChunk);     // the previous chunk was full
-        // ---- 2. the next chunk's inputs and window in flight (unconditional) ----
+        // ---- 2. the next chunk's inputs and new line in flight (unconditional); L + 1 is carried ----
 #pragma unroll
         for (int k = 0; k < kFrChunk; ++k) {
             const float vv = ch::ld1(rIn, io_v, min(f0 + kFrChunk + (uint32_t)k, nf - 1u) * frame_b);
             xn[k] = k < Cn ? vv : 0.f;
         }
-        load_window(t + kFrChunk);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lo[r] = nx[r];
+        lcur = next_line(lcur);
+        load_line(nx, next_line(lcur));
+#pragma unroll
+        for (int k = 0; k < kFrChunk; ++k) y2[k] = y[k];
         // ---- 3. the frames: C + 1 ticks; tick k runs frame k's delay line (both lanes, own
         //         channel) and one filter step per lane: D on frame k, F on frame k - 1 ----
         float b0p = 0.f;                                // F's input: D's b0 of the previous tick
@@ -305,8 +333,8 @@ hipError_t launch_fxrack(const FxRackArgs &a, hipStream_t s) {
     const uint32_t waves = (a.n + 31) / 32;
     const uint32_t blocks = (waves + kFrThreads / 64 - 1) / (kFrThreads / 64);
     const size_t lds = (size_t)(kFrThreads / 64) * kFrRegion * sizeof(float);
-    if (a.components) hipLaunchKernelGGL(fxrack_block_v2<true>, dim3(blocks), dim3(kFrThreads), lds, s, a);
-    else hipLaunchKernelGGL(fxrack_block_v2<false>, dim3(blocks), dim3(kFrThreads), lds, s, a);
+    if (a.components) hipLaunchKernelGGL(fxrack_block_v3<true>, dim3(blocks), dim3(kFrThreads), lds, s, a);
+    else hipLaunchKernelGGL(fxrack_block_v3<false>, dim3(blocks), dim3(kFrThreads), lds, s, a);
     return hipGetLastError();
 }
 

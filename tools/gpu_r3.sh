@@ -8,6 +8,7 @@
 #   bench      the driver's default line (python bench.py)
 #   prof       rocprofv3 kernel stats of the default line
 #   prof_ctl   rocprofv3 kernel stats of the voice / chain legs, one CSV per workload
+#   wl:<name>  one workload's bench line, kernel stats and HBM traffic passes
 set -u
 out=gpurun_out
 mkdir -p "$out"
@@ -68,6 +69,11 @@ for m in "$@"; do
       for w in voice voice_events chain chain_cc chain_65536; do
         prof "$w" 300 --workload "$w" --also "" --steps 20 --warmup 5 --cpu-seconds 0
       done ;;
+    wl:*)      # one workload: bench line, kernel stats, HBM traffic passes (tools/traffic_r2.sh)
+      w=${m#wl:}
+      step "bench_$w" 300 python bench.py --workload "$w" --also "" --steps 20 --warmup 5 --cpu-seconds 0
+      prof "$w" 300 --workload "$w" --also "" --steps 20 --warmup 5 --cpu-seconds 0
+      step "traffic_$w" 600 bash tools/traffic_r2.sh "$w" ;;
     *) echo "unknown mode $m"; exit 2 ;;
   esac
 done
