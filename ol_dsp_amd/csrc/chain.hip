@@ -42,6 +42,7 @@ enum { F_C0 = 0, F_C1, F_PIN, F_POUT, F_DIN };   // chunks published by C0 / C1,
 __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int kChunk = 16;
+    const float4 kNoRows[4] = {};                          // the stages take their input per lane
     const uint32_t tid = threadIdx.x;
     const uint32_t wib = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
     const uint32_t lane = tid & 63u;
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) 
                 float y[kChunk];
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) y[k] = 0.f;
-                s1.template chunk<decltype(par)::value>(x, xn, C, Cn, [&](int k, float v) { y[k] = v; }, prefetch);
+                s1.template chunk<decltype(par)::value>(x, xn, C, Cn, [&](int k, float v) { y[k] = v; }, prefetch, kNoRows);
                 const uint32_t gc = gc0 + c;
                 wait_for([&] { return flag_get(flags + F_PIN) + kDepth > gc; });   // buffer gc % kDepth free
                 float *q = q1 + (gc % kDepth) * kQBuf + qcol;
@@ -128,12 +129,12 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) 
                 float y[kChunk];
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) y[k] = 0.f;
-                sa.template chunk<P>(xa, xa, C, Cn, [&](int k, float v) { y[k] = v; }, []() {});
+                sa.template chunk<P>(xa, xa, C, Cn, [&](int k, float v) { y[k] = v; }, []() {}, kNoRows);
                 wait_for([&] { return flag_get(flags + F_DIN) + kDepth > gc; });
                 float *qo = q2 + (gc % kDepth) * kQBuf;
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) { qo[qa + k * 64] = y[k]; y[k] = 0.f; }
-                sb.template chunk<P>(xb, xb, C, Cn, [&](int k, float v) { y[k] = v; }, []() {});
+                sb.template chunk<P>(xb, xb, C, Cn, [&](int k, float v) { y[k] = v; }, []() {}, kNoRows);
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) qo[qb + k * 64] = y[k];
                 flag_put(flags + F_POUT, gc + 1);

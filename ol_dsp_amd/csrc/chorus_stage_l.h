@@ -45,8 +45,15 @@ struct PlanL {
     bool okA, okB;
 };
 
-// 64-bit phasors (2^64 = one cycle): the float phase is the top 24 bits of the high word, exact
-__device__ __forceinline__ float unit24h(uint64_t acc) { return unit24((uint32_t)(acc >> 32)); }
+// 64-bit phasors (2^64 = one cycle): the float phase is the top 24 bits of the high word, exact.
+// The empty asm hides that the high word came from a 64-bit value: otherwise the compiler folds
+// (float)(hi >> 8) into a 64-bit integer -> float conversion (five extra instructions each).
+__device__ __forceinline__ uint32_t hi32(uint64_t acc) {
+    uint32_t h = (uint32_t)(acc >> 32);
+    asm("" : "+v"(h));
+    return h;
+}
+__device__ __forceinline__ float unit24h(uint64_t acc) { return unit24(hi32(acc)); }
 constexpr uint64_t kHalfCycle = 0x8000000000000000ull;
 
 template <int kWin>
@@ -86,14 +93,27 @@ __device__ __forceinline__ PlanL plan_chunk_l(uint64_t lfo_acc, uint64_t lfo_inc
     return p;
 }
 
-template <bool FULL, bool XPREV = false>
+// COOP (not with XPREV): the driver loads the block's input cooperatively -- per chunk 4 x 16 B per
+// lane, rows (frame, channel) of the wave's 32 instances (coop_row below) -- and the stage
+// transposes them through its LDS staging into the lanes' own frames; outputs go the same way
+// (out_stage / coop_out below).  4 + 4 wide vector-memory instructions per chunk instead of
+// 16 + 16 single-float ones (the per-CU vector-memory pipeline, TA/TD, is the busiest unit).
+template <bool FULL, bool XPREV = false, bool COOP = false>
 struct ChStageL {
+    static_assert(!(COOP && XPREV), "cooperative input is for a stage whose input comes from HBM");
     static constexpr int kChunk = 16, kWin = 24, kSlots = kWin + 1;
     // floats of LDS per wave: one window per tap (chorus 4,800 = 19.2 KB: 2 waves/SIMD; pitch-shift
     // alone 3,200 = 12.8 KB, so its 137-VGPR kernel runs 3 waves/SIMD)
-    static constexpr int kRegion = (FULL ? 3 : 2) * kSlots * kRow;
+    // COOP output staging [ch][frame][instance] (kOutCh below): in the chorus it overlays the pitch
+    // windows' staging area (LDS is at its 2-waves/SIMD limit); the pitch-shifter has room for its own
+    static constexpr uint32_t kOutCh = 544, kOutFloats = kOutCh + 16 * 32;
+    static constexpr uint32_t kOutBase = FULL ? 0u : (uint32_t)(2 * kSlots * kRow);
+    static constexpr int kRegion = (FULL ? 3 : 2) * kSlots * kRow + (COOP && !FULL ? (int)kOutFloats : 0);
     static constexpr int kStride = 36;
     static constexpr uint32_t kPsvBase = 32u * kStride;
+    // (the channel planes 544 floats apart: conflict-free per-frame writes; in the chorus below the
+    // psv staging, which must survive into the next chunk)
+    static_assert(!FULL || kOutFloats <= kPsvBase, "output staging must not reach the psv staging");
     static constexpr int kTaps = FULL ? 3 : 2;
     static_assert(2 * 32 * kStride <= kRegion, "staging must fit in the window region");
 
@@ -273,15 +293,50 @@ struct ChStageL {
         }
     }
 
+    // COOP input: row r = 8 q + lane / 8 of instruction q is (frame r / 2, channel r % 2) of
+    // instances 4 (lane % 8) .. + 3 -> the staging [j][2 frame + ch]; then each lane reads its own
+    __device__ __forceinline__ static uint32_t coop_row(int q, uint32_t lane_) { return (uint32_t)q * 8u + (lane_ >> 3); }
+    __device__ __forceinline__ void stage_rows(const float4 (&xq)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float *st = region + (lane & 7u) * 4u * kStride + coop_row(q, lane);
+            st[0] = xq[q].x;
+            st[kStride] = xq[q].y;
+            st[2 * kStride] = xq[q].z;
+            st[3 * kStride] = xq[q].w;
+        }
+    }
+    __device__ __forceinline__ void read_own(float (&v)[kChunk], int Cv) const {
+        const float *st = region + j * kStride + ch;
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k) v[k] = k < Cv ? st[2 * k] : 0.f;
+    }
+    // COOP output: frame k of this lane -> [ch][k][j]; coop_out(q) = row 8 q + lane / 8 (frame,
+    // channel) of instances 4 (lane % 8) .. + 3, after the chunk
+    __device__ __forceinline__ void out_stage(int k, float v) { region[kOutBase + ch * kOutCh + (uint32_t)k * 32u + j] = v; }
+    __device__ __forceinline__ float4 coop_out(int q) const {
+        const uint32_t r = coop_row(q, lane);
+        return *(const float4 *)(region + kOutBase + (r & 1u) * kOutCh + (r >> 1) * 32u + (lane & 7u) * 4u);
+    }
+
     // first chunk of the launch: store its inputs, then load both lines of every window (fresh).
-    // XPREV: no store (chunk 0 stores its own input), x is unused
-    __device__ __forceinline__ void begin(const float (&x)[kChunk], int C) {
-        if (!XPREV) {
+    // XPREV: no store (chunk 0 stores its own input), x is unused.  COOP: x is read from xq.
+    __device__ __forceinline__ void begin(float (&x)[kChunk], int C, const float4 (&xq)[4]) {
+        if (COOP) {
+            stage_rows(xq);
+            coop_store(true, 0, wpos, C);
+            read_own(x, C);
+        } else if (!XPREV) {
             stage_run(x, 0);
             coop_store(true, 0, wpos, C);
         }
         pl = plan_chunk_l<kWin>(lfo_acc, lfo_inc, lfo_off, ps_acc, ps_inc, C, D, W, pmax, cmax, FULL);
         load_lines<0>(pl, wpos, true);
+    }
+    __device__ __forceinline__ void begin(float (&x)[kChunk], int C) {
+        static_assert(!COOP, "COOP stages begin with the cooperative rows");
+        const float4 none[4] = {};
+        begin(x, C, none);
     }
 
     // One chunk; PAR = chunk parity (the line set holding this chunk's line L'+1).
@@ -289,8 +344,8 @@ struct ChStageL {
     // chunk c+1's plan and line loads
     template <int PAR>
     __device__ __forceinline__ void stores_and_next(const float (&psv)[kChunk], const float (&x)[kChunk],
-                                                    const float (&xn)[kChunk], uint32_t w0, int C, int Cn,
-                                                    uint64_t lfo0, uint64_t ps0) {
+                                                    float (&xn)[kChunk], const float4 (&xq)[4], uint32_t w0,
+                                                    int C, int Cn, uint64_t lfo0, uint64_t ps0) {
         if (FULL) {
             stage_run(psv, kPsvBase);
             coop_store(false, kPsvBase, w0, C);
@@ -298,6 +353,12 @@ struct ChStageL {
         if (XPREV) {                                    // this chunk's own input
             stage_run(x, 0);
             coop_store(true, 0, w0, C);
+        } else if (COOP) {                              // x_{c+1}: rows -> staging -> ring and lanes
+            if (Cn > 0) {
+                stage_rows(xq);
+                coop_store(true, 0, w0 + (uint32_t)C, Cn);
+            }
+            read_own(xn, Cn);
         } else if (Cn > 0) {
             stage_run(xn, 0);
             coop_store(true, 0, w0 + (uint32_t)C, Cn);
@@ -319,8 +380,8 @@ struct ChStageL {
     //      plan chunk c+1, issue its line loads (they see both stores)
     //   C  chorus tap + lores~ + outputs (the cover for those loads)
     template <int PAR, class Sink, class Prefetch>
-    __device__ __forceinline__ void chunk(const float (&x)[kChunk], const float (&xn)[kChunk], int C, int Cn,
-                                          Sink &&sink, Prefetch &&prefetch) {
+    __device__ __forceinline__ void chunk(const float (&x)[kChunk], float (&xn)[kChunk], int C, int Cn,
+                                          Sink &&sink, Prefetch &&prefetch, const float4 (&xq)[4]) {
         // Everything lane-dependent is recomputed per chunk from a lane index the compiler must
         // treat as new: hoisted loop invariants (ring and LDS addresses) were spilled under the
         // pressure of the 96 line registers, and each scratch reload is a vmcnt(0) drain.
@@ -330,7 +391,7 @@ struct ChStageL {
         const uint32_t w0 = wpos;
         const uint64_t lfo0 = lfo_acc, ps0 = ps_acc;     // the phasors at the chunk's first frame
         const PlanL cur = pl;
-        float psv[kChunk];
+        float psv[kChunk], yo[kChunk];
         float *wP0 = region + 0 * kSlots * kRow + lane;
         float *wP1 = region + 1 * kSlots * kRow + lane;
         float *wC = region + 2 * kSlots * kRow + lane;
@@ -392,7 +453,7 @@ struct ChStageL {
                     gA0 = pair_even(m_gA); gA1 = pair_odd(m_gA);
                     gB0 = pair_even(m_gB); gB1 = pair_odd(m_gB);
                 }
-                const uint32_t ph = (uint32_t)(ps_acc >> 32);
+                const uint32_t ph = hi32(ps_acc);
                 const float d0 = (float)(ph >> 8) * Ws;
                 const float d1 = (float)((ph + 0x80000000u) >> 8) * Ws;
                 ps_acc += ps_inc;
@@ -425,6 +486,7 @@ struct ChStageL {
             float pl_lfo[2], pl_gA[2], pl_gB[2];
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) {
+                if (COOP && FULL) yo[k] = 0.f;
                 if ((k & 1) == 0) {
                     const uint64_t la = lfo_acc + (ch ? lfo_inc : 0ull), pa = ps_acc + (ch ? ps_inc : 0ull);
                     const float m_lfo = cos2pi(unit24h(la + lfo_off));
@@ -475,12 +537,20 @@ struct ChStageL {
                     z2 = b2 * wet - a2 * lp;
                     out = x[k] * dry + lp * mix;
                 }
-                sink(k, out);
+                if (COOP && FULL) yo[k] = out;
+                else sink(k, out);
             }
         }
         // one call site: line registers loaded on two paths meet in a phi, and the copies it needs
         // pushed the kernel from 211 VGPRs to 256 + spills
-        stores_and_next<PAR>(psv, x, xn, w0, C, Cn, lfo0, ps0);
+        stores_and_next<PAR>(psv, x, xn, xq, w0, C, Cn, lfo0, ps0);
+        if (COOP && FULL && !fast) {
+            // the generic chunk's outputs leave after the stores and staging above (a COOP sink
+            // writes LDS that was the pitch windows until then)
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k)
+                if (k < C) sink(k, yo[k]);
+        }
         if (fast) {
             // C. the chorus tap + lores~ (reads independent of each other; only the biquad is serial),
             //    the cover for chunk c+1's line loads
