@@ -84,17 +84,6 @@ __device__ __forceinline__ int floor_delay(float d, float dmin, float dmax) {
 
 __device__ __forceinline__ float lerp_pair(float x0, float x1, float fr) { return x0 + fr * (x1 - x0); }
 
-// cos(2 pi x) for |x| <= 0.25: cos2pi() (olfx_internal.h) with its range reduction folded away.
-// There u = x - rint(x) = x, a = |x| <= 0.25 never takes the reflected branch, and
-// (x 2pi)^2 == (|x| 2pi)^2 exactly: bit-identical results, six fewer instructions.
-__device__ __forceinline__ float cos2pi_q(float x) {
-    const float th = x * 6.28318530717958647692f;
-    const float t2 = th * th;
-    return 1.0f + t2 * (-0.5f + t2 * (4.16666666666666666667e-2f +
-           t2 * (-1.38888888888888888889e-3f + t2 * (2.48015873015873015873e-5f +
-           t2 * (-2.75573192239858906526e-7f + t2 * (2.08767569878680989792e-9f +
-           t2 * (-1.14707455977297247139e-11f)))))));
-}
 // a value of lane 2j (EVEN) or 2j+1 (odd) to both lanes of the pair: DPP quad_perm [0,0,2,2] / [1,1,3,3]
 __device__ __forceinline__ float pair_even(float v) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xA0, 0xF, 0xF, false));

@@ -399,34 +399,49 @@ struct ChStageL {
         // tap C first: psv_{c-1}, still in its LDS staging (region + kPsvBase, under taps A/B),
         // is not in a carried line -- patch it in, then stage taps A and B over the staging
         if (FULL) {
-            stage_tap<PAR, 2>();
-            if (started && cur.sC > -kWin - kChunk) {
+            // psv_{c-1}'s frame k goes to slot k - 16 - sC when that lies in the window: all 16 read
+            // first (a read after a store that may alias it would wait for the store, slot by slot),
+            // then stored exec-masked at constant offsets from the window's slot for k = 0
+            const bool need = started && cur.sC > -kWin - kChunk;
+            float pv[kChunk];
+            if (need) {
                 const float *prev = region + kPsvBase + j * kStride + ch;
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) wC[junk_or(k - kChunk - cur.sC) * kRow] = prev[2 * k];
+                for (int k = 0; k < kChunk; ++k) pv[k] = prev[2 * k];
+            }
+            stage_tap<PAR, 2>();
+            if (need) {
+                const int lo = kChunk + cur.sC;          // frames k in [lo, lo + kWin) land in the window
+                float *pC = wC - lo * kRow;
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k)
+                    if (k >= lo && k < lo + kWin) pC[k * kRow] = pv[k];
             }
         }
         stage_tap<PAR, 0>();
         stage_tap<PAR, 1>();
         // XPREV: x_{c-1} is not in a carried line (stored during chunk c-1, after its loads)
         if (XPREV && started) {
-            if (cur.sA > -kWin - kChunk) {
+            // frame k of x_{c-1} -> slot k - 16 - s when in the window (exec-masked, constant offsets)
+            const int loA = kChunk + cur.sA, loB = kChunk + cur.sB;
+            float *pA = wP0 - loA * kRow, *pB = wP1 - loB * kRow;
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) wP0[junk_or(k - kChunk - cur.sA) * kRow] = xp[k];
-            }
-            if (cur.sB > -kWin - kChunk) {
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) wP1[junk_or(k - kChunk - cur.sB) * kRow] = xp[k];
+            for (int k = 0; k < kChunk; ++k) {
+                if (k >= loA && k < loA + kWin) pA[k * kRow] = xp[k];
+                if (k >= loB && k < loB + kWin) pB[k * kRow] = xp[k];
             }
         }
-        // x_c is not in a carried line either
-        if (cur.sA > -kWin) {
+        // x_c is not in a carried line either.  Its slot k - s is >= 2 (a pitch window starts at
+        // s <= -4: delays are >= 1), so only the top can leave the window: one compare per frame,
+        // the store exec-masked at a constant offset from the window's frame-0 slot
+        {
+            const int limA = kWin + cur.sA, limB = kWin + cur.sB;
+            float *pA = wP0 - cur.sA * kRow, *pB = wP1 - cur.sB * kRow;
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) wP0[junk_or(k < C ? k - cur.sA : kWin) * kRow] = x[k];
-        }
-        if (cur.sB > -kWin) {
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) wP1[junk_or(k < C ? k - cur.sB : kWin) * kRow] = x[k];
+            for (int k = 0; k < kChunk; ++k) {
+                if (k < C && k < limA) pA[k * kRow] = x[k];
+                if (k < C && k < limB) pB[k * kRow] = x[k];
+            }
         }
         started = true;
         prefetch();
@@ -446,10 +461,11 @@ struct ChStageL {
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) {
                 if ((k & 1) == 0) {
-                    // gain arguments (p - 1/2)/2 lie in [-1/4, 1/4): cos2pi_q == cos2pi there
+                    // this lane's frame (k + ch): both window gains from its phase, then both
+                    // frames' gains to both lanes
                     const uint64_t pa = ps_acc + (ch ? ps_inc : 0ull);
-                    const float m_gA = cos2pi_q((unit24h(pa) - 0.5f) * 0.5f);
-                    const float m_gB = cos2pi_q((unit24h(pa + kHalfCycle) - 0.5f) * 0.5f);
+                    float m_gA, m_gB;
+                    win_gains(unit24h(pa), m_gA, m_gB);
                     gA0 = pair_even(m_gA); gA1 = pair_odd(m_gA);
                     gB0 = pair_even(m_gB); gB1 = pair_odd(m_gB);
                 }
@@ -490,8 +506,8 @@ struct ChStageL {
                 if ((k & 1) == 0) {
                     const uint64_t la = lfo_acc + (ch ? lfo_inc : 0ull), pa = ps_acc + (ch ? ps_inc : 0ull);
                     const float m_lfo = cos2pi(unit24h(la + lfo_off));
-                    const float m_gA = cos2pi((unit24h(pa) - 0.5f) * 0.5f);
-                    const float m_gB = cos2pi((unit24h(pa + kHalfCycle) - 0.5f) * 0.5f);
+                    float m_gA, m_gB;
+                    win_gains(unit24h(pa), m_gA, m_gB);
                     const float o_lfo = swap_pair(m_lfo), o_gA = swap_pair(m_gA), o_gB = swap_pair(m_gB);
                     pl_lfo[0] = ch ? o_lfo : m_lfo; pl_lfo[1] = ch ? m_lfo : o_lfo;
                     pl_gA[0] = ch ? o_gA : m_gA;    pl_gA[1] = ch ? m_gA : o_gA;

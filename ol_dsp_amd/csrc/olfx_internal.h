@@ -83,24 +83,40 @@ struct DattorroArgs {
 };
 
 // ----------------------------------------------------------------------------------------------
-// Deterministic cos(2*pi*x): used by the chorus LFO (RNBO cycle~) and the pitch-shifter
-// crossfade windows (gen~ cos).  Branch-free (selects only, no lane divergence): reduce to
-// b in [0, 1/4] exactly, then one Taylor polynomial of cos to theta^14 on [0, pi/2].  Only
-// +, -, *, rint and compares in a fixed order, so the host (oracle) and gfx950 produce identical
-// bits under -ffp-contract=off.  |err| < 3e-7.
+// Deterministic cos(2*pi*x): used by the chorus LFO (RNBO cycle~).  Branch-free (selects only, no
+// lane divergence): reduce to b in [0, 1/4] exactly, then one minimax polynomial of cos in
+// theta^2 on [0, pi/2] (degree 8, Remez, coefficients rounded to float; round 2 used the Taylor
+// series to theta^14: the same accuracy class at twice the operations).  Only +, -, *, rint and
+// compares in a fixed order, so the host (oracle) and gfx950 produce identical bits under
+// -ffp-contract=off.  |err| < 3e-7 (measured 1.8e-7; tests/test_oracle.py).
 // ----------------------------------------------------------------------------------------------
+OLFX_HD float cos_poly(float t2) {                 // cos(theta), t2 = theta^2, theta in [0, pi/2]
+    return 1.0f + t2 * (-0.4999993145465851f + t2 * (0.041663989424705505f +
+           t2 * (-0.001385592739097774f + t2 * 2.31943868129747e-05f)));
+}
+OLFX_HD float sin_poly(float th, float t2) {       // sin(theta), theta in [0, pi/2]
+    return th * (1.0f + t2 * (-0.16666656732559204f + t2 * (0.008333017118275166f +
+           t2 * (-0.00019806614727713168f + t2 * 2.6000548132287804e-06f))));
+}
 OLFX_HD float cos2pi(float x) {
     const float u = x - rintf(x);                  // exact, u in [-0.5, 0.5]
     const float a = u < 0.0f ? -u : u;             // cos is even
     const bool hi = a > 0.25f;
     const float b = hi ? 0.5f - a : a;             // exact (Sterbenz); cos(2pi(1/2-b)) = -cos(2pi b)
     const float th = b * 6.28318530717958647692f;
-    const float t2 = th * th;
-    const float r = 1.0f + t2 * (-0.5f + t2 * (4.16666666666666666667e-2f +
-                    t2 * (-1.38888888888888888889e-3f + t2 * (2.48015873015873015873e-5f +
-                    t2 * (-2.75573192239858906526e-7f + t2 * (2.08767569878680989792e-9f +
-                    t2 * (-1.14707455977297247139e-11f)))))));
+    const float r = cos_poly(th * th);
     return hi ? -r : r;
+}
+// The pitch-shifter's crossfade windows at phasor phase p in [0, 1) (pitchshift.gendsp: tap 0's
+// gain cos((p - 1/2) pi), tap 1's cos((p1 - 1/2) pi) with p1 = (p + 1/2) mod 1) are sin(pi p) and
+// |cos(pi p)|, i.e. sin(pi q) and cos(pi q) for q = min(p, 1 - p) in [0, 1/2] (1 - p is exact: p is
+// a 24-bit fraction): one argument, two short polynomials.
+OLFX_HD void win_gains(float p, float &g0, float &g1) {
+    const float q = fminf(p, 1.0f - p);
+    const float th = q * 3.14159265358979323846f;
+    const float t2 = th * th;
+    g0 = sin_poly(th, t2);
+    g1 = cos_poly(t2);
 }
 
 // ----------------------------------------------------------------------------------------------

@@ -12,8 +12,9 @@
  *   - fp32 arithmetic (gen~/RNBO compute in double);
  *   - phasors as 64-bit fixed-point accumulators (2^64 = one cycle; the increment rounding drifts a
  *     phase by < 2^-64 cycle per sample), their top 24 bits -> the float phase (exact);
- *   - cos(2 pi x) by a fixed polynomial (cos2pi below), standing in for cycle~'s wavetable and
- *     gen~'s cos;
+ *   - cos(2 pi x) by a fixed minimax polynomial (oracle_cos2pi below), standing in for cycle~'s
+ *     wavetable, and the crossfade windows cos((p - .5) pi) by sin / cos polynomials of one
+ *     argument (oracle_win_gains), standing in for gen~'s cos;
  *   - gen Delay.read: linear interpolation, delay clamped to [1, size-2] (read before write);
  *     RNBO delay~: linear interpolation, delay clamped to [0, size-2] (write before read);
  *   - lores~: RBJ biquad low-pass (transposed direct form II), Q = 1/sqrt(2) + 20 q^3.
@@ -51,8 +52,22 @@ static uint64_t fix64(double cycles)
 /* the float phase of a 64-bit accumulator: its top 24 bits, exact in fp32 */
 static float unit24(uint64_t acc) { return (float)((uint32_t)(acc >> 32) >> 8) * 5.9604644775390625e-8f; }
 
-/* cos(2 pi x): reduce to b in [0, 1/4] (exact), one Taylor polynomial of cos to theta^14 on
-   [0, pi/2]; same operations in the same order as the GPU (spec choice) */
+/* minimax polynomials on [0, pi/2] in theta^2 (degree 8 cos, degree 9 sin; Remez, coefficients
+   rounded to float): the same operations in the same order as the GPU (spec choice, DESIGN.md
+   section 3) */
+static float cos_poly(float t2)
+{
+    return 1.0f + t2 * (-0.4999993145465851f + t2 * (0.041663989424705505f +
+           t2 * (-0.001385592739097774f + t2 * 2.31943868129747e-05f)));
+}
+
+static float sin_poly(float th, float t2)
+{
+    return th * (1.0f + t2 * (-0.16666656732559204f + t2 * (0.008333017118275166f +
+           t2 * (-0.00019806614727713168f + t2 * 2.6000548132287804e-06f))));
+}
+
+/* cos(2 pi x): reduce to b in [0, 1/4] (exact), then cos_poly */
 float oracle_cos2pi(float x)
 {
     const float u = x - rintf(x);
@@ -60,12 +75,19 @@ float oracle_cos2pi(float x)
     const int hi = a > 0.25f;
     const float b = hi ? 0.5f - a : a;
     const float th = b * 6.28318530717958647692f;
-    const float t2 = th * th;
-    const float r = 1.0f + t2 * (-0.5f + t2 * (4.16666666666666666667e-2f +
-                    t2 * (-1.38888888888888888889e-3f + t2 * (2.48015873015873015873e-5f +
-                    t2 * (-2.75573192239858906526e-7f + t2 * (2.08767569878680989792e-9f +
-                    t2 * (-1.14707455977297247139e-11f)))))));
+    const float r = cos_poly(th * th);
     return hi ? -r : r;
+}
+
+/* the crossfade windows of the pitch-shifter at phase p (pitchshift.gendsp: cos((p0 - .5) pi) and
+   cos((p1 - .5) pi), p1 = (p0 + .5) % 1) = sin(pi q), cos(pi q), q = min(p, 1 - p) */
+void oracle_win_gains(float p, float *g0, float *g1)
+{
+    const float q = fminf(p, 1.0f - p);
+    const float th = q * 3.14159265358979323846f;
+    const float t2 = th * th;
+    *g0 = sin_poly(th, t2);
+    *g1 = cos_poly(t2);
 }
 
 typedef struct {
@@ -193,8 +215,8 @@ static void chorus_frame(const oracle_chorus *o, const chcoef_t *k, chstate_t *s
     const float p0 = unit24(s->ps_acc);
     const float p1 = unit24(s->ps_acc + 0x8000000000000000ull);
     s->ps_acc += k->ps_inc;
-    const float g0 = oracle_cos2pi((p0 - 0.5f) * 0.5f);
-    const float g1 = oracle_cos2pi((p1 - 0.5f) * 0.5f);
+    float g0, g1;
+    oracle_win_gains(p0, &g0, &g1);
     const float d0 = p0 * k->W, d1 = p1 * k->W;
     for (int c = 0; c < 2; c++) {
         const float t0 = read_frac(s->pring[c], pmask, w, d0, 1.0f, pmax);

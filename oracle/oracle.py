@@ -60,6 +60,8 @@ def lib(o0: bool = False) -> ctypes.CDLL:
         L.oracle_fnv1a64_lr.argtypes = [_PF, _PF, ctypes.c_long, ctypes.c_long]
         L.oracle_cos2pi.restype = _F
         L.oracle_cos2pi.argtypes = [_F]
+        L.oracle_win_gains.restype = None
+        L.oracle_win_gains.argtypes = [_F, ctypes.POINTER(_F), ctypes.POINTER(_F)]
         L.oracle_chorus_create.restype = ctypes.c_void_p
         L.oracle_chorus_create.argtypes = [ctypes.c_int, _F, ctypes.c_int]
         L.oracle_chorus_destroy.argtypes = [ctypes.c_void_p]

@@ -148,8 +148,8 @@ def test_chorus_fp32_deviation_from_double(golden, key, mode):
     """The spec's declared deviation (fp32 arithmetic, 64-bit fixed-point phasors) MEASURED against
     the same graph in double precision with double phasors (gen~ / RNBO arithmetic,
     oracle/chorus_ref_f64.c) on the golden inputs (6 instances x 6,000 frames of white noise).
-    Measured (round 3, 64-bit phasors): chorus max |d| / max(|ref|, rms) 1.58e-4 (SNR 93.5 dB),
-    pitch-shift 1.29e-4 (93.3 dB) -- the fp32 arithmetic alone: rounding the double restatement's
+    Measured (round 3, 64-bit phasors, minimax cosines): chorus max |d| / max(|ref|, rms) 1.62e-4
+    (SNR 93.3 dB), pitch-shift 1.29e-4 (93.3 dB) -- the fp32 arithmetic alone: rounding the double restatement's
     increments to the spec's fixed point changes nothing measurable.  (Round 2's 32-bit phasor
     increments drifted the LFO phase: 1.51e-3 / 4.2e-4.)  Parity stays unpinned (RNBO / genlib
     absent); this bounds only the arithmetic."""
@@ -179,6 +179,24 @@ def test_cos2pi_accuracy():
     xs = np.linspace(-3, 3, 20001).astype(np.float32)
     got = np.array([O.lib().oracle_cos2pi(float(v)) for v in xs], np.float64)
     assert np.max(np.abs(got - np.cos(2 * np.pi * xs.astype(np.float64)))) < 3e-7
+
+
+def test_window_gains_accuracy():
+    """The pitch-shifter's crossfade windows (pitchshift.gendsp: cos((p0 - 1/2) pi) for tap 0 and
+    cos((p1 - 1/2) pi), p1 = (p0 + 1/2) mod 1, for tap 1) from one argument, sin / cos of
+    pi min(p, 1 - p): within 3e-7 of both cosines over 24-bit phases, and exact at the ends."""
+    import ctypes
+    L = O.lib()
+    ps = (np.arange(0, 1 << 24, 997, dtype=np.int64).astype(np.float64) / (1 << 24))
+    g0, g1 = ctypes.c_float(), ctypes.c_float()
+    e = 0.0
+    for p in ps:
+        L.oracle_win_gains(float(p), ctypes.byref(g0), ctypes.byref(g1))
+        p1 = (p + 0.5) % 1.0
+        e = max(e, abs(g0.value - np.cos((p - 0.5) * np.pi)), abs(g1.value - np.cos((p1 - 0.5) * np.pi)))
+    assert e < 3e-7, e
+    L.oracle_win_gains(0.0, ctypes.byref(g0), ctypes.byref(g1))
+    assert g0.value == 0.0 and g1.value == 1.0
 
 
 def test_chorus_behaviour():

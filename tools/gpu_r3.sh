@@ -9,6 +9,7 @@
 #   prof       rocprofv3 kernel stats of the default line
 #   prof_ctl   rocprofv3 kernel stats of the voice / chain legs, one CSV per workload
 #   wl:<name>  one workload's bench line, kernel stats and HBM traffic passes
+#   util       utilisation counter passes (UTIL_WLS, default chorus fxrack voice chain chain_65536)
 set -u
 out=gpurun_out
 mkdir -p "$out"
@@ -69,6 +70,8 @@ for m in "$@"; do
       for w in voice voice_events chain chain_cc chain_65536; do
         prof "$w" 300 --workload "$w" --also "" --steps 20 --warmup 5 --cpu-seconds 0
       done ;;
+    util)      # utilisation counters (tools/pmc_util.sh) of the VERDICT's kernels
+      step util 900 bash tools/pmc_util.sh "${UTIL_WLS:-chorus fxrack voice chain chain_65536}" 10 ;;
     wl:*)      # one workload: bench line, kernel stats, HBM traffic passes (tools/traffic_r2.sh)
       w=${m#wl:}
       step "bench_$w" 300 python bench.py --workload "$w" --also "" --steps 20 --warmup 5 --cpu-seconds 0
