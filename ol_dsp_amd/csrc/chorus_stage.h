@@ -91,6 +91,8 @@ __device__ __forceinline__ float pair_even(float v) {
 __device__ __forceinline__ float pair_odd(float v) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xF5, 0xF, 0xF, false));
 }
+__device__ __forceinline__ int pair_even_i(int v) { return __builtin_amdgcn_mov_dpp(v, 0xA0, 0xF, 0xF, false); }
+__device__ __forceinline__ int pair_odd_i(int v) { return __builtin_amdgcn_mov_dpp(v, 0xF5, 0xF, 0xF, false); }
 // split_delay with the clamp as one v_med3 (identical to fminf(fmaxf()) for non-NaN delays,
 // and delays here are phasor arithmetic, never NaN)
 __device__ __forceinline__ void split_delay3(float d, float dmin, float dmax, int &di, float &fr) {

@@ -455,32 +455,41 @@ struct ChStageL {
             //     never reads a position newer than its own, so writing them all first is the same
             //     as writing each just before its frame;
             //  (C, the chorus tap, follows the ring stores and chunk c+1's line loads below)
-            // p W == (hi >> 8) (W 2^-24) exactly (scaling by a power of two is exact)
+            // p W == (hi >> 8) (W 2^-24) exactly (scaling by a power of two is exact).  L and R
+            // lanes share every tap delay: per pair of frames each lane computes its own frame's
+            // (k + ch) gains and delay splits once, and DPP hands both frames' values to both lanes;
+            // slot offsets are kept relative to the pair's first frame, whose part of the address
+            // is an immediate offset
             const float Ws = W * 5.9604644775390625e-8f;
-            float gA0 = 0.f, gA1 = 0.f, gB0 = 0.f, gB1 = 0.f;
+            const int chA = (int)ch - cur.sA, chB = (int)ch - cur.sB;
+            float gA0 = 0.f, gA1 = 0.f, gB0 = 0.f, gB1 = 0.f, fA0 = 0.f, fA1 = 0.f, fB0 = 0.f, fB1 = 0.f;
+            int rA0 = 0, rA1 = 0, rB0 = 0, rB1 = 0;
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) {
                 if ((k & 1) == 0) {
-                    // this lane's frame (k + ch): both window gains from its phase, then both
-                    // frames' gains to both lanes
                     const uint64_t pa = ps_acc + (ch ? ps_inc : 0ull);
+                    const uint32_t ph = hi32(pa);
                     float m_gA, m_gB;
-                    win_gains(unit24h(pa), m_gA, m_gB);
+                    win_gains(unit24(ph), m_gA, m_gB);
                     gA0 = pair_even(m_gA); gA1 = pair_odd(m_gA);
                     gB0 = pair_even(m_gB); gB1 = pair_odd(m_gB);
+                    int di; float fr;
+                    split_delay3((float)(ph >> 8) * Ws, 1.0f, pmax, di, fr);
+                    const int ra = chA - di;
+                    rA0 = pair_even_i(ra); rA1 = pair_odd_i(ra);
+                    fA0 = pair_even(fr); fA1 = pair_odd(fr);
+                    split_delay3((float)((ph + 0x80000000u) >> 8) * Ws, 1.0f, pmax, di, fr);
+                    const int rb = chB - di;
+                    rB0 = pair_even_i(rb); rB1 = pair_odd_i(rb);
+                    fB0 = pair_even(fr); fB1 = pair_odd(fr);
                 }
-                const uint32_t ph = hi32(ps_acc);
-                const float d0 = (float)(ph >> 8) * Ws;
-                const float d1 = (float)((ph + 0x80000000u) >> 8) * Ws;
                 ps_acc += ps_inc;
-                int di; float fr;
-                split_delay3(d0, 1.0f, pmax, di, fr);
-                int jw = k - di - cur.sA;
-                const float tA = lerp_pair(wP0[jw * kRow], wP0[(jw - 1) * kRow], fr);
-                split_delay3(d1, 1.0f, pmax, di, fr);
-                jw = k - di - cur.sB;
-                const float tB = lerp_pair(wP1[jw * kRow], wP1[(jw - 1) * kRow], fr);
-                psv[k] = tB * ((k & 1) ? gB1 : gB0) + tA * ((k & 1) ? gA1 : gA0);
+                const bool odd = k & 1;
+                const float *qA = wP0 + (k & ~1) * kRow + (odd ? rA1 : rA0) * kRow;
+                const float *qB = wP1 + (k & ~1) * kRow + (odd ? rB1 : rB0) * kRow;
+                const float tA = lerp_pair(qA[0], qA[-kRow], odd ? fA1 : fA0);
+                const float tB = lerp_pair(qB[0], qB[-kRow], odd ? fB1 : fB0);
+                psv[k] = tB * (odd ? gB1 : gB0) + tA * (odd ? gA1 : gA0);
             }
             if (FULL) {
 #pragma unroll
@@ -571,19 +580,25 @@ struct ChStageL {
             // C. the chorus tap + lores~ (reads independent of each other; only the biquad is serial),
             //    the cover for chunk c+1's line loads
             if (FULL) {
-                float l0 = 0.f, l1 = 0.f;
+                // the tap delay shared by L and R as in phase A: each lane splits its own frame's
+                // (k + ch) delay, DPP hands both frames' slot offsets and fractions to both lanes
+                const int chC = (int)ch - cur.sC;
+                int r0 = 0, r1 = 0;
+                float f0 = 0.f, f1 = 0.f;
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) {
                     if ((k & 1) == 0) {
                         const float m_lfo = cos2pi(unit24h(lfo_acc + (ch ? lfo_inc : 0ull) + lfo_off));
-                        l0 = pair_even(m_lfo); l1 = pair_odd(m_lfo);
+                        int di; float fr;
+                        split_delay3(m_lfo * D + D, 0.0f, cmax, di, fr);
+                        const int rc = chC - di;
+                        r0 = pair_even_i(rc); r1 = pair_odd_i(rc);
+                        f0 = pair_even(fr); f1 = pair_odd(fr);
                     }
-                    const float dch = ((k & 1) ? l1 : l0) * D + D;
                     lfo_acc += lfo_inc;
-                    int di; float fr;
-                    split_delay3(dch, 0.0f, cmax, di, fr);
-                    const int jw = k - di - cur.sC;
-                    const float wet = lerp_pair(wC[jw * kRow], wC[(jw - 1) * kRow], fr);
+                    const bool odd = k & 1;
+                    const float *qC = wC + (k & ~1) * kRow + (odd ? r1 : r0) * kRow;
+                    const float wet = lerp_pair(qC[0], qC[-kRow], odd ? f1 : f0);
                     const float lp = b0 * wet + z1;
                     z1 = (b1 * wet - a1 * lp) + z2;
                     z2 = b2 * wet - a2 * lp;
