@@ -48,6 +48,10 @@ __device__ __forceinline__ float sin_quarter(float x) {
     return x + (x * x2) * p;
 }
 
+// packed FP32 (v_pk_mul_f32 / v_pk_add_f32: two IEEE operations per lane and instruction, the same
+// bits as two scalar ones)
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 // daisysp::LadderFilter's tanh: Pade approximant, saturating beyond |x| > 3 (the exact division
 // keeps it bit-identical with the oracle)
 __device__ __forceinline__ float ladder_tanh(float x) {
@@ -371,7 +375,7 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
 // FOUR role waves per workgroup of 64 voices (two workgroups per CU, two waves per SIMD):
 //   ENV  : the amp and filter Adsr, the cutoff sum                            -> (amp, fc_in)
 //   OSC  : Port, the oscillator's phase, the polyBLEP saw                     -> (src, amp)
-//   FREQ : Svf::SetFreq(fc_in)                                                -> (fq, damp)
+//   FREQ : Svf::SetFreq(fc_in)                                                -> (-damp, fq)
 //   FILT : the two Svf passes, Low() * amp, the output store
 // A three-stage pipeline over 8-sample chunks (kVcChunk): at step k ENV makes chunk k, OSC and FREQ chunk
 // k-1, FILT chunk k-2; one barrier per step; 24 KB of LDS per workgroup.  Measured per role (16-sample chunks,
@@ -384,7 +388,7 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
 __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     __shared__ float2 eq[2][kVcChunk][64];      // ENV -> OSC, FREQ: (amp, fc_in)
     __shared__ float2 sq[2][kVcChunk][64];      // OSC -> FILT: (src, amp)
-    __shared__ float2 fdq[2][kVcChunk][64];     // FREQ -> FILT: (fq, damp)
+    __shared__ float2 fdq[2][kVcChunk][64];     // FREQ -> FILT: (-damp, fq)
     __shared__ uint2 evslot[64];                // ENV's staging of the block's events (OSC reads it)
     const uint32_t n = a.n;
     const uint32_t lane = threadIdx.x & 63;
@@ -429,12 +433,20 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     // redone sample by sample from its start with the exact segment machine.
                     const float xa0 = ea.x, xf0 = ef.x;
                     bool ended = false;
+                    // both envelopes' Env::step_spec in packed operations (the pair lives in a
+                    // register pair for the chunk), then (x_a amp_amt, x_f 20000)
+                    f2 X = {ea.x, ef.x};
+                    const f2 D0 = {ea.d0, ef.d0}, T = {ea.tgt, ef.tgt}, AMT = {amp_amt, 20000.0f};
 #pragma unroll
                     for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) {
-                        const float amp = ea.step_spec(ended) * amp_amt;
-                        const float fe = ef.step_spec(ended);
-                        qo[j * 64] = make_float2(amp, cutoff + ((fe * 20000.0f) * fenv_amt));
+                        const f2 xn = X + D0 * (T - X);
+                        ended = ended || xn.x > ea.hi || xn.x < ea.lo || xn.y > ef.hi || xn.y < ef.lo;
+                        X = xn;
+                        const f2 m = X * AMT;
+                        qo[j * 64] = make_float2(m.x, cutoff + m.y * fenv_amt);
                     }
+                    ea.x = X.x;
+                    ef.x = X.y;
                     if (__builtin_amdgcn_ballot_w64(ended)) {
                         ea.x = xa0;
                         ef.x = xf0;
@@ -502,15 +514,60 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
             if (k >= 1 && k + 1 < nsteps) {
                 const float2 *qi = &eq[(k - 1) & 1][0][lane];
                 float2 *qo = &fdq[(k - 1) & 1][0][lane];
-                for_chunk(len(k - 1), [&](uint32_t j) {
-                    const float fc = fminf(fmaxf(qi[j * 64].y, 1.0e-6f), fc_max);
-                    const float fcn = fc * inv_2sr;
-                    const float arg = 0.25f < fcn ? 0.25f : fcn;
-                    const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
-                    const float lim = 2.0f * __builtin_amdgcn_rcpf(fq) - fq * 0.5f;
-                    const float dlim = 2.0f < lim ? 2.0f : lim;
-                    qo[j * 64] = make_float2(fq, damp_res < dlim ? damp_res : dlim);
-                });
+                // hands FILT (-damp, fq): its notch src - damp band is src + (-damp) band, exactly
+                if (len(k - 1) == (uint32_t)kVcChunk) {
+                    // no recurrence here: two samples per packed operation, the chunk's four pairs
+                    // stage by stage (a packed result read by the next instruction costs a wait
+                    // state; four independent pairs fill them)
+                    constexpr int P = kVcChunk / 2;
+                    f2 x[P], x2[P], pp[P], fq[P];
+#pragma unroll
+                    for (int q = 0; q < P; ++q) {
+                        const float c0 = fminf(fmaxf(qi[(2 * q) * 64].y, 1.0e-6f), fc_max);
+                        const float c1 = fminf(fmaxf(qi[(2 * q + 1) * 64].y, 1.0e-6f), fc_max);
+                        const f2 fcn = (f2){c0, c1} * inv_2sr;
+                        const f2 arg = {0.25f < fcn.x ? 0.25f : fcn.x, 0.25f < fcn.y ? 0.25f : fcn.y};
+                        x[q] = 3.1415927410125732f * arg;
+                    }
+#pragma unroll
+                    for (int q = 0; q < P; ++q) x2[q] = x[q] * x[q];
+#pragma unroll
+                    for (int q = 0; q < P; ++q) pp[q] = (f2)2.7557319e-6f * x2[q];
+#pragma unroll
+                    for (int q = 0; q < P; ++q) pp[q] = pp[q] + -1.9841270e-4f;
+#pragma unroll
+                    for (int q = 0; q < P; ++q) pp[q] = pp[q] * x2[q];
+#pragma unroll
+                    for (int q = 0; q < P; ++q) pp[q] = pp[q] + 8.3333333e-3f;
+#pragma unroll
+                    for (int q = 0; q < P; ++q) pp[q] = pp[q] * x2[q];
+#pragma unroll
+                    for (int q = 0; q < P; ++q) pp[q] = pp[q] + -1.6666667e-1f;
+#pragma unroll
+                    for (int q = 0; q < P; ++q) x2[q] = x[q] * x2[q];
+#pragma unroll
+                    for (int q = 0; q < P; ++q) pp[q] = x2[q] * pp[q];
+#pragma unroll
+                    for (int q = 0; q < P; ++q) fq[q] = 2.0f * (x[q] + pp[q]);   // 2 sin_quarter
+#pragma unroll
+                    for (int q = 0; q < P; ++q) {
+                        const f2 rq = {__builtin_amdgcn_rcpf(fq[q].x), __builtin_amdgcn_rcpf(fq[q].y)};
+                        const f2 lim = 2.0f * rq - fq[q] * 0.5f;
+                        const float d0 = 2.0f < lim.x ? 2.0f : lim.x, d1 = 2.0f < lim.y ? 2.0f : lim.y;
+                        qo[(2 * q) * 64] = make_float2(-(damp_res < d0 ? damp_res : d0), fq[q].x);
+                        qo[(2 * q + 1) * 64] = make_float2(-(damp_res < d1 ? damp_res : d1), fq[q].y);
+                    }
+                } else {
+                    for (uint32_t j = 0; j < len(k - 1); ++j) {
+                        const float fc = fminf(fmaxf(qi[j * 64].y, 1.0e-6f), fc_max);
+                        const float fcn = fc * inv_2sr;
+                        const float arg = 0.25f < fcn ? 0.25f : fcn;
+                        const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
+                        const float lim = 2.0f * __builtin_amdgcn_rcpf(fq) - fq * 0.5f;
+                        const float dlim = 2.0f < lim ? 2.0f : lim;
+                        qo[j * 64] = make_float2(-(damp_res < dlim ? damp_res : dlim), fq);
+                    }
+                }
             }
             __syncthreads();
         }
@@ -526,13 +583,15 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                 const float2 *qf = &fdq[k & 1][0][lane];
                 for_chunk(len(k - 2), [&](uint32_t j) {
                     const float2 sa = qs[j * 64], fd = qf[j * 64];
-                    const float src = sa.x, fq = fd.x, damp = fd.y;
-                    float notch = src - damp * band;
+                    // (packing this serial recurrence's paired products cost as many register
+                    // moves as it saved operations: scalar)
+                    const float src = sa.x, ndamp = fd.x, fq = fd.y;     // FREQ hands over -damp
+                    float notch = src + ndamp * band;                    // == src - damp * band
                     low = low + fq * band;
                     float high = notch - low;
                     band = fq * high + band - drive * band * band * band;
                     float out_low = 0.5f * low;
-                    notch = src - damp * band;
+                    notch = src + ndamp * band;
                     low = low + fq * band;
                     high = notch - low;
                     band = fq * high + band - drive * band * band * band;
