@@ -48,25 +48,30 @@ constexpr int kFrStride = 36;                       // staging floats per instan
 constexpr int kFrRegion = kFrSlots * 64 + 32 * kFrStride;   // floats of LDS per wave
 
 // Svf::Process (DaisySP, double-sampled Chamberlin) returning the selected output
-// (0 low, 1 band, 2 high, 3 notch, 4 peak), as oracle/fxrack_ref.c
+// (0 low, 1 band, 2 high, 3 notch, 4 peak), as oracle/fxrack_ref.c.  Each output is the mean of its
+// two passes' values, 0.5 x1 + 0.5 x2: the pass's value is selected first and only the selected
+// output is formed (the same operations for it; the reference forms all five)
+__device__ __forceinline__ float svf_pick(uint32_t type, float low, float band, float high, float notch) {
+    float peak = low - high;
+    asm volatile("" : "+v"(peak));                  // computed for every lane: selects, not branches
+    float r = type == 4 ? peak : low;
+    r = type == 3 ? notch : r;
+    r = type == 2 ? high : r;
+    return type == 1 ? band : r;
+}
 __device__ __forceinline__ float svf_tick(float in, float freq, float damp, float drive, uint32_t type,
                                           float &low, float &band) {
     float notch = in - damp * band;
     low = low + freq * band;
     float high = notch - low;
     band = freq * high + band - drive * band * band * band;
-    float o_low = 0.5f * low, o_high = 0.5f * high, o_band = 0.5f * band;
-    float o_peak = 0.5f * (low - high), o_notch = 0.5f * notch;
+    const float x1 = svf_pick(type, low, band, high, notch);
     notch = in - damp * band;
     low = low + freq * band;
     high = notch - low;
     band = freq * high + band - drive * band * band * band;
-    o_low += 0.5f * low;
-    o_high += 0.5f * high;
-    o_band += 0.5f * band;
-    o_peak += 0.5f * (low - high);
-    o_notch += 0.5f * notch;
-    return type == 1 ? o_band : (type == 2 ? o_high : (type == 3 ? o_notch : (type == 4 ? o_peak : o_low)));
+    const float x2 = svf_pick(type, low, band, high, notch);
+    return 0.5f * x1 + 0.5f * x2;
 }
 
 // f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>), unrolled at compile time
@@ -209,7 +214,8 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v3(FxRackArgs a) {
             const uint32_t q = (uint32_t)r * 64u + lane, oo = q >> 3, f2 = 2u * (q & 7u);
             const float4 vv = *(const float4 *)(stage + oo * kFrStride + 2u * f2);
             const uint32_t oi = inst0 + oo;
-            if (oi < n && (int)f2 < Cp) ch::st4(rR, oo * kRing + wrap48k((int64_t)tp + f2) * 8u, vv);
+            const bool ok = oi < n && (int)f2 < Cp;     // else an offset past the buffer: dropped
+            ch::st4(rR, ok ? oo * kRing + wrap48k((int64_t)tp + f2) * 8u : 0xFFFFFFF0u, vv);
         }
 #pragma unroll
         for (int k = 0; k < kFrChunk; ++k)
@@ -223,14 +229,16 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v3(FxRackArgs a) {
         // ---- 1. this chunk's window -> LDS from its two lines, patched with the last two chunks'
         //         writes: line L was loaded before chunk c-2's stores, L + 1 before chunk c-1's ----
         stage_lines();
-        if (f0 >= 2u * kFrChunk) {
+        // (only delays below 2 chunks + a window reach those positions: skipped wave-uniformly
+        // otherwise; rel = -D - 1 or -D - 2)
+        if (f0 >= 2u * kFrChunk && __builtin_amdgcn_ballot_w64(-2 * kFrChunk - rel < kFrWin)) {
 #pragma unroll
             for (int k = 0; k < kFrChunk; ++k) {
                 const int s = k - 2 * kFrChunk - rel;   // slot of position t - 32 + k
                 if (s >= 0 && s < kFrWin) wcol[s * 64] = y2[k];
             }
         }
-        if (f0 > 0) {
+        if (f0 > 0 && __builtin_amdgcn_ballot_w64(-kFrChunk - rel < kFrWin)) {
 #pragma unroll
             for (int k = 0; k < kFrChunk; ++k) {
                 const int s = k - kFrChunk - rel;       // slot of position t - 16 + k
