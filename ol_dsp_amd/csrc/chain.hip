@@ -39,6 +39,9 @@ enum { F_C0 = 0, F_C1, F_PIN, F_POUT, F_DIN };   // chunks published by C0 / C1,
 
 }  // namespace
 
+// COOP: the C role takes its input as cooperative rows (4 x 16 B per lane and chunk instead of 16
+// single floats; ChStageL COOP, chorus.hip), for n and the plane distance multiples of 4
+template <bool COOP>
 __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int kChunk = 16;
@@ -60,27 +63,47 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) 
 
     if (wib < 2) {
         // ---------------- C: the chorus, per (instance, channel) lane ----------------
-        ch::ChStageL<true> s1;
+        using StageC = ch::ChStageL<true, false, COOP, false>;
+        StageC s1;
         const ch::Rsrc rIn = ch::rsrc(a.in, (a.plane + (uint64_t)nf * n) * 4);
         const uint32_t frame_b = n * 4u;
         for (uint32_t g = blockIdx.x, gi = 0; g < ngroups; g += gridDim.x, ++gi) {
             const uint32_t base = g * 64u, gc0 = gi * nchunks;
-            s1.init(a.c1, lds + wib * kChainRegion, lane, base + 32u * wib);
+            const uint32_t inst0 = base + 32u * wib;
+            s1.init(a.c1, lds + wib * kChainRegion, lane, inst0);
             const uint32_t io_v = s1.ch * (uint32_t)a.plane * 4u + s1.i * 4u;
             const uint32_t qcol = s1.ch * kQCh + 32u * wib + s1.j;
+            // COOP rows: (frame r / 2, channel r % 2) of instances inst0 + 4 (lane % 8) .. + 3
+            const uint32_t pinst = inst0 + (lane & 7u) * 4u;
+            auto row_v = [&](int q, uint32_t f0) {
+                const uint32_t r = StageC::coop_row(q, lane);
+                return (r & 1u) * (uint32_t)a.plane * 4u + min(f0 + (r >> 1), nf - 1u) * frame_b + pinst * 4u;
+            };
             float x[kChunk], xn[kChunk];
+            float4 xq[4];
             int C = (int)min((uint32_t)kChunk, nf);
+            if constexpr (COOP) {
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) x[k] = k < C ? ch::ld1(rIn, io_v, (uint32_t)k * frame_b) : 0.f;
-            s1.begin(x, C);
+                for (int q = 0; q < 4; ++q) xq[q] = ch::ld4(rIn, row_v(q, 0));
+                s1.begin(x, C, xq);
+            } else {
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) x[k] = k < C ? ch::ld1(rIn, io_v, (uint32_t)k * frame_b) : 0.f;
+                s1.begin(x, C);
+            }
             auto step = [&](auto par, uint32_t f0, uint32_t c) {
                 C = (int)min((uint32_t)kChunk, nf - f0);
                 const int Cn = f0 + kChunk < nf ? (int)min((uint32_t)kChunk, nf - f0 - kChunk) : 0;
                 auto prefetch = [&]() {                       // next chunk's input, clamped, unconditional
+                    if constexpr (COOP) {
 #pragma unroll
-                    for (int k = 0; k < kChunk; ++k) {
-                        const float v = ch::ld1(rIn, io_v, min(f0 + kChunk + (uint32_t)k, nf - 1u) * frame_b);
-                        xn[k] = k < Cn ? v : 0.f;
+                        for (int q = 0; q < 4; ++q) xq[q] = ch::ld4(rIn, row_v(q, f0 + kChunk));
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < kChunk; ++k) {
+                            const float v = ch::ld1(rIn, io_v, min(f0 + kChunk + (uint32_t)k, nf - 1u) * frame_b);
+                            xn[k] = k < Cn ? v : 0.f;
+                        }
                     }
                 };
                 // outputs to registers first, then to the queue: a store through a generic
@@ -88,7 +111,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) 
                 float y[kChunk];
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) y[k] = 0.f;
-                s1.template chunk<decltype(par)::value>(x, xn, C, Cn, [&](int k, float v) { y[k] = v; }, prefetch, kNoRows);
+                s1.template chunk<decltype(par)::value>(x, xn, C, Cn, [&](int k, float v) { y[k] = v; }, prefetch, xq);
                 const uint32_t gc = gc0 + c;
                 wait_for([&] { return flag_get(flags + F_PIN) + kDepth > gc; });   // buffer gc % kDepth free
                 float *q = q1 + (gc % kDepth) * kQBuf + qcol;
@@ -192,7 +215,9 @@ hipError_t launch_chain(const ChainArgs &a, hipStream_t s) {
     if (a.cus == 0) return hipErrorInvalidValue;
     const uint32_t groups = (a.n + 63u) / 64u;
     const uint32_t blocks = groups < a.cus ? groups : a.cus;
-    hipLaunchKernelGGL(chain_block_v5, dim3(blocks), dim3(kChainThreads), (size_t)kChainLds * sizeof(float), s, a);
+    const bool coop = (a.n & 3u) == 0 && (a.plane & 3u) == 0 && (((uintptr_t)a.in | (uintptr_t)a.out) & 15u) == 0;
+    if (coop) hipLaunchKernelGGL(chain_block_v5<true>, dim3(blocks), dim3(kChainThreads), (size_t)kChainLds * sizeof(float), s, a);
+    else hipLaunchKernelGGL(chain_block_v5<false>, dim3(blocks), dim3(kChainThreads), (size_t)kChainLds * sizeof(float), s, a);
     return hipGetLastError();
 }
 

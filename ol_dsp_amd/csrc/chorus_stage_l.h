@@ -98,7 +98,10 @@ __device__ __forceinline__ PlanL plan_chunk_l(uint64_t lfo_acc, uint64_t lfo_inc
 // transposes them through its LDS staging into the lanes' own frames; outputs go the same way
 // (out_stage / coop_out below).  4 + 4 wide vector-memory instructions per chunk instead of
 // 16 + 16 single-float ones (the per-CU vector-memory pipeline, TA/TD, is the busiest unit).
-template <bool FULL, bool XPREV = false, bool COOP = false>
+// OUT_LDS (default COOP): the sink writes the stage's LDS (out_stage), so a generic chunk emits its
+// outputs only after stores_and_next has finished with the pitch windows (the fused chain's C role
+// takes cooperative input but sinks into registers: OUT_LDS = false)
+template <bool FULL, bool XPREV = false, bool COOP = false, bool OUT_LDS = COOP>
 struct ChStageL {
     static_assert(!(COOP && XPREV), "cooperative input is for a stage whose input comes from HBM");
     static constexpr int kChunk = 16, kWin = 24, kSlots = kWin + 1;
@@ -108,7 +111,7 @@ struct ChStageL {
     // windows' staging area (LDS is at its 2-waves/SIMD limit); the pitch-shifter has room for its own
     static constexpr uint32_t kOutCh = 544, kOutFloats = kOutCh + 16 * 32;
     static constexpr uint32_t kOutBase = FULL ? 0u : (uint32_t)(2 * kSlots * kRow);
-    static constexpr int kRegion = (FULL ? 3 : 2) * kSlots * kRow + (COOP && !FULL ? (int)kOutFloats : 0);
+    static constexpr int kRegion = (FULL ? 3 : 2) * kSlots * kRow + (OUT_LDS && !FULL ? (int)kOutFloats : 0);
     static constexpr int kStride = 36;
     static constexpr uint32_t kPsvBase = 32u * kStride;
     // (the channel planes 544 floats apart: conflict-free per-frame writes; in the chorus below the
@@ -511,7 +514,7 @@ struct ChStageL {
             float pl_lfo[2], pl_gA[2], pl_gB[2];
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) {
-                if (COOP && FULL) yo[k] = 0.f;
+                if (OUT_LDS && FULL) yo[k] = 0.f;
                 if ((k & 1) == 0) {
                     const uint64_t la = lfo_acc + (ch ? lfo_inc : 0ull), pa = ps_acc + (ch ? ps_inc : 0ull);
                     const float m_lfo = cos2pi(unit24h(la + lfo_off));
@@ -562,14 +565,14 @@ struct ChStageL {
                     z2 = b2 * wet - a2 * lp;
                     out = x[k] * dry + lp * mix;
                 }
-                if (COOP && FULL) yo[k] = out;
+                if (OUT_LDS && FULL) yo[k] = out;
                 else sink(k, out);
             }
         }
         // one call site: line registers loaded on two paths meet in a phi, and the copies it needs
         // pushed the kernel from 211 VGPRs to 256 + spills
         stores_and_next<PAR>(psv, x, xn, xq, w0, C, Cn, lfo0, ps0);
-        if (COOP && FULL && !fast) {
+        if (OUT_LDS && FULL && !fast) {
             // the generic chunk's outputs leave after the stores and staging above (a COOP sink
             // writes LDS that was the pitch windows until then)
 #pragma unroll
