@@ -490,17 +490,74 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
             if (k >= 1 && k + 1 < nsteps) {
                 const float2 *qi = &eq[(k - 1) & 1][0][lane];
                 float2 *qo = &sq[(k - 1) & 1][0][lane];
-                for_chunk(len(k - 1), [&](uint32_t j) {
-                    port_z = freq + port_c * (port_z - freq);     // Port::Process (Portamento.h:218-221)
-                    const float inc = port_z * inv_sr;             // Oscillator::SetFreq
-                    const float t = phase;                         // Oscillator::Process reads, then advances
-                    phase += inc;
-                    phase = phase > 1.0f ? phase - 1.0f : phase;
-                    float o = (2.0f * t) - 1.0f;
-                    o -= polyblep(inc, t);
-                    o *= -1.0f;
-                    qo[j * 64] = make_float2(o * 0.5f, qi[j * 64].x);
-                });
+                if (len(k - 1) == (uint32_t)kVcChunk) {
+                    // only Port and the phase are recurrences: run them for the chunk, then the
+                    // polyBLEP saw per sample over four packed sample pairs (stage by stage, as FREQ)
+                    constexpr int P = kVcChunk / 2;
+                    f2 t[P], dt[P];
+#pragma unroll
+                    for (int q = 0; q < P; ++q) {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            port_z = freq + port_c * (port_z - freq);     // Port::Process (Portamento.h:218-221)
+                            const float inc = port_z * inv_sr;             // Oscillator::SetFreq
+                            t[q][h] = phase;                               // Oscillator::Process reads, then advances
+                            dt[q][h] = inc;
+                            phase += inc;
+                            phase = phase > 1.0f ? phase - 1.0f : phase;
+                        }
+                    }
+                    f2 num[P], qv[P], qq[P], rlo[P], rhi[P], o[P];
+                    bool lo[P][2], hi[P][2];
+#pragma unroll
+                    for (int q = 0; q < P; ++q) {
+                        const f2 one_m = 1.0f - dt[q];
+                        const f2 tm1 = t[q] - 1.0f;
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            lo[q][h] = t[q][h] < dt[q][h];
+                            hi[q][h] = !lo[q][h] && t[q][h] > one_m[h];
+                            num[q][h] = lo[q][h] ? t[q][h] : tm1[h];
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < P; ++q)
+                        qv[q] = num[q] * (f2){__builtin_amdgcn_rcpf(dt[q].x), __builtin_amdgcn_rcpf(dt[q].y)};
+#pragma unroll
+                    for (int q = 0; q < P; ++q) qq[q] = qv[q] * qv[q];
+#pragma unroll
+                    for (int q = 0; q < P; ++q) { rlo[q] = qv[q] + qv[q]; rhi[q] = qq[q] + qv[q]; }
+#pragma unroll
+                    for (int q = 0; q < P; ++q) { rlo[q] = rlo[q] - qq[q]; rhi[q] = rhi[q] + qv[q]; }
+#pragma unroll
+                    for (int q = 0; q < P; ++q) { rlo[q] = rlo[q] - 1.0f; rhi[q] = rhi[q] + 1.0f; o[q] = 2.0f * t[q]; }
+#pragma unroll
+                    for (int q = 0; q < P; ++q) {
+                        f2 blep;
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) blep[h] = lo[q][h] ? rlo[q][h] : (hi[q][h] ? rhi[q][h] : 0.0f);
+                        o[q] = (o[q] - 1.0f) - blep;
+                    }
+#pragma unroll
+                    for (int q = 0; q < P; ++q) {
+                        // o *= -1; o * 0.5 (== o * -0.5 exactly)
+                        const f2 y = (-o[q]) * 0.5f;
+                        qo[(2 * q) * 64] = make_float2(y.x, qi[(2 * q) * 64].x);
+                        qo[(2 * q + 1) * 64] = make_float2(y.y, qi[(2 * q + 1) * 64].x);
+                    }
+                } else {
+                    for (uint32_t j = 0; j < len(k - 1); ++j) {
+                        port_z = freq + port_c * (port_z - freq);
+                        const float inc = port_z * inv_sr;
+                        const float t = phase;
+                        phase += inc;
+                        phase = phase > 1.0f ? phase - 1.0f : phase;
+                        float o = (2.0f * t) - 1.0f;
+                        o -= polyblep(inc, t);
+                        o *= -1.0f;
+                        qo[j * 64] = make_float2(o * 0.5f, qi[j * 64].x);
+                    }
+                }
             }
             __syncthreads();
         }
