@@ -9,6 +9,7 @@
 #   prof       rocprofv3 kernel stats of the default line
 #   prof_ctl   rocprofv3 kernel stats of the voice / chain legs, one CSV per workload
 #   wl:<name>  one workload's bench line, kernel stats and HBM traffic passes
+#   final      default bench line + kernel stats of it and of every workload (one CSV each)
 #   util       utilisation counter passes (UTIL_WLS, default chorus fxrack voice chain chain_65536)
 set -u
 out=gpurun_out
@@ -68,6 +69,12 @@ for m in "$@"; do
       prof default 900 --steps 50 --warmup 5 --cpu-seconds 0 ;;
     prof_ctl)
       for w in voice voice_events chain chain_cc chain_65536; do
+        prof "$w" 300 --workload "$w" --also "" --steps 20 --warmup 5 --cpu-seconds 0
+      done ;;
+    final)     # the round's artifacts: default bench line, its kernel stats, per-workload stats
+      step bench_default 900 python bench.py --steps 20 --warmup 5
+      prof default 900 --steps 50 --warmup 5 --cpu-seconds 0
+      for w in chorus pitchshift dattorro chain chain_65536 voice voice_moog voice_events chain_cc fxrack; do
         prof "$w" 300 --workload "$w" --also "" --steps 20 --warmup 5 --cpu-seconds 0
       done ;;
     util)      # utilisation counters (tools/pmc_util.sh) of the VERDICT's kernels
