@@ -288,8 +288,13 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v3(FxRackArgs a) {
             if constexpr (!COMP) {
                 if constexpr (k >= 1) o[k - 1] = (ch ? so : (fw ? b0p : 0.0f)) * master;
             } else {
-                if constexpr (k >= 1)
-                    o[k - 1] = ch ? (pass0 ? b0p : so * master) : (comp ? a1p : (fw ? b0p : 0.0f)) * master;
+                if constexpr (k >= 1) {
+                    // every candidate in a register first: a select chain, not exec-mask branches
+                    float f_out = so * master, d_in = fw ? b0p : 0.0f;
+                    asm volatile("" : "+v"(f_out), "+v"(d_in));
+                    d_in = comp ? a1p : d_in;
+                    o[k - 1] = ch ? (pass0 ? b0p : f_out) : d_in * master;
+                }
             }
             if (frame_k) {
                 if constexpr (!COMP) {
@@ -304,10 +309,13 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v3(FxRackArgs a) {
                     // F on its raw read (channel 1 has no filter, FilterFx acts on channel 0 only)
                     const float da = ((ch ? r : so) * dbal) + (x[kk] * (1 - dbal));
                     // ReverbFx over the stub: on the delay's output, or on the input when alone
-                    const float src = topo == 3u ? x[kk] : da;
-                    const float rv = ((src * 0.8f) * rbal) + (src * (1 - rbal));
+                    float dav = da, xin = x[kk];
+                    const float src = topo == 3u ? xin : dav;
+                    float rv = ((src * 0.8f) * rbal) + (src * (1 - rbal));
+                    asm volatile("" : "+v"(rv), "+v"(dav), "+v"(xin));   // selects, not branches
                     // D: the value lane F filters / outputs next tick; F: its channel-1 output
-                    const float val = topo == 2u ? da : (topo == 4u ? x[kk] : rv);
+                    float val = topo == 4u ? xin : rv;
+                    val = topo == 2u ? dav : val;
                     b0p = ch::pair_even(val);
                     a1p = ch::pair_odd(val);
                 }
