@@ -382,17 +382,43 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
 // 18 steps; the others skipping their arithmetic): the skeleton (launch, state,
 // 18 barriers) 9.7 us, FREQ 10.0, FILT 15, OSC 20, ENV 26 of the kernel's 43.6 us.  The envelopes
 // of a full chunk run speculatively (Env::step_spec, no per-sample lane vote and branch) and the
-// chunk is redone exactly when a lane's segment ended in it.  Role = wave: rotating the roles of
-// co-resident workgroups was measured slower and is not built.
+// chunk is redone exactly when a lane's segment ended in it.  Roles are assigned by SIMD (below).
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     __shared__ float2 eq[2][kVcChunk][64];      // ENV -> OSC, FREQ: (amp, fc_in)
     __shared__ float2 sq[2][kVcChunk][64];      // OSC -> FILT: (src, amp)
     __shared__ float2 fdq[2][kVcChunk][64];     // FREQ -> FILT: (-damp, fq)
     __shared__ uint2 evslot[64];                // ENV's staging of the block's events (OSC reads it)
+    __shared__ uint32_t hw_simd[5];             // the SIMD of each wave; [4]: wave 0's slot parity
     const uint32_t n = a.n;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if OLFX_VOICE_ROLE_WAVE
+    const uint32_t role = wave;
+#else
+    // Roles by SIMD.  The roles' VALU loads differ (per 8-sample chunk FILT ~218, OSC ~190, FREQ
+    // ~159, ENV ~111 instructions) and the two co-resident workgroups of a CU put wave w on the
+    // same SIMD, so role = wave stacks two FILTs on one SIMD.  Each wave reads its SIMD (HW_ID
+    // bits 5:4) and slot (bits 3:0); a workgroup whose wave 0 sits in an odd slot takes the roles in
+    // mirrored SIMD order, pairing ENV with FILT and OSC with FREQ on every SIMD.  Waves that do
+    // not sit on four distinct SIMDs keep role = wave (any assignment is correct; this one only
+    // balances).
+    {
+        const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
+        if (lane == 0) {
+            hw_simd[wave] = (hw >> 4) & 3u;
+            if (wave == 0) hw_simd[4] = hw & 1u;
+        }
+    }
+    __syncthreads();
+    uint32_t role = wave;
+    {
+        const uint32_t m = (1u << hw_simd[0]) | (1u << hw_simd[1]) | (1u << hw_simd[2]) | (1u << hw_simd[3]);
+        const uint32_t sm = hw_simd[wave];
+        if (m == 15u) role = hw_simd[4] ? 3u - sm : sm;
+        role = __builtin_amdgcn_readfirstlane(role);
+    }
+#endif
     const uint32_t i0 = blockIdx.x * 64 + lane;
     const uint32_t i = i0 < n ? i0 : n - 1;      // dead lanes mirror voice n-1, as in v4
     const uint32_t me = i - blockIdx.x * 64;
@@ -400,7 +426,6 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     const uint32_t nsteps = (nf + kVcChunk - 1) / kVcChunk + 2;
     const float *c = a.coef;
     float *s = a.state;
-    const uint32_t role = wave;                  // role = wave
     auto len = [&](uint32_t k) {             // frames of chunk k (the last may be short)
         const uint32_t f0 = k * kVcChunk;
         return nf - f0 < (uint32_t)kVcChunk ? nf - f0 : (uint32_t)kVcChunk;
