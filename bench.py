@@ -431,13 +431,23 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
         res["control"] = {"instances_changed_per_block": int(np.mean([len(c[1]) for c in step_ccs])),
                           "note": "changed coefficients re-derived on the host for those instances only and "
                                   "scattered on the device ahead of the block (control.hip coef_scatter)"}
+    # the CPU baseline runs after every GPU leg (main): no leg is timed right after a many-thread
+    # CPU run (a short-kernel leg measured 1.7x slow once, launch-bound behind it)
+    res["cpu_baseline"] = None
     if with_cpu and world == 1 and args.cpu_seconds > 0:
-        threads = args.cpu_threads or host_facts()["nproc"]
-        res["cpu_baseline"] = cpu_baseline(kind, B, args.sample_rate, args.cpu_seconds, threads,
-                                           PARAM_SET.get(name, ""))
-    else:
-        res["cpu_baseline"] = None
+        res["cpu_job"] = (kind, PARAM_SET.get(name, ""))
     return res
+
+
+def run_cpu_jobs(jobs, reuse, args):
+    """The deferred CPU baselines: jobs = [(result dict, kind, param set)], reuse = [(result dict,
+    the dict whose baseline it reuses, its key)]."""
+    threads = args.cpu_threads or host_facts()["nproc"]
+    for target, kind, pset in jobs:
+        target["cpu_baseline"] = cpu_baseline(kind, args.block, args.sample_rate, args.cpu_seconds, threads, pset)
+    for target, src, key in reuse:
+        if src.get("cpu_baseline"):
+            target["cpu_baseline"] = dict(src["cpu_baseline"], reused_from=key)
 
 
 def main():
@@ -454,7 +464,10 @@ def main():
     torch.cuda.set_device(dev)
 
     n = args.instances or WORKLOADS[args.workload][1]
+    cpu_jobs, cpu_reuse = [], []
     main_res = run_workload(args.workload, n, args, rank, world, dev, with_cpu=True)
+    if rank == 0 and "cpu_job" in main_res:
+        cpu_jobs.append((main_res, *main_res.pop("cpu_job")))
     also = args.also if args.also is not None else (DEFAULT_ALSO if args.workload == "chorus" else "")
     also_res = {}
     for name in [a for a in also.split(",") if a]:
@@ -462,13 +475,16 @@ def main():
         tkey = twin if twin != "chain" else "chain_16384"
         # a control leg's CPU work per block is its twin's (the CPU oracle applies events and
         # parameters per instance at block boundaries): the twin's measured baseline is reused
-        r = run_workload(name, WORKLOADS[name][1], args, rank, world, dev, with_cpu=not (twin and tkey in also_res))
-        if rank == 0 and twin and tkey in also_res and also_res[tkey].get("cpu_baseline"):
-            r["cpu_baseline"] = dict(also_res[tkey]["cpu_baseline"], reused_from=tkey)
+        reuse = bool(twin and tkey in also_res)
+        r = run_workload(name, WORKLOADS[name][1], args, rank, world, dev, with_cpu=not reuse)
         if rank == 0:
             key = name if name != "chain" else "chain_16384"
             also_res[key] = {k: r[k] for k in ("value", "unit", "ms_per_step", "config", "roofline", "control",
                                                 "cpu_baseline", "output_checksum", "output_nonfinite_rank0") if k in r}
+            if "cpu_job" in r:
+                cpu_jobs.append((also_res[key], *r["cpu_job"]))
+            elif reuse:
+                cpu_reuse.append((also_res[key], also_res[tkey], tkey))
             base = EVENT_FREE.get(name)
             bkey = base if base != "chain" else "chain_16384"
             # the control leg's cost against its event-free twin (an `also` leg or the main workload)
@@ -480,6 +496,7 @@ def main():
                     "ms_per_step_ratio": r["ms_per_step"] / b["ms_per_step"]})
 
     if rank == 0:
+        run_cpu_jobs(cpu_jobs, cpu_reuse, args)
         res = {
             "metric": METRIC,
             "value": main_res["value"],
