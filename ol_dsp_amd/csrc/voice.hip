@@ -191,7 +191,10 @@ struct Env {
 // samples per hand-off between the roles: 8 (34 barrier steps per 256-frame block, pipeline fill
 // 2 of them) measured 2 % faster than 16 (18 steps) for the Svf voice and equal for the Moog
 // voice; 32 halves the workgroups per CU (96 KB of LDS each) and is 1.7x slower
-constexpr int kVcChunk = 8;
+#ifndef OLFX_VC_CHUNK
+#define OLFX_VC_CHUNK 8
+#endif
+constexpr int kVcChunk = OLFX_VC_CHUNK;
 
 // Runs f(j) for the m samples of a chunk: unrolled when the chunk is full, so the off-recurrence
 // work of neighbouring samples interleaves (ILP for a wave that is alone on its SIMD).
