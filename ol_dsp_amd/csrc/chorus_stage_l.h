@@ -36,6 +36,10 @@
 #include "chorus_stage.h"
 
 
+#ifndef OLFX_CH_CLAMP
+#define OLFX_CH_CLAMP 1
+#endif
+
 namespace olfx {
 namespace ch {
 
@@ -104,7 +108,8 @@ __device__ __forceinline__ PlanL plan_chunk_l(uint64_t lfo_acc, uint64_t lfo_inc
 template <bool FULL, bool XPREV = false, bool COOP = false, bool OUT_LDS = COOP>
 struct ChStageL {
     static_assert(!(COOP && XPREV), "cooperative input is for a stage whose input comes from HBM");
-    static constexpr int kChunk = 16, kWin = 24, kSlots = kWin + 1;
+    // window slots: kWin, then junk: one slot (patches, the straggler), two with clamped staging
+    static constexpr int kChunk = 16, kWin = 24, kSlots = kWin + (OLFX_CH_CLAMP ? 2 : 1);
     // floats of LDS per wave: one window per tap (chorus 4,800 = 19.2 KB: 2 waves/SIMD; pitch-shift
     // alone 3,200 = 12.8 KB, so its 137-VGPR kernel runs 3 waves/SIMD)
     // COOP output staging [ch][frame][instance] (kOutCh below): in the chorus it overlays the pitch
@@ -119,6 +124,9 @@ struct ChStageL {
     static_assert(!FULL || kOutFloats <= kPsvBase, "output staging must not reach the psv staging");
     static constexpr int kTaps = FULL ? 3 : 2;
     static_assert(2 * 32 * kStride <= kRegion, "staging must fit in the window region");
+    // window patches as stores to a clamped slot (out-of-window frames land in the junk slot) rather
+    // than exec-masked stores (A/B knob)
+    static constexpr bool kClampPatch = OLFX_CH_CLAMP != 0;
 
     uint32_t lane, j, ch, inst0, n, i;
     bool valid;
@@ -263,17 +271,28 @@ struct ChStageL {
             const int st = (int)(((s15 >> (2 * (t * 4 + r))) & 3u) << 2);
             const int slo = 2 * (int)pm() - st;          // line L' piece -> slots slo, slo + 1
             const int shi = slo + 16;                     // line L'+1 piece
-            // only pieces inside the window are written (exec-masked)
             const float4 a = ln[t][LO][r], b = ln[t][HI][r];
-            if (slo >= 0) {
-                float *plo = base + slo * kRow + 2 * jj;
+            if constexpr (kClampPatch) {
+                // pieces outside the window go to the junk slots kWin, kWin + 1 (slo is even, so a
+                // piece is wholly inside or outside; slo < 0 wraps to a large unsigned value)
+                float *plo = base + min((uint32_t)slo, (uint32_t)kWin) * kRow + 2 * jj;
+                float *phi = base + min((uint32_t)shi, (uint32_t)kWin) * kRow + 2 * jj;
                 *(float2 *)plo = make_float2(a.x, a.y);
                 *(float2 *)(plo + kRow) = make_float2(a.z, a.w);
-            }
-            if (shi < kWin) {
-                float *phi = base + shi * kRow + 2 * jj;
                 *(float2 *)phi = make_float2(b.x, b.y);
                 *(float2 *)(phi + kRow) = make_float2(b.z, b.w);
+            } else {
+                // only pieces inside the window are written (exec-masked)
+                if (slo >= 0) {
+                    float *plo = base + slo * kRow + 2 * jj;
+                    *(float2 *)plo = make_float2(a.x, a.y);
+                    *(float2 *)(plo + kRow) = make_float2(a.z, a.w);
+                }
+                if (shi < kWin) {
+                    float *phi = base + shi * kRow + 2 * jj;
+                    *(float2 *)phi = make_float2(b.x, b.y);
+                    *(float2 *)(phi + kRow) = make_float2(b.z, b.w);
+                }
             }
         }
         if (t == 2) base[strag_slot * kRow + lane] = strag;
@@ -404,46 +423,83 @@ struct ChStageL {
         if (FULL) {
             // psv_{c-1}'s frame k goes to slot k - 16 - sC when that lies in the window: all 16 read
             // first (a read after a store that may alias it would wait for the store, slot by slot),
-            // then stored exec-masked at constant offsets from the window's slot for k = 0
-            const bool need = started && cur.sC > -kWin - kChunk;
-            float pv[kChunk];
-            if (need) {
-                const float *prev = region + kPsvBase + j * kStride + ch;
+            // then stored
+            if constexpr (kClampPatch) {
+                // branch-free: a slot outside the window becomes the junk slot kWin (unsigned min), so
+                // no exec-mask region per store (each cost a compare, a saveexec, an exec restore and a
+                // skip branch: instructions that a wave alone on its SIMD issues one by one)
+                if (started) {
+                    const float *prev = region + kPsvBase + j * kStride + ch;
+                    float pv[kChunk];
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) pv[k] = prev[2 * k];
-            }
-            stage_tap<PAR, 2>();
-            if (need) {
-                const int lo = kChunk + cur.sC;          // frames k in [lo, lo + kWin) land in the window
-                float *pC = wC - lo * kRow;
+                    for (int k = 0; k < kChunk; ++k) pv[k] = prev[2 * k];
+                    stage_tap<PAR, 2>();
+                    const uint32_t nlo = (uint32_t)(-(kChunk + cur.sC));   // slot of frame k = k + nlo
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k)
-                    if (k >= lo && k < lo + kWin) pC[k * kRow] = pv[k];
+                    for (int k = 0; k < kChunk; ++k) wC[min((uint32_t)k + nlo, (uint32_t)kWin) * kRow] = pv[k];
+                } else {
+                    stage_tap<PAR, 2>();
+                }
+            } else {
+                const bool need = started && cur.sC > -kWin - kChunk;
+                float pv[kChunk];
+                if (need) {
+                    const float *prev = region + kPsvBase + j * kStride + ch;
+#pragma unroll
+                    for (int k = 0; k < kChunk; ++k) pv[k] = prev[2 * k];
+                }
+                stage_tap<PAR, 2>();
+                if (need) {
+                    const int lo = kChunk + cur.sC;          // frames k in [lo, lo + kWin) land in the window
+                    float *pC = wC - lo * kRow;
+#pragma unroll
+                    for (int k = 0; k < kChunk; ++k)
+                        if (k >= lo && k < lo + kWin) pC[k * kRow] = pv[k];
+                }
             }
         }
         stage_tap<PAR, 0>();
         stage_tap<PAR, 1>();
         // XPREV: x_{c-1} is not in a carried line (stored during chunk c-1, after its loads)
         if (XPREV && started) {
-            // frame k of x_{c-1} -> slot k - 16 - s when in the window (exec-masked, constant offsets)
+            // frame k of x_{c-1} -> slot k - 16 - s when in the window
             const int loA = kChunk + cur.sA, loB = kChunk + cur.sB;
-            float *pA = wP0 - loA * kRow, *pB = wP1 - loB * kRow;
+            if constexpr (kClampPatch) {              // outside the window: the junk slot kWin
+                const uint32_t nA = (uint32_t)(-loA), nB = (uint32_t)(-loB);
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) {
-                if (k >= loA && k < loA + kWin) pA[k * kRow] = xp[k];
-                if (k >= loB && k < loB + kWin) pB[k * kRow] = xp[k];
+                for (int k = 0; k < kChunk; ++k) {
+                    wP0[min((uint32_t)k + nA, (uint32_t)kWin) * kRow] = xp[k];
+                    wP1[min((uint32_t)k + nB, (uint32_t)kWin) * kRow] = xp[k];
+                }
+            } else {                                  // exec-masked, constant offsets
+                float *pA = wP0 - loA * kRow, *pB = wP1 - loB * kRow;
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) {
+                    if (k >= loA && k < loA + kWin) pA[k * kRow] = xp[k];
+                    if (k >= loB && k < loB + kWin) pB[k * kRow] = xp[k];
+                }
             }
         }
         // x_c is not in a carried line either.  Its slot k - s is >= 2 (a pitch window starts at
-        // s <= -4: delays are >= 1), so only the top can leave the window: one compare per frame,
-        // the store exec-masked at a constant offset from the window's frame-0 slot
+        // s <= -4: delays are >= 1), so only the top can leave the window
         {
             const int limA = kWin + cur.sA, limB = kWin + cur.sB;
             float *pA = wP0 - cur.sA * kRow, *pB = wP1 - cur.sB * kRow;
+            if constexpr (kClampPatch) {
+                // frame k -> slot min(k, lim) - s: past the window that is the junk slot kWin; past
+                // a short chunk's C frames, slot C - s, a position no frame of this chunk reads
+                const int mA = min(limA, C), mB = min(limB, C);
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) {
-                if (k < C && k < limA) pA[k * kRow] = x[k];
-                if (k < C && k < limB) pB[k * kRow] = x[k];
+                for (int k = 0; k < kChunk; ++k) {
+                    pA[min(k, mA) * kRow] = x[k];
+                    pB[min(k, mB) * kRow] = x[k];
+                }
+            } else {                                  // one compare per frame, exec-masked stores
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) {
+                    if (k < C && k < limA) pA[k * kRow] = x[k];
+                    if (k < C && k < limB) pB[k * kRow] = x[k];
+                }
             }
         }
         started = true;

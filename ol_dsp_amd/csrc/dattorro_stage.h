@@ -30,16 +30,23 @@ __device__ __forceinline__ float el(const float4 &v, int e) {
     return e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
 }
 
-// v[k] = element s + k of the 8-float window (a, b), s in 0..3 (runtime).  Written as explicit
-// per-element selects: an array-based form gets rewritten into a runtime-indexed stack array.
-__device__ __forceinline__ float sel4(uint32_t s, float p0, float p1, float p2, float p3) {
-    return s == 0 ? p0 : (s == 1 ? p1 : (s == 2 ? p2 : p3));
+// v[k] = element s + k of the 8-float window (a0..a3, b0..b2), s in 0..3 (runtime, uniform or per
+// lane): a shift by 2 on bit 1, then by 1 on bit 0 -- 9 v_cndmask.  The two bits pass through an
+// empty asm: a chain of `s == 0 ? .. : s == 1 ? ..` selects was rebuilt by the compiler into a
+// switch on s, i.e. an exec-mask branch tree per element (about 25 instructions each, every merge
+// a loss of waitcnt precision for the prefetch in flight)
+__device__ __forceinline__ void shift4(uint32_t s, float a0, float a1, float a2, float a3, float b0, float b1,
+                                       float b2, float (&v)[4]) {
+    uint32_t hi = s & 2u, lo = s & 1u;
+    asm volatile("" : "+v"(hi), "+v"(lo));
+    const float t0 = hi ? a2 : a0, t1 = hi ? a3 : a1, t2 = hi ? b0 : a2, t3 = hi ? b1 : a3, t4 = hi ? b2 : b0;
+    v[0] = lo ? t1 : t0;
+    v[1] = lo ? t2 : t1;
+    v[2] = lo ? t3 : t2;
+    v[3] = lo ? t4 : t3;
 }
 __device__ __forceinline__ void shift4(uint32_t s, const float4 &a, const float4 &b, float (&v)[4]) {
-    v[0] = sel4(s, a.x, a.y, a.z, a.w);
-    v[1] = sel4(s, a.y, a.z, a.w, b.x);
-    v[2] = sel4(s, a.z, a.w, b.x, b.y);
-    v[3] = sel4(s, a.w, b.x, b.y, b.z);
+    shift4(s, a.x, a.y, a.z, a.w, b.x, b.y, b.z, v);
 }
 
 template <int L>
@@ -105,14 +112,9 @@ struct ModTap {
         r0 = g1.x; r1 = g1.y; r2 = g1.z; r3 = g1.w;
     }
     __device__ __forceinline__ void resolve() {       // shift q & 3 (wave-uniform) by selects
-        // moved to a VGPR so the selects stay v_cndmask (an SGPR shift compiles to scalar
-        // branches, and the extra blocks cost precise waitcnt tracking of the prefetch)
-        uint32_t s;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(s) : "s"(q & 3u));
-        v[0] = sel4(s, c0, c1, c2, c3);
-        v[1] = sel4(s, c1, c2, c3, n0);
-        v[2] = sel4(s, c2, c3, n0, n1);
-        v[3] = sel4(s, c3, n0, n1, n2);
+        // (shift4 keeps them v_cndmask: scalar or exec-mask branches cost precise waitcnt
+        // tracking of the prefetch at every merge)
+        shift4(q & 3u, c0, c1, c2, c3, n0, n1, n2, v);
     }
     __device__ __forceinline__ void advance() {
         uint32_t k;                                   // VGPR copy of the uniform flag, as in resolve()
@@ -148,17 +150,23 @@ struct PreTap {
         pre = *grp<DT_PRE>(a, ((t0 - d) >> 2) + 2u, i);
     }
     // xpd[k] = mono input at t0 + k - d
+    // d <= 8: xpd[k] = r[8 - d + k] of the history r = x2 | x1 | xin, i.e. groups g, g + 1 of r
+    // (g = (8 - d) / 4) shifted by (8 - d) & 3 -- group selects and a shift4, no compare per d
     __device__ __forceinline__ void resolve(const float (&xin)[4], uint32_t d, float (&xpd)[4]) const {
-        shift4(s, cur, nxt, xpd);
-        const float r[12] = {x2[0], x2[1], x2[2], x2[3], x1[0], x1[1], x1[2], x1[3],
-                             xin[0], xin[1], xin[2], xin[3]};
+        float ring[4], reg[4];
+        shift4(s, cur, nxt, ring);
+        const uint32_t idx = 8u - min(d, 8u);
+        uint32_t g1 = idx & 4u, g2 = idx & 8u, near = d <= 8u ? 1u : 0u;
+        asm volatile("" : "+v"(g1), "+v"(g2), "+v"(near));
+        float a[4], b[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            float v = xpd[k];
-#pragma unroll
-            for (int dd = 0; dd <= 8; ++dd) v = d == (uint32_t)dd ? r[8 + k - dd] : v;
-            xpd[k] = v;
+            a[k] = g2 ? xin[k] : (g1 ? x1[k] : x2[k]);
+            b[k] = g1 ? xin[k] : x1[k];               // (g = 2 is d = 0: shift 0, b unused)
         }
+        shift4(idx & 3u, a[0], a[1], a[2], a[3], b[0], b[1], b[2], reg);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xpd[k] = near ? reg[k] : ring[k];
     }
     __device__ __forceinline__ void advance(const float (&xin)[4]) {
         cur = nxt; nxt = pre;
