@@ -107,10 +107,11 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) 
                     }
                 };
                 // outputs to registers first, then to the queue: a store through a generic
-                // pointer inside the stage's sink may alias the stage object (scratch)
+                // pointer inside the stage's sink may alias the stage object (scratch).  Frames
+                // past a short chunk's C are never read downstream: no zero fill (16 moves)
                 float y[kChunk];
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) y[k] = 0.f;
+                for (int k = 0; k < kChunk; ++k) y[k] = __builtin_nondeterministic_value(0.f);
                 s1.template chunk<decltype(par)::value>(x, xn, C, Cn, [&](int k, float v) { y[k] = v; }, prefetch, xq);
                 const uint32_t gc = gc0 + c;
                 wait_for([&] { return flag_get(flags + F_PIN) + kDepth > gc; });   // buffer gc % kDepth free
@@ -147,16 +148,22 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) 
                 wait_for([&] { return flag_get(flags + F_C0) > gc && flag_get(flags + F_C1) > gc; });
                 const float *qi = q1 + (gc % kDepth) * kQBuf;
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) { xa[k] = qi[qa + k * 64]; xb[k] = qi[qb + k * 64]; }
-                flag_put(flags + F_PIN, gc + 1);              // (the release waits for these reads)
+                for (int k = 0; k < kChunk; ++k) xa[k] = qi[qa + k * 64];
+                // (frames past a short chunk's C are never read downstream: no zero fill)
                 float y[kChunk];
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) y[k] = 0.f;
+                for (int k = 0; k < kChunk; ++k) y[k] = __builtin_nondeterministic_value(0.f);
                 sa.template chunk<P>(xa, xa, C, Cn, [&](int k, float v) { y[k] = v; }, []() {}, kNoRows);
+                // group b's input is read only now (16 registers fewer live across group a's
+                // chunk: the role is past 256 VGPRs and pays for every value parked in an AGPR);
+                // the queue buffer is released after it
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) xb[k] = qi[qb + k * 64];
+                flag_put(flags + F_PIN, gc + 1);              // (the release waits for these reads)
                 wait_for([&] { return flag_get(flags + F_DIN) + kDepth > gc; });
                 float *qo = q2 + (gc % kDepth) * kQBuf;
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) { qo[qa + k * 64] = y[k]; y[k] = 0.f; }
+                for (int k = 0; k < kChunk; ++k) { qo[qa + k * 64] = y[k]; y[k] = __builtin_nondeterministic_value(0.f); }
                 sb.template chunk<P>(xb, xb, C, Cn, [&](int k, float v) { y[k] = v; }, []() {}, kNoRows);
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) qo[qb + k * 64] = y[k];

@@ -54,6 +54,15 @@ __device__ __forceinline__ float4 *grp(const DattorroArgs &a, uint32_t g, uint32
     constexpr uint32_t gm = kDtSize[L] / 4u - 1u;
     return (float4 *)a.ring[L] + ((size_t)(g & gm) * a.n + i);
 }
+// The same for a wave-uniform g: the group's row start is uniform (scalar arithmetic) and the
+// lane's 16 B an unsigned 32-bit offset from it, so the access is a global load/store with an SGPR
+// base and a VGPR offset -- no 64-bit vector address add per access
+template <int L>
+__device__ __forceinline__ float4 *grpu(const DattorroArgs &a, uint32_t g, uint32_t i) {
+    constexpr uint32_t gm = kDtSize[L] / 4u - 1u;
+    char *row = (char *)a.ring[L] + (size_t)(g & gm) * a.n * 16u;
+    return (float4 *)(row + (uint32_t)(i * 16u));
+}
 
 // A fixed tap: delay D, read at t + OFF (OFF = 1 for the output taps, verb.cpp:298,302-325).
 template <int L, uint32_t D, uint32_t OFF>
@@ -62,11 +71,11 @@ struct Tap {
     float4 cur, nxt, pre;
     __device__ __forceinline__ static uint32_t g0(uint32_t t0) { return (t0 + OFF - D) >> 2; }
     __device__ __forceinline__ void prime(const DattorroArgs &a, uint32_t t0, uint32_t i) {
-        cur = *grp<L>(a, g0(t0), i);
-        if (S) nxt = *grp<L>(a, g0(t0) + 1u, i);
+        cur = *grpu<L>(a, g0(t0), i);
+        if (S) nxt = *grpu<L>(a, g0(t0) + 1u, i);
     }
     __device__ __forceinline__ void prefetch(const DattorroArgs &a, uint32_t t0, uint32_t i) {
-        pre = *grp<L>(a, g0(t0) + (S ? 2u : 1u), i);
+        pre = *grpu<L>(a, g0(t0) + (S ? 2u : 1u), i);
     }
     __device__ __forceinline__ float get(int k) const {
         return (int)S + k < 4 ? el(cur, (int)S + k) : el(nxt, (int)S + k - 4);
@@ -92,7 +101,7 @@ struct ModTap {
     bool carry;                                       // next window's first group = n0..n3
     __device__ __forceinline__ void prime(const DattorroArgs &a, uint32_t t0, uint32_t i) {
         q = t0 - (D + dt_ap1_extra(t0 & 0xFFFFu));
-        const float4 g0 = *grp<L>(a, q >> 2, i), g1 = *grp<L>(a, (q >> 2) + 1u, i);
+        const float4 g0 = *grpu<L>(a, q >> 2, i), g1 = *grpu<L>(a, (q >> 2) + 1u, i);
         c0 = g0.x; c1 = g0.y; c2 = g0.z; c3 = g0.w;
         n0 = g1.x; n1 = g1.y; n2 = g1.z; n3 = g1.w;
     }
@@ -101,7 +110,7 @@ struct ModTap {
         qn = t0n - (D + dt_ap1_extra(t0n & 0xFFFFu));
         const uint32_t gq = qn >> 2;
         carry = gq == (q >> 2) + 1u;
-        const float4 g1 = *grp<L>(a, gq + 1u, i);
+        const float4 g1 = *grpu<L>(a, gq + 1u, i);
         constexpr uint32_t gm = kDtSize[L] / 4u - 1u;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             a.ring[L], (short)0, (int)(uint32_t)((uint64_t)kDtSize[L] * a.n * 4u), 0x00020000);
@@ -142,7 +151,7 @@ struct PreTap {
         s = q & 3u;
         cur = *grp<DT_PRE>(a, q >> 2, i);
         nxt = *grp<DT_PRE>(a, (q >> 2) + 1u, i);
-        const float4 g1 = *grp<DT_PRE>(a, (t0 >> 2) - 1u, i), g2 = *grp<DT_PRE>(a, (t0 >> 2) - 2u, i);
+        const float4 g1 = *grpu<DT_PRE>(a, (t0 >> 2) - 1u, i), g2 = *grpu<DT_PRE>(a, (t0 >> 2) - 2u, i);
         x1[0] = g1.x; x1[1] = g1.y; x1[2] = g1.z; x1[3] = g1.w;
         x2[0] = g2.x; x2[1] = g2.y; x2[2] = g2.z; x2[3] = g2.w;
     }
@@ -250,19 +259,19 @@ __device__ __forceinline__ void step_body(
 
     // ---- writes: one 16-B group per line ----
     const uint32_t gw = t0 >> 2;
-    *grp<DT_PRE>(a, gw, i) = make_float4(xin[0], xin[1], xin[2], xin[3]);
-    *grp<DT_IN0>(a, gw, i) = make_float4(w_in0[0], w_in0[1], w_in0[2], w_in0[3]);
-    *grp<DT_IN1>(a, gw, i) = make_float4(w_in1[0], w_in1[1], w_in1[2], w_in1[3]);
-    *grp<DT_IN2>(a, gw, i) = make_float4(w_in2[0], w_in2[1], w_in2[2], w_in2[3]);
-    *grp<DT_IN3>(a, gw, i) = make_float4(w_in3[0], w_in3[1], w_in3[2], w_in3[3]);
-    *grp<DT_AP1A>(a, gw, i) = make_float4(w_ap1a[0], w_ap1a[1], w_ap1a[2], w_ap1a[3]);
-    *grp<DT_DL1A>(a, gw, i) = make_float4(w_dl1a[0], w_dl1a[1], w_dl1a[2], w_dl1a[3]);
-    *grp<DT_AP2A>(a, gw, i) = make_float4(w_ap2a[0], w_ap2a[1], w_ap2a[2], w_ap2a[3]);
-    *grp<DT_DL2A>(a, gw, i) = make_float4(w_dl2a[0], w_dl2a[1], w_dl2a[2], w_dl2a[3]);
-    *grp<DT_AP1B>(a, gw, i) = make_float4(w_ap1b[0], w_ap1b[1], w_ap1b[2], w_ap1b[3]);
-    *grp<DT_DL1B>(a, gw, i) = make_float4(w_dl1b[0], w_dl1b[1], w_dl1b[2], w_dl1b[3]);
-    *grp<DT_AP2B>(a, gw, i) = make_float4(w_ap2b[0], w_ap2b[1], w_ap2b[2], w_ap2b[3]);
-    *grp<DT_DL2B>(a, gw, i) = make_float4(w_dl2b[0], w_dl2b[1], w_dl2b[2], w_dl2b[3]);
+    *grpu<DT_PRE>(a, gw, i) = make_float4(xin[0], xin[1], xin[2], xin[3]);
+    *grpu<DT_IN0>(a, gw, i) = make_float4(w_in0[0], w_in0[1], w_in0[2], w_in0[3]);
+    *grpu<DT_IN1>(a, gw, i) = make_float4(w_in1[0], w_in1[1], w_in1[2], w_in1[3]);
+    *grpu<DT_IN2>(a, gw, i) = make_float4(w_in2[0], w_in2[1], w_in2[2], w_in2[3]);
+    *grpu<DT_IN3>(a, gw, i) = make_float4(w_in3[0], w_in3[1], w_in3[2], w_in3[3]);
+    *grpu<DT_AP1A>(a, gw, i) = make_float4(w_ap1a[0], w_ap1a[1], w_ap1a[2], w_ap1a[3]);
+    *grpu<DT_DL1A>(a, gw, i) = make_float4(w_dl1a[0], w_dl1a[1], w_dl1a[2], w_dl1a[3]);
+    *grpu<DT_AP2A>(a, gw, i) = make_float4(w_ap2a[0], w_ap2a[1], w_ap2a[2], w_ap2a[3]);
+    *grpu<DT_DL2A>(a, gw, i) = make_float4(w_dl2a[0], w_dl2a[1], w_dl2a[2], w_dl2a[3]);
+    *grpu<DT_AP1B>(a, gw, i) = make_float4(w_ap1b[0], w_ap1b[1], w_ap1b[2], w_ap1b[3]);
+    *grpu<DT_DL1B>(a, gw, i) = make_float4(w_dl1b[0], w_dl1b[1], w_dl1b[2], w_dl1b[3]);
+    *grpu<DT_AP2B>(a, gw, i) = make_float4(w_ap2b[0], w_ap2b[1], w_ap2b[2], w_ap2b[3]);
+    *grpu<DT_DL2B>(a, gw, i) = make_float4(w_dl2b[0], w_dl2b[1], w_dl2b[2], w_dl2b[3]);
 
 #define DT_ADVANCE_OP(T) T.advance();
     DT_ALL_TAPS(DT_ADVANCE_OP)
