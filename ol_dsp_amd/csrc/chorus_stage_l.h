@@ -110,8 +110,8 @@ struct ChStageL {
     static_assert(!(COOP && XPREV), "cooperative input is for a stage whose input comes from HBM");
     // window slots: kWin, then junk: one slot (patches, the straggler), two with clamped staging
     static constexpr int kChunk = 16, kWin = 24, kSlots = kWin + (OLFX_CH_CLAMP ? 2 : 1);
-    // floats of LDS per wave: one window per tap (chorus 4,800 = 19.2 KB: 2 waves/SIMD; pitch-shift
-    // alone 3,200 = 12.8 KB, so its 137-VGPR kernel runs 3 waves/SIMD)
+    // floats of LDS per wave: one window per tap (chorus 3 x 26 x 64 = 4,992 = 19.5 KB: 2 waves/SIMD,
+    // 156 KB per CU; pitch-shift alone 3,328 + its output staging)
     // COOP output staging [ch][frame][instance] (kOutCh below): in the chorus it overlays the pitch
     // windows' staging area (LDS is at its 2-waves/SIMD limit); the pitch-shifter has room for its own
     static constexpr uint32_t kOutCh = 544, kOutFloats = kOutCh + 16 * 32;

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -584,6 +585,17 @@ void mark_dirty(olfx_engine *e, uint32_t first, uint32_t count) {
 // envelopes (:245-251); NoteOff / GateOff = gate off (:236-239, :253-256); GateOn = gate on
 // (:231-234); SetFrequency = freq_ (:264-267).  The last gate call decides the gate, any NoteOn
 // retriggers (gate calls do not touch the envelope modes), the last NoteOn / SetFrequency the pitch.
+// daisysp::mtof of a MIDI note, from a table of the same expression (notes are 0..127; one powf
+// per NoteOn had been the largest host cost of a block with note events)
+float mtof_note(uint8_t note) {
+    static const std::array<float, 128> t = [] {
+        std::array<float, 128> r{};
+        for (int k = 0; k < 128; ++k) r[(size_t)k] = powf(2.f, ((float)k - 69.0f) / 12.0f) * 440.0f;
+        return r;
+    }();
+    return t[note & 127u];
+}
+
 void fold_events(olfx_engine *e) {
     e->folded.clear();
     for (const olfx_voice_event &ev : e->events) {
@@ -596,7 +608,7 @@ void fold_events(olfx_engine *e) {
         switch (ev.type) {
         case OLFX_EV_NOTE_ON: {
             r.op |= VEV_GATE_SET | VEV_GATE_ON | VEV_RETRIGGER | VEV_FREQ;
-            const float hz = powf(2.f, (ev.note - 69.0f) / 12.0f) * 440.0f;   // daisysp::mtof
+            const float hz = mtof_note(ev.note);                              // daisysp::mtof
             std::memcpy(&r.freq, &hz, 4);
             break;
         }
