@@ -4,7 +4,7 @@
 // A workgroup owns 64 instances and runs the three stages as a pipeline of four single-role waves,
 // one per SIMD:
 //   waves 0, 1 ("C"):  the chorus stage, 32 instances x 2 channels each, input from HBM;
-//   wave 2     ("P"):  the pitch-shift stage for all 64 instances, as two 32-instance groups;
+//   wave 2     ("P"):  the pitch-shift stage for all 64 instances, lane = instance (both channels);
 //   wave 3     ("DT"): the 64 reverbs, lane = instance, output to HBM.
 // Stage outputs go through LDS queues (double-buffered, [ch][16 frames][64 instances]).  Barrier
 // b ends step b: the C waves produce chunk b, P runs chunk b-1, DT runs chunk b-2; nchunks + 2
@@ -12,16 +12,18 @@
 // composition of the three stages (bit-exact with the oracle's chorus -> pitch-shift -> dattorro,
 // tests/test_gpu_parity.py), and the intermediates never touch HBM.
 //
-// The chorus and pitch stages are the line-carry stage of chorus_block_v11 (chorus_stage_l.h):
-// per tap and instance the two aligned 128-B lines of the window live in registers and a chunk
-// loads only the new line, so every ring byte is read about once (v1 re-fetched a fresh window
-// per tap per chunk: 296 B/frame of HBM traffic against 228.6 algorithmic; v3: 245).  The pitch
-// stage's next input (the chorus output of the next chunk) does not exist while it runs a chunk,
-// so it uses the XPREV form (stores its own input, patches the previous one from registers).
+// The chorus and pitch stages carry their windows' lines in registers (line carry): the chorus
+// stage is chorus_block_v11's (chorus_stage_l.h), the pitch stage its stereo-lane form
+// (pitch_stage_s.h): per tap and instance the two aligned 128-B lines of the window live in
+// registers and a chunk loads only the new line, so every ring byte is read about once (v1
+// re-fetched a fresh window per tap per chunk: 296 B/frame of HBM traffic against 228.6
+// algorithmic; v3: 245).  The pitch stage's next input (the chorus output of the next chunk) does
+// not exist while it runs a chunk, so it stores its own input and patches it in at the next chunk.
 // Why four roles (history in DESIGN.md section 4): every wave of the kernel gets the reverb's
 // register allocation (256 VGPR + AGPRs), so a CU holds four waves; v2 ran chorus and pitch
 // in the same two waves (12.6 us per step against the reverb's 8.1) and left one SIMD idle.
 #include "chorus_stage_l.h"
+#include "pitch_stage_s.h"
 #include "dattorro_stage.h"
 #include "lds_flags.h"
 
@@ -45,7 +47,6 @@ template <bool COOP>
 __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int kChunk = 16;
-    const float4 kNoRows[4] = {};                          // the stages take their input per lane
     const uint32_t tid = threadIdx.x;
     const uint32_t wib = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
     const uint32_t lane = tid & 63u;
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) 
 
     if (wib < 2) {
         // ---------------- C: the chorus, per (instance, channel) lane ----------------
-        using StageC = ch::ChStageL<true, false, COOP, false>;
+        using StageC = ch::ChStageL<true, COOP, false>;
         StageC s1;
         const ch::Rsrc rIn = ch::rsrc(a.in, (a.plane + (uint64_t)nf * n) * 4);
         const uint32_t frame_b = n * 4u;
@@ -129,52 +130,41 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) 
             s1.finish(a.c1);
         }
     } else if (wib == 2) {
-        // ---------------- P: the pitch-shifter, two 32-instance groups per lane ----------------
-        ch::ChStageL<false, true> sa, sb;
+        // ---------------- P: the pitch-shifter, one lane per instance (pitch_stage_s.h) ----------------
+        ch::PStageS sp;
+        static_assert(ch::PStageS::kRegion <= 2 * kChainRegion, "P's LDS share");
         for (uint32_t g = blockIdx.x, gi = 0; g < ngroups; g += gridDim.x, ++gi) {
-            const uint32_t base = g * 64u, gc0 = gi * nchunks;
-            sa.init(a.c2, lds + 2 * kChainRegion, lane, base);
-            sb.init(a.c2, lds + 3 * kChainRegion, lane, base + 32u);
-            const uint32_t qa = sa.ch * kQCh + sa.j, qb = qa + 32u;
-            float xa[kChunk], xb[kChunk];
+            const uint32_t gc0 = gi * nchunks;
+            sp.init(a.c2, lds + 2 * kChainRegion, lane, g * 64u);
             int C = (int)min((uint32_t)kChunk, nf);
-            sa.begin(xa, C);                                  // XPREV: lines only, x unused
-            sb.begin(xb, C);
+            sp.begin(C);
             auto step = [&](auto par, uint32_t f0, uint32_t c) {
                 constexpr int P = decltype(par)::value;
                 C = (int)min((uint32_t)kChunk, nf - f0);
                 const int Cn = f0 + kChunk < nf ? (int)min((uint32_t)kChunk, nf - f0 - kChunk) : 0;
                 const uint32_t gc = gc0 + c;
                 wait_for([&] { return flag_get(flags + F_C0) > gc && flag_get(flags + F_C1) > gc; });
-                const float *qi = q1 + (gc % kDepth) * kQBuf;
+                const float *qi = q1 + (gc % kDepth) * kQBuf + lane;
+                float2 x[kChunk];
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) xa[k] = qi[qa + k * 64];
-                // (frames past a short chunk's C are never read downstream: no zero fill)
-                float y[kChunk];
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) y[k] = __builtin_nondeterministic_value(0.f);
-                sa.template chunk<P>(xa, xa, C, Cn, [&](int k, float v) { y[k] = v; }, []() {}, kNoRows);
-                // group b's input is read only now (16 registers fewer live across group a's
-                // chunk: the role is past 256 VGPRs and pays for every value parked in an AGPR);
-                // the queue buffer is released after it
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) xb[k] = qi[qb + k * 64];
+                for (int k = 0; k < kChunk; ++k) x[k] = make_float2(qi[k * 64], qi[kQCh + k * 64]);
                 flag_put(flags + F_PIN, gc + 1);              // (the release waits for these reads)
+                // (frames past a short chunk's C are never read downstream: no zero fill)
+                float2 y[kChunk];
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) y[k] = make_float2(__builtin_nondeterministic_value(0.f), __builtin_nondeterministic_value(0.f));
+                sp.template chunk<P>(x, C, Cn, [&](int k, float2 v) { y[k] = v; });
                 wait_for([&] { return flag_get(flags + F_DIN) + kDepth > gc; });
-                float *qo = q2 + (gc % kDepth) * kQBuf;
+                float *qo = q2 + (gc % kDepth) * kQBuf + lane;
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) { qo[qa + k * 64] = y[k]; y[k] = __builtin_nondeterministic_value(0.f); }
-                sb.template chunk<P>(xb, xb, C, Cn, [&](int k, float v) { y[k] = v; }, []() {}, kNoRows);
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) qo[qb + k * 64] = y[k];
+                for (int k = 0; k < kChunk; ++k) { qo[k * 64] = y[k].x; qo[kQCh + k * 64] = y[k].y; }
                 flag_put(flags + F_POUT, gc + 1);
             };
             for (uint32_t f0 = 0, c = 0; f0 < nf; f0 += 2 * kChunk, c += 2) {
                 step(std::integral_constant<int, 0>{}, f0, c);
                 if (f0 + kChunk < nf) step(std::integral_constant<int, 1>{}, f0 + kChunk, c + 1);
             }
-            sa.finish(a.c2);
-            sb.finish(a.c2);
+            sp.finish(a.c2);
         }
     } else {
         // ---------------- DT: the reverb, lane = instance, input from the queue ----------------

@@ -12,7 +12,7 @@ namespace olfx {
 // the last instance); otherwise one float per lane, frame and direction.
 template <bool FULL, bool COOP>
 __global__ __launch_bounds__(ch::kThreads, 2) void chorus_block_v11(ChorusArgs a) {
-    using Stage = ch::ChStageL<FULL, false, COOP>;
+    using Stage = ch::ChStageL<FULL, COOP>;
     constexpr int kChunk = Stage::kChunk;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const uint32_t tid = threadIdx.x;
@@ -102,7 +102,7 @@ hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s) {
     const uint32_t waves = (a.n + 31) / 32;              // 32 instances x 2 channels per wave
     const uint32_t blocks = (waves + ch::kThreads / 64 - 1) / (ch::kThreads / 64);
     auto lds = [](auto full, auto coop) {
-        return (size_t)(ch::kThreads / 64) * ch::ChStageL<decltype(full)::value, false, decltype(coop)::value>::kRegion *
+        return (size_t)(ch::kThreads / 64) * ch::ChStageL<decltype(full)::value, decltype(coop)::value>::kRegion *
                sizeof(float);
     };
     using T = std::true_type;

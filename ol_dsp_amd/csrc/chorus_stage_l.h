@@ -24,10 +24,9 @@
 // that did not advance by exactly one line (or the first chunk of a launch) is FRESH: it also
 // reloads L' (the "lo" load, exec-masked, so a carried line is never clobbered).
 //
-// XPREV variant (the fused chain's second stage, whose next input is not known while a chunk runs):
-// each chunk stores its OWN input x_c before the next chunk's line loads, and keeps it in registers
-// (xp) for one more chunk.  A line loaded during chunk c then holds everything up to x_c; at chunk
-// c+1 a carried line lacks x_c (patched from xp) and x_{c+1} (patched from x, as always).
+// The fused chain's pitch-shift stage, whose next input is not known while a chunk runs, is the
+// stereo-lane variant of this scheme in pitch_stage_s.h (it stores its OWN input before the next
+// chunk's line loads and patches it in at the next chunk).
 //
 // The chorus tap can span 18 positions (its delay may fall by one inside a chunk); when such a
 // window starts at the last position of a line, its highest position lies in line L'+2: that one
@@ -97,7 +96,7 @@ __device__ __forceinline__ PlanL plan_chunk_l(uint64_t lfo_acc, uint64_t lfo_inc
     return p;
 }
 
-// COOP (not with XPREV): the driver loads the block's input cooperatively -- per chunk 4 x 16 B per
+// COOP: the driver loads the block's input cooperatively -- per chunk 4 x 16 B per
 // lane, rows (frame, channel) of the wave's 32 instances (coop_row below) -- and the stage
 // transposes them through its LDS staging into the lanes' own frames; outputs go the same way
 // (out_stage / coop_out below).  4 + 4 wide vector-memory instructions per chunk instead of
@@ -105,9 +104,8 @@ __device__ __forceinline__ PlanL plan_chunk_l(uint64_t lfo_acc, uint64_t lfo_inc
 // OUT_LDS (default COOP): the sink writes the stage's LDS (out_stage), so a generic chunk emits its
 // outputs only after stores_and_next has finished with the pitch windows (the fused chain's C role
 // takes cooperative input but sinks into registers: OUT_LDS = false)
-template <bool FULL, bool XPREV = false, bool COOP = false, bool OUT_LDS = COOP>
+template <bool FULL, bool COOP = false, bool OUT_LDS = COOP>
 struct ChStageL {
-    static_assert(!(COOP && XPREV), "cooperative input is for a stage whose input comes from HBM");
     // window slots: kWin, then junk: one slot (patches, the straggler), two with clamped staging
     static constexpr int kChunk = 16, kWin = 24, kSlots = kWin + (OLFX_CH_CLAMP ? 2 : 1);
     // floats of LDS per wave: one window per tap (chorus 3 x 26 x 64 = 4,992 = 19.5 KB: 2 waves/SIMD,
@@ -146,7 +144,6 @@ struct ChStageL {
     PlanL pl;
     uint32_t wpos;
     bool started;
-    float xp[XPREV ? kChunk : 1];   // XPREV: the previous chunk's input
 
     __device__ __forceinline__ void init(const ChorusArgs &a, float *lds_region, uint32_t lane_, uint32_t inst0_) {
         lane = lane_; j = lane >> 1; ch = lane & 1u; inst0 = inst0_; n = a.n;
@@ -342,13 +339,13 @@ struct ChStageL {
     }
 
     // first chunk of the launch: store its inputs, then load both lines of every window (fresh).
-    // XPREV: no store (chunk 0 stores its own input), x is unused.  COOP: x is read from xq.
+    // COOP: x is read from xq.
     __device__ __forceinline__ void begin(float (&x)[kChunk], int C, const float4 (&xq)[4]) {
         if (COOP) {
             stage_rows(xq);
             coop_store(true, 0, wpos, C);
             read_own(x, C);
-        } else if (!XPREV) {
+        } else {
             stage_run(x, 0);
             coop_store(true, 0, wpos, C);
         }
@@ -372,10 +369,7 @@ struct ChStageL {
             stage_run(psv, kPsvBase);
             coop_store(false, kPsvBase, w0, C);
         }
-        if (XPREV) {                                    // this chunk's own input
-            stage_run(x, 0);
-            coop_store(true, 0, w0, C);
-        } else if (COOP) {                              // x_{c+1}: rows -> staging -> ring and lanes
+        if (COOP) {                              // x_{c+1}: rows -> staging -> ring and lanes
             if (Cn > 0) {
                 stage_rows(xq);
                 coop_store(true, 0, w0 + (uint32_t)C, Cn);
@@ -460,26 +454,6 @@ struct ChStageL {
         }
         stage_tap<PAR, 0>();
         stage_tap<PAR, 1>();
-        // XPREV: x_{c-1} is not in a carried line (stored during chunk c-1, after its loads)
-        if (XPREV && started) {
-            // frame k of x_{c-1} -> slot k - 16 - s when in the window
-            const int loA = kChunk + cur.sA, loB = kChunk + cur.sB;
-            if constexpr (kClampPatch) {              // outside the window: the junk slot kWin
-                const uint32_t nA = (uint32_t)(-loA), nB = (uint32_t)(-loB);
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) {
-                    wP0[min((uint32_t)k + nA, (uint32_t)kWin) * kRow] = xp[k];
-                    wP1[min((uint32_t)k + nB, (uint32_t)kWin) * kRow] = xp[k];
-                }
-            } else {                                  // exec-masked, constant offsets
-                float *pA = wP0 - loA * kRow, *pB = wP1 - loB * kRow;
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) {
-                    if (k >= loA && k < loA + kWin) pA[k * kRow] = xp[k];
-                    if (k >= loB && k < loB + kWin) pB[k * kRow] = xp[k];
-                }
-            }
-        }
         // x_c is not in a carried line either.  Its slot k - s is >= 2 (a pitch window starts at
         // s <= -4: delays are >= 1), so only the top can leave the window
         {
@@ -557,16 +531,6 @@ struct ChStageL {
         } else {
             // generic chunk (partial, or a pitch window the lines cannot cover): per frame, with
             // per-frame guards and direct ring reads for the uncovered pitch taps
-            if (XPREV) {
-                // XPREV stores the chunk's own input only after its line loads (stores_and_next),
-                // but a direct read of an uncovered tap can reach into this chunk (a delay below
-                // 16 right after a phasor wrap): store it now, per lane (the coalesced store
-                // follows as usual).  The reads below are this lane's own, in issue order.
-                const uint32_t pb = own_pb();
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k)
-                    st1(rP, valid && k < C ? pb + ((w0 + (uint32_t)k) & pmask) * 8u : 0xFFFFFFF0u, 0, x[k]);
-            }
             float pl_lfo[2], pl_gA[2], pl_gB[2];
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) {
@@ -670,10 +634,6 @@ struct ChStageL {
             }
         }
         wpos = w0 + (uint32_t)C;
-        if (XPREV) {
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) xp[k] = x[k];
-        }
     }
 
     __device__ __forceinline__ void finish(const ChorusArgs &a) const {
