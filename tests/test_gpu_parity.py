@@ -691,6 +691,23 @@ def test_chain_vs_composed_oracle(cuda):
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
 
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 129])
+def test_chain_ragged_groups_and_short_blocks(cuda, n):
+    """The chain's stages at group edges (the pitch role's stereo lanes past the last instance mirror
+    it; one, two and three 64-instance groups, the last partial) and blocks of 4 and 20 frames (a
+    lone short chunk, a full chunk plus a short one): bit-exact against the composed oracle."""
+    rng = np.random.default_rng(53 + n)
+    pc, pp, pd = chorus_params(rng, n), chorus_params(rng, n)[[0, 7]], dt_params(rng, n, 0.0)
+    pd[0] = rng.uniform(0, 0.05, n)
+    x = fast_noise(n, 600, seed=53 + n)
+    e = engine("chain", n)
+    e.set_params(0, np.concatenate([pc, pp, pd], 0))
+    y = run_gpu(e, x, [4, 20, 256, 4, 316], cuda)
+    c1, c2, d = _chain_oracle(n, pc, pp, pd)
+    yr = d.process(c2.process(c1.process(x)))
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
 def _chain_oracle(n, pc, pp, pd):
     c1, c2, d = O.Chorus(n), O.Chorus(n, mode=1), O.Dattorro(n)
     _chain_oracle_set(c1, c2, d, n, pc, pp, pd)
