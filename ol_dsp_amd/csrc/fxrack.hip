@@ -38,6 +38,11 @@
 
 namespace olfx {
 
+// A/B knob: 1 = per-lane audio I/O (16 + 16 single floats per lane and chunk) everywhere
+#ifndef OLFX_FXRACK_PERLANE
+#define OLFX_FXRACK_PERLANE 0
+#endif
+
 namespace {
 
 constexpr int kFrThreads = 256;
@@ -45,7 +50,15 @@ constexpr int kFrChunk = 16;
 constexpr int kFrWin = 20;                          // window slots (18 read) staged from two lines
 constexpr int kFrSlots = kFrWin + 1;                // + junk slot
 constexpr int kFrStride = 36;                       // staging floats per instance (32 + pad)
-constexpr int kFrRegion = kFrSlots * 64 + 32 * kFrStride;   // floats of LDS per wave
+constexpr int kFrOutCh = 16 * 32 + 32;              // output staging [ch][frame][instance], per channel
+// floats of LDS per wave: the window, the ring-run staging (which also transposes the cooperative
+// input rows) and, with cooperative I/O, the output staging
+constexpr int kFrRegion = kFrSlots * 64 + 32 * kFrStride + 2 * kFrOutCh;
+__device__ __forceinline__ void wave_lds_order() {   // one wave's LDS writes before its other lanes' reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // Svf::Process (DaisySP, double-sampled Chamberlin) returning the selected output
 // (0 low, 1 band, 2 high, 3 notch, 4 peak), as oracle/fxrack_ref.c.  Each output is the mean of its
@@ -95,7 +108,11 @@ __device__ __forceinline__ uint32_t wrap48k(int64_t p) {
 // 3 ReverbFx<2>, 4 FilterFx<2>; the firmware's objects, ol_daisy/app/synth/main.cpp:82-85): the
 // same lanes and ticks, with per-instance selects of what each lane outputs.  Engines of racks only
 // (topologies 0 / 1) run COMP = false, the rack's own instruction stream.
-template <bool COMP>
+// COOP (round 3): the block's audio moves as cooperative (frame, channel) rows of the wave's 32
+// instances (4 x 16 B per lane and chunk each way, transposed through LDS, as the chorus) instead of
+// 16 + 16 single floats per lane; for n and the plane distance multiples of 4 and 16-B aligned
+// buffers.
+template <bool COMP, bool COOP>
 __global__ __launch_bounds__(kFrThreads) void fxrack_block_v3(FxRackArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const uint32_t tid = threadIdx.x;
@@ -153,6 +170,32 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v3(FxRackArgs a) {
     float *win = lds + wib * kFrRegion;                 // [kFrSlots][64]
     float *wcol = win + lane;
     float *stage = win + kFrSlots * 64;                 // [32][kFrStride]
+    float *ostage = stage + 32 * kFrStride;             // COOP: [ch][frame][instance]
+    // COOP rows: row r = 8 q + lane / 8 of instruction q is (frame r / 2, channel r % 2) of
+    // instances pinst .. + 3
+    const uint32_t pinst = inst0 + (lane & 7u) * 4u;
+    auto row_r = [&](int q) { return (uint32_t)q * 8u + (lane >> 3); };
+    auto row_v = [&](int q, uint32_t f) {
+        const uint32_t r = row_r(q);
+        return (r & 1u) * (uint32_t)a.plane * 4u + min(f + (r >> 1), nf - 1u) * frame_b + pinst * 4u;
+    };
+    float4 xq[4];
+    // the rows -> the staging [instance][2 frame + ch] -> this lane's frames (k < Cx; else 0)
+    auto rows_to_lanes = [&](float (&xv)[kFrChunk], int Cx) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float *st = stage + (lane & 7u) * 4u * kFrStride + row_r(q);
+            st[0] = xq[q].x;
+            st[kFrStride] = xq[q].y;
+            st[2 * kFrStride] = xq[q].z;
+            st[3 * kFrStride] = xq[q].w;
+        }
+        wave_lds_order();
+        const float *own = stage + j * kFrStride + ch;
+#pragma unroll
+        for (int k = 0; k < kFrChunk; ++k) xv[k] = k < Cx ? own[2 * k] : 0.f;
+        wave_lds_order();
+    };
 
     // window of the chunk starting at t: first position (t - D - 1) rounded down to even, as an
     // offset from t -- the same for every chunk (t is even)
@@ -197,8 +240,14 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v3(FxRackArgs a) {
     float x[kFrChunk], xn[kFrChunk], y[kFrChunk], y2[kFrChunk];
     const uint32_t t00 = a.t0;                          // ring position of frame 0
     int C = (int)min((uint32_t)kFrChunk, nf);
+    if constexpr (COOP) {
 #pragma unroll
-    for (int k = 0; k < kFrChunk; ++k) x[k] = k < C ? ch::ld1(rIn, io_v, (uint32_t)k * frame_b) : 0.f;
+        for (int q = 0; q < 4; ++q) xq[q] = ch::ld4(rIn, row_v(q, 0));
+        rows_to_lanes(x, C);
+    } else {
+#pragma unroll
+        for (int k = 0; k < kFrChunk; ++k) x[k] = k < C ? ch::ld1(rIn, io_v, (uint32_t)k * frame_b) : 0.f;
+    }
     load_line(lo, lcur);
     load_line(nx, next_line(lcur));
     // A chunk's stores (ring run and outputs) are issued at the start of the NEXT chunk, ahead of
@@ -217,9 +266,20 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v3(FxRackArgs a) {
             const bool ok = oi < n && (int)f2 < Cp;     // else an offset past the buffer: dropped
             ch::st4(rR, ok ? oo * kRing + wrap48k((int64_t)tp + f2) * 8u : 0xFFFFFFF0u, vv);
         }
+        if constexpr (COOP) {
+            // the outputs, staged [ch][frame][instance] by the chunk (lane ch holds plane 1 - ch)
 #pragma unroll
-        for (int k = 0; k < kFrChunk; ++k)
-            if (k < Cp) ch::st1(rOut, out_v, (fp + (uint32_t)k) * frame_b, o[k]);
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t r = row_r(q), f = r >> 1;
+                const float4 v = *(const float4 *)(ostage + (r & 1u) * kFrOutCh + f * 32u + (lane & 7u) * 4u);
+                const bool ok = pinst < n && (int)f < Cp;
+                ch::st4(rOut, ok ? (r & 1u) * (uint32_t)a.plane * 4u + (fp + f) * frame_b + pinst * 4u : 0xFFFFFFF0u, v);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kFrChunk; ++k)
+                if (k < Cp) ch::st1(rOut, out_v, (fp + (uint32_t)k) * frame_b, o[k]);
+        }
     };
     for (uint32_t f0 = 0; f0 < nf; f0 += kFrChunk) {
         C = (int)min((uint32_t)kFrChunk, nf - f0);
@@ -247,10 +307,15 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v3(FxRackArgs a) {
         }
         if (f0 > 0) flush(f0 - kFrChunk, kFrChunk);     // the previous chunk was full
         // ---- 2. the next chunk's inputs and new line in flight (unconditional); L + 1 is carried ----
+        if constexpr (COOP) {
 #pragma unroll
-        for (int k = 0; k < kFrChunk; ++k) {
-            const float vv = ch::ld1(rIn, io_v, min(f0 + kFrChunk + (uint32_t)k, nf - 1u) * frame_b);
-            xn[k] = k < Cn ? vv : 0.f;
+            for (int q = 0; q < 4; ++q) xq[q] = ch::ld4(rIn, row_v(q, f0 + kFrChunk));
+        } else {
+#pragma unroll
+            for (int k = 0; k < kFrChunk; ++k) {
+                const float vv = ch::ld1(rIn, io_v, min(f0 + kFrChunk + (uint32_t)k, nf - 1u) * frame_b);
+                xn[k] = k < Cn ? vv : 0.f;
+            }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) lo[r] = nx[r];
@@ -323,6 +388,13 @@ __global__ __launch_bounds__(kFrThreads) void fxrack_block_v3(FxRackArgs a) {
         };
         if (C == kFrChunk) static_for<kFrChunk + 1>([&](auto kt) { tick(std::false_type{}, kt); });
         else static_for<kFrChunk + 1>([&](auto kt) { tick(std::true_type{}, kt); });
+        if constexpr (COOP) {
+            // the next chunk's input rows through the staging (free since this chunk's flush) into
+            // the lanes, and this chunk's outputs into their staging (read by the next flush)
+            rows_to_lanes(xn, Cn);
+#pragma unroll
+            for (int k = 0; k < kFrChunk; ++k) ostage[(1u - ch) * kFrOutCh + (uint32_t)k * 32u + j] = o[k];
+        }
         // ---- 4. the chunk's writes -> LDS staging ([instance][frame][ch]); they leave as 128-B
         //         runs (8 lanes each) with the next chunk's flush ----
         {
@@ -349,8 +421,15 @@ hipError_t launch_fxrack(const FxRackArgs &a, hipStream_t s) {
     const uint32_t waves = (a.n + 31) / 32;
     const uint32_t blocks = (waves + kFrThreads / 64 - 1) / (kFrThreads / 64);
     const size_t lds = (size_t)(kFrThreads / 64) * kFrRegion * sizeof(float);
-    if (a.components) hipLaunchKernelGGL(fxrack_block_v3<true>, dim3(blocks), dim3(kFrThreads), lds, s, a);
-    else hipLaunchKernelGGL(fxrack_block_v3<false>, dim3(blocks), dim3(kFrThreads), lds, s, a);
+    const bool coop = !OLFX_FXRACK_PERLANE && (a.n & 3u) == 0 && (a.plane & 3u) == 0 &&
+                      (((uintptr_t)a.in | (uintptr_t)a.out) & 15u) == 0;
+    if (a.components) {
+        if (coop) hipLaunchKernelGGL((fxrack_block_v3<true, true>), dim3(blocks), dim3(kFrThreads), lds, s, a);
+        else hipLaunchKernelGGL((fxrack_block_v3<true, false>), dim3(blocks), dim3(kFrThreads), lds, s, a);
+    } else {
+        if (coop) hipLaunchKernelGGL((fxrack_block_v3<false, true>), dim3(blocks), dim3(kFrThreads), lds, s, a);
+        else hipLaunchKernelGGL((fxrack_block_v3<false, false>), dim3(blocks), dim3(kFrThreads), lds, s, a);
+    }
     return hipGetLastError();
 }
 
