@@ -224,6 +224,49 @@ def test_host_io_streams_and_interleaved_engines(cuda, kind):
     assert bits_equal(ya, yc), first_mismatch(ya, yc)
 
 
+@pytest.mark.parametrize("kind", ["chain", "chorus", "pitchshift", "fxrack", "dattorro"])
+def test_cooperative_and_per_lane_io_agree(cuda, kind):
+    """The kernels move audio as cooperative 16-B rows when n, the plane distance and both buffers
+    allow it (16-B aligned), and per lane otherwise.  n = 64 with 16-B aligned tensors takes the
+    rows; the same tensors offset by one float (4-B aligned) take the per-lane path: bit-identical,
+    with ragged and short blocks."""
+    import torch
+    n = 64
+    rng = np.random.default_rng(21)
+    if kind == "chain":
+        p = np.concatenate([chorus_params(rng, n), chorus_params(rng, n)[[0, 7]], dt_params(rng, n, 0.02)], 0)
+    elif kind == "chorus":
+        p = chorus_params(rng, n)
+    elif kind == "fxrack":
+        p = fxrack_params(rng, n)
+    elif kind == "dattorro":
+        p = dt_params(rng, n, 0.02)
+    else:
+        p = None                                   # pitch-shift defaults
+    blocks = [256, 20, 4, 236, 512]
+    x = fast_noise(n, sum(blocks), seed=21)
+    ea, eb = engine(kind, n), engine(kind, n)
+    if p is not None:
+        ea.set_params(0, p)
+        eb.set_params(0, p)
+    ya = run_gpu(ea, x, blocks, cuda)
+    och = ea.info.out_channels
+    outs, f0 = [], 0
+    for b in blocks:
+        xs = torch.empty(x.shape[0] * b * n + 1, dtype=torch.float32, device=cuda)
+        xo = xs[1:].view(x.shape[0], b, n)
+        xo.copy_(torch.from_numpy(np.ascontiguousarray(x[:, f0:f0 + b])))
+        ys = torch.empty(och * b * n + 1, dtype=torch.float32, device=cuda)
+        yo = ys[1:].view(och, b, n)
+        assert xo.data_ptr() % 16 and yo.data_ptr() % 16
+        eb.process(xo, out=yo)
+        outs.append(yo.cpu().numpy())
+        f0 += b
+    torch.cuda.synchronize()
+    yb = np.concatenate(outs, 1)
+    assert bits_equal(ya, yb), first_mismatch(ya, yb)
+
+
 def test_dattorro_reset(cuda):
     n = 8
     x = fast_noise(n, 512, seed=6)
