@@ -734,7 +734,7 @@ def test_chain_vs_composed_oracle(cuda):
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
 
-@pytest.mark.parametrize("n", [1, 63, 64, 65, 129])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 68, 129])
 def test_chain_ragged_groups_and_short_blocks(cuda, n):
     """The chain's stages at group edges (the pitch role's stereo lanes past the last instance mirror
     it; one, two and three 64-instance groups, the last partial) and blocks of 4 and 20 frames (a
@@ -807,7 +807,7 @@ def _fxrack_pair(n, p):
     return e, ref
 
 
-@pytest.mark.parametrize("n", [37, 96])
+@pytest.mark.parametrize("n", [36, 37, 96])
 def test_fxrack_vs_oracle(cuda, n):
     """FxRack<2> bit-exact against the oracle: ragged instance counts, partial chunks, and
     delays from 0 to 47999 samples (every 4th instance shorter than a chunk)."""
