@@ -11,7 +11,9 @@
 // for 32.  A wave alone on its SIMD issues every one of those instructions serially (DESIGN.md
 // section 4), so the role's instruction count is its time.
 //
-// Everything else is ChStageL's XPREV form, operation for operation (bit-exact):
+// Everything else follows the per-lane stage it replaced (ChStageL's former XPREV form, which took
+// its input one chunk late; removed from chorus_stage_l.h with this file), operation for operation
+// (bit-exact):
 //   * per tap and instance the two aligned 128-B lines L', L'+1 of the window are carried in
 //     registers, spread over the wave (8 lanes x 16 B per line; 8 parts of 8 instances);
 //   * the stage stores its own input x_c (staged in LDS, cooperative 128-B runs) before the next
