@@ -4,21 +4,28 @@
 One step = one 256-frame block (48 kHz) processed for every instance on every rank, inputs
 already resident in HBM (a pool of distinct synthetic blocks, cycled, larger than the 256 MiB
 Infinity Cache).  Default workload = BASELINE.json configs[1]: 65,536 stereo ChorusEffect
-instances per GPU.  Multi-GPU: one process per GPU (torchrun); the job is `instances per GPU x
-world` GLOBAL instances, each rank takes its contiguous shard (ol_dsp_amd.dist.shard) and derives
-every instance's parameters and input stream from its global index (ol_dsp_amd.workload), so an
-N-GPU run processes exactly the instances a one-GPU run of the same total would.  No data-path
-collective (weak scaling); one RCCL all-reduce after each timed region gathers the counters.
+instances per GPU.
 
-Prints ONE JSON line (rank 0): metric/value/unit/... plus
+Multi-GPU: one process per GPU.  Under torchrun the ranks come from the environment; without a
+launcher, `--gpus N` (N > 1) starts the N rank processes itself (ol_dsp_amd.dist.launch_ranks),
+before anything touches the GPU.  The job is `instances per GPU x world` GLOBAL instances, each
+rank takes its contiguous shard (ol_dsp_amd.dist.shard) and derives every instance's parameters
+and input stream from its global index (ol_dsp_amd.workload), so an N-GPU run processes exactly
+the instances a one-GPU run of the same total would.  No data-path collective (weak scaling); one
+RCCL all-reduce after each timed region gathers the counters.
+
+Prints ONE compact JSON line (rank 0; the whole record, every leg in full, goes to --full-json):
   roofline     : algorithmic bytes of the dominant kernel / its HIP-event-timed duration vs 8 TB/s
                  (frac = read+write, frac_read = the read share: the north star's HBM-read roofline)
   cpu_baseline : the CPU oracle (port) or the compiled reference (reference) on all host cores
-                 given to this process, at -O2 and -O0 (the reference's CMake default)
+                 given to this process, at -O2 (value) and -O0 (value_O0, the reference's default)
+  parity       : UNTIMED, after all legs: sampled instances (first, last, wave edges) of the last
+                 timed block against the CPU oracle replaying the same W+K blocks (inputs read back
+                 from the device pool, the same control/note schedule) -- bit-exact for the reverb,
+                 chorus, pitch-shift, chain and rack, max rel err vs 1e-5 for the voices
   cpu_c1       : BASELINE configs[0]: one chorus instance, one core, per-frame calls
-  also         : the other BASELINE configs timed in the same run (dattorro = configs[2], the
-                 north star's >= 64k chorus+reverb chains, configs[4]'s per-GPU shard, configs[3]'s
-                 voices, the fxlib rack), each with its own roofline and cpu_baseline
+  also         : the other BASELINE configs timed in the same run, one compact entry each (the
+                 north star's 65,536 chains last)
 """
 from __future__ import annotations
 
@@ -47,6 +54,7 @@ VOICE_FLOPS_PER_SAMPLE = 64.0
 # accumulate 3 (x4 = 168) -> 216.
 VOICE_MOOG_FLOPS_PER_SAMPLE = 216.0
 VOICE_KINDS = ("voice", "voice_moog")
+VOICE_TOL = 1e-5      # max |gpu - ref| / max(|ref|, rms(ref)) per voice (tests/test_gpu_parity.py)
 WORKLOADS = {
     # name: (kind, default instances per GPU, BASELINE config it restates)
     "chorus": ("chorus", 65536, "configs[1]: 65,536 ChorusEffect instances, 48 kHz, 256-sample blocks, 1xMI355X"),
@@ -74,12 +82,15 @@ WORKLOADS = {
 PARAM_SET = {"dattorro_rpd": "dattorro_rpd", "chain_rpd": "chain_rpd"}
 # the event-free workload a control leg is compared with (same kind and instances)
 EVENT_FREE = {"voice_events": "voice", "chain_cc": "chain"}
-DEFAULT_ALSO = "dattorro,chain_65536,chain,voice,voice_moog,fxrack,voice_events,chain_cc,dattorro_rpd,chain_rpd"
+# legs in print order; the north star's 65,536 chains last (the end of the line survives any tail cut)
+DEFAULT_ALSO = ("voice_poly,voice_events,chain_cc,dattorro_rpd,chain_rpd,voice_moog,fxrack,voice,chain,"
+                "dattorro,chain_65536")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without torchrun, N > 1 launches the N rank processes itself")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="chorus", choices=sorted(WORKLOADS))
@@ -92,8 +103,21 @@ def parse():
     ap.add_argument("--pool-bytes", type=float, default=1.0e9, help="bytes of distinct input blocks (> 256 MiB IC)")
     ap.add_argument("--cpu-seconds", type=float, default=4.0, help="wall budget of each -O2 CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may run on")
+    ap.add_argument("--no-parity", action="store_true", help="skip the untimed oracle parity check per leg")
     ap.add_argument("--traffic-json", default="", help="PMC traffic summary (tools/pmc_traffic.py)")
-    return ap.parse_args()
+    ap.add_argument("--full-json", default=os.path.join(ROOT, "gpurun_out", "bench_full.json"),
+                    help="where the full (verbose) record of every leg is written ('' = nowhere)")
+    ap.add_argument("--stub", action="store_true",
+                    help="CPU launcher check: a no-GPU stand-in leg over gloo (tests/test_bench_launch.py)")
+    return ap.parse_args(argv)
+
+
+def _r(x, sig: int = 4):
+    """Round for the compact line (significant digits)."""
+    if x is None or isinstance(x, (bool, int, str)):
+        return x
+    x = float(x)
+    return float(f"{x:.{sig}g}") if np.isfinite(x) else None
 
 
 # ------------------------------------------------------------------------------------------------
@@ -122,45 +146,59 @@ def host_facts() -> dict:
     return {"nproc": nproc, "host_cpus": os.cpu_count(), "cpu_model": model}
 
 
-def _cpu_bank(kind: str, n: int, sr: float, o0: bool, ref: bool, pset: str = ""):
+def _oracle():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    from ol_dsp_amd.workload import instance_params, voice_notes
-    p = instance_params(pset or kind, 0, n)
+    return O
+
+
+def _oracle_bank(kind: str, p: np.ndarray, sr: float, o0: bool = False, ref: bool = False, notes=None,
+                 frames: int = 256):
+    """CPU oracle bank of `kind` for params p [fields][m] (columns = instances): (step, banks,
+    setter).  step(x [ch][frames][m] or None, threads) -> [och][frames][m]; setter(j, field, v)
+    sets one C-ABI field of instance j (the chain's fields route to their stage)."""
+    O = _oracle()
+    n = p.shape[1]
     if kind == "dattorro":
         bank = O.Dattorro(n, ref=ref, o0=o0)
         for i in range(n):
             for f in range(7):
                 bank.set(i, f, float(p[f, i]))
-        return lambda x, t: bank.process(x, t), bank
+        return (lambda x, t=1: bank.process(x, t)), bank, (lambda j, f, v: bank.set(j, f, v))
     if kind in ("chorus", "pitchshift"):
         bank = O.Chorus(n, sr, 0 if kind == "chorus" else 1, o0=o0)
+        fmap = (lambda f: f) if kind == "chorus" else (lambda f: (0, 7)[f])
         for i in range(n):
             for f in range(p.shape[0]):
-                bank.set(i, f if kind == "chorus" else (0, 7)[f], float(p[f, i]))
-        return lambda x, t: bank.process(x, t), bank
+                bank.set(i, fmap(f), float(p[f, i]))
+        return (lambda x, t=1: bank.process(x, t)), bank, (lambda j, f, v: bank.set(j, fmap(f), v))
     if kind == "fxrack":
         bank = O.FxRack(n, sr, o0=o0)
         for i in range(n):
             for f in range(p.shape[0]):
                 bank.set(i, f, float(p[f, i]))
-        return lambda x, t: bank.process(x, t), bank
+        return (lambda x, t=1: bank.process(x, t)), bank, (lambda j, f, v: bank.set(j, f, v))
     if kind in VOICE_KINDS:
         bank = O.Voice(n, sr, moog=kind == "voice_moog", o0=o0)
-        notes = voice_notes(0, n)
         for i in range(n):
             bank.config(i, p[:, i])
-            bank.note(i, True, int(notes[i]))
-        return lambda x, t: bank.process(x.shape[1], t), bank
+            if notes is not None:
+                bank.note(i, True, int(notes[i]))
+        return (lambda x, t=1: bank.process(frames if x is None else x.shape[1], t)), bank, None
     # chain: the composed stages, each a real bank with the chain's parameters
     c1, c2, d = O.Chorus(n, sr, 0, o0=o0), O.Chorus(n, sr, 1, o0=o0), O.Dattorro(n, ref=ref, o0=o0)
+
+    def setter(j, f, v):
+        if f < 8:
+            c1.set(j, f, v)
+        elif f < 10:
+            c2.set(j, (0, 7)[f - 8], v)
+        else:
+            d.set(j, f - 10, v)
     for i in range(n):
-        for f in range(8):
-            c1.set(i, f, float(p[f, i]))
-        c2.set(i, 0, float(p[8, i]))
-        c2.set(i, 7, float(p[9, i]))
-        for f in range(7):
-            d.set(i, f, float(p[10 + f, i]))
-    return lambda x, t: d.process(c2.process(c1.process(x, t), t), t), (c1, c2, d)
+        for f in range(p.shape[0]):
+            setter(i, f, float(p[f, i]))
+    return (lambda x, t=1: d.process(c2.process(c1.process(x, t), t), t)), (c1, c2, d), setter
 
 
 def cpu_baseline(kind: str, block: int, sr: float, budget_s: float, threads: int, pset: str = "") -> dict:
@@ -168,16 +206,17 @@ def cpu_baseline(kind: str, block: int, sr: float, budget_s: float, threads: int
     sample of the same workload: the same global instances 0..n-1 with the same parameters and
     input streams, 256-frame blocks, OpenMP schedule(static) over instances, until the wall
     budget is spent; then the same at -O0 for a quarter of the budget."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
-    from ol_dsp_amd.workload import noise_np
+    O = _oracle()
+    from ol_dsp_amd.workload import instance_params, noise_np, voice_notes
     n = 8192 if kind not in VOICE_KINDS else 32768
     ich = 0 if kind in VOICE_KINDS else 2
-    x = noise_np(0, n, block, 2) if ich else np.zeros((1, block, n), np.float32)
+    x = noise_np(0, n, block, 2) if ich else None
     ref = kind in ("dattorro", "chain") and O.ref_available() and O.ref_available(o0=True)
+    p = instance_params(pset or kind, 0, n)
+    notes = voice_notes(0, n) if kind in VOICE_KINDS else None
 
     def timed(o0: bool, budget: float):
-        step, _keep = _cpu_bank(kind, n, sr, o0, ref, pset)
+        step, _keep, _ = _oracle_bank(kind, p, sr, o0, ref, notes, block)
         step(x, threads)  # warm
         t0 = time.perf_counter()
         blocks = 0
@@ -204,8 +243,7 @@ def cpu_baseline(kind: str, block: int, sr: float, budget_s: float, threads: int
 def cpu_c1(sr: float, block: int) -> dict:
     """BASELINE configs[0]: one ChorusEffect instance, one core, 60 s of audio in
     256-frame blocks, one process() call per frame as in the reference's fx_test.cpp:45-54 loop."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
+    O = _oracle()
     from ol_dsp_amd.workload import instance_params
     p = instance_params("chorus", 0, 1)[:, 0]
     frames = int(60 * sr)
@@ -220,6 +258,59 @@ def cpu_c1(sr: float, block: int) -> dict:
                 "sample": f"1 instance, {frames} frames (60 s @ {sr:.0f} Hz), {block}-frame blocks, per-frame "
                           "process() calls (fx_test.cpp:45-54 loop shape), oracle C restatement -O2 / -O0"})
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# Untimed on-box parity of each leg's last timed block (the oracle as the checker)
+# ------------------------------------------------------------------------------------------------
+def sample_instances(n: int) -> np.ndarray:
+    """First, last, and the edges of waves (32 chorus instances, 64 reverb/voice lanes) and of the
+    middle of the shard."""
+    idx = {0, 1, 31, 32, 63, 64, 127, n // 2 - 1, n // 2, n - 65, n - 64, n - 33, n - 32, n - 1}
+    return np.array(sorted(i for i in idx if 0 <= i < n), np.int64)
+
+
+def parity_check(job: dict, sr: float) -> dict:
+    """Replay the leg's W+K blocks for the sampled instances on the CPU oracle and compare the
+    last block with what the GPU produced (job filled in by run_workload)."""
+    kind, idx, B = job["kind"], job["idx"], job["block"]
+    m = len(idx)
+    step, _banks, setter = _oracle_bank(kind, job["params"], sr, notes=job.get("notes"), frames=B)
+    voice = kind in VOICE_KINDS
+    bank = _banks if voice else None
+    xs, pool_n = job.get("pool"), job.get("pool_n", 1)
+    y = None
+    for b in range(job["blocks"]):
+        if voice:
+            if b == job.get("note_off_block", -1):
+                for j in range(m):
+                    bank.note(j, False, int(job["notes"][j]))
+            for j, on, note in job.get("events", lambda b: [])(b):
+                bank.note(j, on, note)
+        for j, f, v in job.get("ccs", lambda b: [])(b):
+            setter(j, f, v)
+        y = step(None if voice else xs[b % pool_n])
+    g = job["gpu"]
+    res = {"instances": m, "blocks": job["blocks"]}
+    if voice:
+        fin = np.isfinite(y).all(axis=(0, 1)) & np.isfinite(g).all(axis=(0, 1))
+        same_fin = bool(np.array_equal(np.isfinite(y), np.isfinite(g)))
+        a = g[0][:, fin].T.astype(np.float64)
+        r = y[0][:, fin].T.astype(np.float64)
+        rms = np.sqrt(np.mean(r ** 2, axis=1, keepdims=True)) + 1e-30
+        err = float(np.max(np.abs(a - r) / np.maximum(np.abs(r), rms))) if a.size else 0.0
+        res.update({"check": f"max_rel_err<={VOICE_TOL:g}", "max_rel_err": err,
+                    "ok": bool(same_fin and err <= VOICE_TOL), "finite_instances": int(fin.sum())})
+    else:
+        bad = int(np.count_nonzero(np.ascontiguousarray(g).view(np.uint32) != np.ascontiguousarray(y).view(np.uint32)))
+        res.update({"check": "bit-exact", "ok": bad == 0, "mismatched_samples": bad})
+    if "bus_gpu" in job:     # the mix kernel on the last block: bit-exact against Polyvoice's += order
+        O = _oracle()
+        bus_ref = O.mix_ref(job["bus_voices"], job["bus_lists"])
+        bad = int(np.count_nonzero(bus_ref.view(np.uint32) != job["bus_gpu"].view(np.uint32)))
+        res["buses"] = {"check": "bit-exact", "buses": len(job["bus_lists"]), "mismatched_samples": bad}
+        res["ok"] = res["ok"] and bad == 0
+    return res
 
 
 # ------------------------------------------------------------------------------------------------
@@ -239,6 +330,27 @@ def _traffic(name: str, n: int, B: int, override: str = ""):
     return None
 
 
+def run_stub(name: str, n_per_gpu: int, args, rank: int, world: int) -> dict:
+    """--stub: the launcher's CPU check.  No engine and no GPU: each rank 'processes' its shard for
+    K steps (a host sleep per step), then the same single all-reduce as a real leg (gloo)."""
+    from ol_dsp_amd.dist import RunStats, reduce_stats, shard
+    total = n_per_gpu * world
+    first, n = shard(total, world, rank)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001)
+    elapsed = time.perf_counter() - t0
+    st = reduce_stats(RunStats(elapsed, elapsed * 1e3 / args.steps, float(n) * args.block * args.steps,
+                               float(first), 1.0))
+    if rank != 0:
+        return {}
+    return {"metric": METRIC, "value": st.frames / st.elapsed_s, "unit": "stereo samples/s",
+            "ms_per_step": st.elapsed_s / args.steps * 1e3, "frames": st.frames, "ranks_reporting": int(st.ranks),
+            "config": {"workload": name, "instances_per_gpu": n_per_gpu, "instances_total": total,
+                       "block": args.block, "parallelism": f"instance-shard x{world} (stub: no GPU)"},
+            "roofline": None, "cpu_baseline": None, "output_checksum": st.checksum, "output_nonfinite_rank0": 0}
+
+
 def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, with_cpu: bool) -> dict:
     import torch
 
@@ -252,7 +364,8 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
     B = args.block
     eng = ofx.Engine(kind, n, sample_rate=args.sample_rate, block=B, device=dev.index or 0)
     pset = PARAM_SET.get(name, kind)
-    eng.set_params(0, instance_params(pset, first, n))
+    params = instance_params(pset, first, n)
+    eng.set_params(0, params)
     ich, och = eng.info.in_channels, eng.info.out_channels
 
     # input pool: distinct synthetic blocks of each global instance's own stream, on the device
@@ -267,9 +380,9 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
         eng.note_events(eng.make_events(np.arange(n), 1, notes))
         note_off = eng.make_events(np.arange(n), 0, notes)
     # control legs: the per-step calls are prebuilt (untimed), so a step is the library call only
+    gi = np.arange(first, first + n)
     step_events = None
     if name == "voice_events":     # voices i % 40 == k % 40 get NoteOn, i % 40 == (k + 20) % 40 NoteOff
-        gi = np.arange(first, first + n)
         step_events = []
         for k in range(40):
             on = np.nonzero(gi % 40 == k)[0]
@@ -280,7 +393,6 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
     step_ccs = None
     if name == "chain_cc":         # chains i % 100 == k % 100 get a new value of one field per step
         from ol_dsp_amd.workload import uniform01
-        gi = np.arange(first, first + n)
         fields = [("chorus_depth", .08, 1.0), ("chorus_mix", 0.0, 1.0), ("verb_decay", .25, .95),
                   ("verb_damping", .05, .95), ("pitch_shift", 0.0, 3.0)]
         step_ccs = []
@@ -291,7 +403,8 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
             step_ccs.append((eng.field(fname), sel, vals))
     bus = None
     if name == "voice_poly":       # Polyvoice buses of 8 voices (Polyvoice.h:28-33)
-        eng.mix_config([list(range(g, min(g + 8, n))) for g in range(0, n, 8)])
+        bus_lists = [list(range(g, min(g + 8, n))) for g in range(0, n, 8)]
+        eng.mix_config(bus_lists)
         bus = torch.zeros((B, eng.n_buses), device=dev)
     stream = torch.cuda.Stream(dev)        # dedicated non-default stream: events see the kernels
     torch.cuda.synchronize(dev)
@@ -369,7 +482,51 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
     nonfinite = int((~finite).sum().item())
     checksum = float(torch.where(finite, out.abs(), torch.zeros_like(out)).sum().item())
     bus_sum = float(bus.abs().sum().item()) if bus is not None else None
-    stats = reduce_stats(RunStats(elapsed, kern_ms, float(n) * B * K, checksum), device=dev)
+
+    # untimed parity material: the last timed block of sampled instances, the pool blocks they read
+    # (read back from the device: exactly the timed inputs) and the leg's event / control schedule
+    parity_job = None
+    if rank == 0 and not args.no_parity:
+        if bus is not None:        # two whole buses (first, last) so the mix can be checked too
+            nb = len(bus_lists)
+            idx = np.array(sorted(set(bus_lists[0]) | set(bus_lists[nb - 1])), np.int64)
+        else:
+            idx = sample_instances(n)
+        ti = torch.from_numpy(idx).to(dev)
+        parity_job = {"kind": kind, "idx": idx, "block": B, "blocks": W + K,
+                      "params": np.ascontiguousarray(params[:, idx]),
+                      "gpu": out.index_select(2, ti).cpu().numpy()}
+        if ich:
+            parity_job["pool"] = [np.ascontiguousarray(p.index_select(2, ti).cpu().numpy()) for p in pool]
+            parity_job["pool_n"] = pool_n
+        if voice:
+            parity_job["notes"] = notes[idx].astype(np.int64)
+            parity_job["note_off_block"] = W + K // 2
+        if step_events is not None:
+            pos = {int(i): j for j, i in enumerate(idx)}
+            sched = []
+            for k in range(40):
+                on = [(pos[int(i)], True, int((notes[i] + 12 * (k & 1)) % 128)) for i in idx if gi[i] % 40 == k]
+                off = [(pos[int(i)], False, int(notes[i])) for i in idx if gi[i] % 40 == (k + 20) % 40]
+                sched.append(on + off)
+            parity_job["events"] = lambda b, s=sched: s[b % 40]
+        if step_ccs is not None:
+            pos = {int(i): j for j, i in enumerate(idx)}
+            sched = []
+            for f, sel, vals in step_ccs:
+                sched.append([(pos[int(i)], f, float(v)) for i, v in zip(sel, vals) if int(i) in pos])
+            parity_job["ccs"] = lambda b, s=sched: s[b % 100]
+        if bus is not None:        # the mix of the last block into zeroed buses (untimed)
+            bus_chk = torch.zeros_like(bus)
+            eng.mix(out, bus_chk, stream=stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            pos = {int(i): j for j, i in enumerate(idx)}
+            lists = [bus_lists[0], bus_lists[nb - 1]]
+            parity_job["bus_lists"] = [[pos[v] for v in bl] for bl in lists]
+            parity_job["bus_voices"] = parity_job["gpu"][0]
+            parity_job["bus_gpu"] = np.ascontiguousarray(bus_chk[:, [0, nb - 1]].cpu().numpy())
+
+    stats = reduce_stats(RunStats(elapsed, kern_ms, float(n) * B * K, checksum, 1.0), device=dev)
     bpf, rbpf, kname = eng.algorithmic_bytes_per_frame, eng.algorithmic_read_bytes_per_frame, eng.kernel_name
     eng.close()
     del pool, out
@@ -410,7 +567,7 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
                     "frames_per_launch": per_launch, **measured}
     res = {"metric": METRIC, "value": frames / elapsed,
            "unit": "voice samples/s" if voice else "stereo samples/s",
-           "ms_per_step": elapsed / K * 1e3,
+           "ms_per_step": elapsed / K * 1e3, "frames": frames, "ranks_reporting": int(stats.ranks),
            "config": {"workload": name, "restates": desc, "instances_per_gpu": n_per_gpu,
                       "instances_total": total, "block": B, "sample_rate": args.sample_rate,
                       "input_pool_blocks": pool_n, "parallelism": f"instance-shard x{world} (no data-path collective)"},
@@ -431,18 +588,27 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
         res["control"] = {"instances_changed_per_block": int(np.mean([len(c[1]) for c in step_ccs])),
                           "note": "changed coefficients re-derived on the host for those instances only and "
                                   "scattered on the device ahead of the block (control.hip coef_scatter)"}
-    # the CPU baseline runs after every GPU leg (main): no leg is timed right after a many-thread
-    # CPU run (a short-kernel leg measured 1.7x slow once, launch-bound behind it)
+    # the CPU baseline and the parity replay run after every GPU leg (main): no leg is timed right
+    # after a many-thread CPU run (a short-kernel leg measured 1.7x slow once, launch-bound behind it)
     res["cpu_baseline"] = None
+    res["parity"] = None
     if with_cpu and world == 1 and args.cpu_seconds > 0:
         res["cpu_job"] = (kind, PARAM_SET.get(name, ""))
+    if parity_job is not None:
+        res["parity_job"] = parity_job
     return res
 
 
-def run_cpu_jobs(jobs, reuse, args):
-    """The deferred CPU baselines: jobs = [(result dict, kind, param set)], reuse = [(result dict,
-    the dict whose baseline it reuses, its key)]."""
+def run_cpu_jobs(jobs, reuse, parity_jobs, args):
+    """The deferred CPU work: baselines (jobs = [(result dict, kind, param set)], reuse = [(result
+    dict, the dict whose baseline it reuses, its key)]) and the parity replays ([(result dict,
+    job)])."""
     threads = args.cpu_threads or host_facts()["nproc"]
+    for target, job in parity_jobs:
+        try:
+            target["parity"] = parity_check(job, args.sample_rate)
+        except Exception as e:                 # a checker failure is reported, never hidden
+            target["parity"] = {"ok": False, "error": f"{type(e).__name__}: {e}"}
     for target, kind, pset in jobs:
         target["cpu_baseline"] = cpu_baseline(kind, args.block, args.sample_rate, args.cpu_seconds, threads, pset)
     for target, src, key in reuse:
@@ -450,53 +616,114 @@ def run_cpu_jobs(jobs, reuse, args):
             target["cpu_baseline"] = dict(src["cpu_baseline"], reused_from=key)
 
 
+# ------------------------------------------------------------------------------------------------
+# The compact line
+# ------------------------------------------------------------------------------------------------
+def _compact_parity(p):
+    if not p:
+        return p
+    if "error" in p:
+        return {"ok": False, "error": p["error"][:120]}
+    out = {"ok": p["ok"], "check": p["check"], "inst": p["instances"], "blocks": p["blocks"]}
+    if "max_rel_err" in p:
+        out["max_rel_err"] = _r(p["max_rel_err"], 3)
+    if p.get("mismatched_samples"):
+        out["mismatched"] = p["mismatched_samples"]
+    if "buses" in p:
+        out["buses_bit_exact"] = p["buses"]["mismatched_samples"] == 0
+    return out
+
+
+def compact_leg(r: dict) -> dict:
+    """One leg in ~250 bytes: instances, kernel, time, throughput, roofline fractions, measured
+    traffic per frame, the CPU baseline and the parity verdict."""
+    rf = r["roofline"]
+    c = {"n": r["config"]["instances_per_gpu"], "kernel": rf["kernel"], "kernel_ms": _r(rf["kernel_ms"]),
+         "value": _r(r["value"]), "bound": rf["bound"], "frac": _r(rf["frac"], 3)}
+    if rf["bound"] == "hbm":
+        c["frac_read"] = _r(rf["frac_read"], 3)
+        if rf.get("traffic"):
+            c["traffic_B_per_frame"] = _r(rf["traffic"] / rf["frames_per_launch"], 4)
+    if "mix" in r:
+        c["mix"] = {"kernel_ms": _r(r["mix"]["kernel_ms"]), "frac": _r(r["mix"]["frac"], 3)}
+    if "control" in r and "kernel_ms_ratio" in r["control"]:
+        c["vs_event_free"] = _r(r["control"]["kernel_ms_ratio"], 4)
+    cb = r.get("cpu_baseline")
+    if cb:
+        c["cpu_baseline"] = {"value": _r(cb["value"]), "kind": cb["kind"], "cores": cb["cores"]}
+    c["parity"] = _compact_parity(r.get("parity"))
+    return c
+
+
 def main():
     args = parse()
+    from ol_dsp_amd.dist import env_ranks, launch_ranks, self_command
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no torchrun around us: start the N rank processes here, before anything touches the GPU
+        sys.exit(launch_ranks(self_command(), args.gpus))
+
     import torch
     import torch.distributed as dist
 
-    from ol_dsp_amd.dist import env_ranks
     rank, world, local = env_ranks()
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    if args.stub:
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cpu")
+    else:
+        if world > 1:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
 
     n = args.instances or WORKLOADS[args.workload][1]
-    cpu_jobs, cpu_reuse = [], []
-    main_res = run_workload(args.workload, n, args, rank, world, dev, with_cpu=True)
-    if rank == 0 and "cpu_job" in main_res:
-        cpu_jobs.append((main_res, *main_res.pop("cpu_job")))
-    also = args.also if args.also is not None else (DEFAULT_ALSO if args.workload == "chorus" else "")
-    also_res = {}
-    for name in [a for a in also.split(",") if a]:
-        twin = EVENT_FREE.get(name)
-        tkey = twin if twin != "chain" else "chain_16384"
-        # a control leg's CPU work per block is its twin's (the CPU oracle applies events and
-        # parameters per instance at block boundaries): the twin's measured baseline is reused
-        reuse = bool(twin and tkey in also_res)
-        r = run_workload(name, WORKLOADS[name][1], args, rank, world, dev, with_cpu=not reuse)
-        if rank == 0:
+    cpu_jobs, cpu_reuse, parity_jobs = [], [], []
+    if args.stub:
+        main_res, also_res = run_stub(args.workload, n, args, rank, world), {}
+    else:
+        main_res = run_workload(args.workload, n, args, rank, world, dev, with_cpu=True)
+        if rank == 0 and "cpu_job" in main_res:
+            cpu_jobs.append((main_res, *main_res.pop("cpu_job")))
+        if rank == 0 and "parity_job" in main_res:
+            parity_jobs.append((main_res, main_res.pop("parity_job")))
+        also = args.also if args.also is not None else (DEFAULT_ALSO if args.workload == "chorus" else "")
+        also_res = {}
+        for name in [a for a in also.split(",") if a]:
+            twin = EVENT_FREE.get(name)
+            tkey = twin if twin != "chain" else "chain_16384"
+            # a control leg's CPU work per block is its twin's (the CPU oracle applies events and
+            # parameters per instance at block boundaries): the twin's measured baseline is reused
+            reuse = bool(twin and (tkey in also_res or twin in also.split(",") or twin == args.workload))
+            r = run_workload(name, WORKLOADS[name][1], args, rank, world, dev, with_cpu=not reuse)
+            if rank != 0:
+                continue
             key = name if name != "chain" else "chain_16384"
-            also_res[key] = {k: r[k] for k in ("value", "unit", "ms_per_step", "config", "roofline", "control",
-                                                "cpu_baseline", "output_checksum", "output_nonfinite_rank0") if k in r}
+            also_res[key] = r
             if "cpu_job" in r:
-                cpu_jobs.append((also_res[key], *r["cpu_job"]))
+                cpu_jobs.append((r, *r.pop("cpu_job")))
             elif reuse:
-                cpu_reuse.append((also_res[key], also_res[tkey], tkey))
-            base = EVENT_FREE.get(name)
+                cpu_reuse.append((r, tkey))
+            if "parity_job" in r:
+                parity_jobs.append((r, r.pop("parity_job")))
+        # the control legs against their event-free twins (an `also` leg or the main workload)
+        for key, r in also_res.items():
+            base = EVENT_FREE.get(key)
+            if not base:
+                continue
             bkey = base if base != "chain" else "chain_16384"
-            # the control leg's cost against its event-free twin (an `also` leg or the main workload)
             b = also_res.get(bkey) or (main_res if base == args.workload else None)
-            if base and b is not None:
-                also_res[key]["control"].update({
+            if b is not None:
+                r["control"].update({
                     "event_free_kernel_ms": b["roofline"]["kernel_ms"], "event_free_ms_per_step": b["ms_per_step"],
                     "kernel_ms_ratio": r["roofline"]["kernel_ms"] / b["roofline"]["kernel_ms"],
                     "ms_per_step_ratio": r["ms_per_step"] / b["ms_per_step"]})
+        cpu_reuse = [(r, also_res.get(tkey) or (main_res if tkey == args.workload else {}), tkey)
+                     for r, tkey in cpu_reuse]
 
     if rank == 0:
-        run_cpu_jobs(cpu_jobs, cpu_reuse, args)
+        run_cpu_jobs(cpu_jobs, cpu_reuse, parity_jobs, args)
+        rf = main_res["roofline"]
         res = {
             "metric": METRIC,
             "value": main_res["value"],
@@ -509,20 +736,45 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: per-(instance, channel) xorshift32 noise streams (SURVEY 8d seeds) in a device "
-                    "pool; per-instance params hashed from the global instance index",
-            "config": main_res["config"],
-            "roofline": main_res["roofline"],
-            "cpu_baseline": main_res["cpu_baseline"],
-            "output_checksum": main_res["output_checksum"],
-            "output_nonfinite_rank0": main_res["output_nonfinite_rank0"],
+            "data": "synthetic: per-(instance, channel) xorshift32 noise (SURVEY 8d seeds) in a device pool; "
+                    "per-instance params hashed from the global instance index",
+            "config": {k: main_res["config"][k] for k in ("workload", "instances_per_gpu", "instances_total", "block",
+                                                          "parallelism") if k in main_res["config"]},
+            "frames": main_res["frames"],
+            "ranks_reporting": main_res["ranks_reporting"],
         }
+        if rf is not None:
+            keep = ("bound", "achieved", "peak", "unit", "frac", "traffic", "achieved_read", "frac_read", "kernel",
+                    "kernel_ms", "algorithmic_bytes_per_frame", "algorithmic_read_bytes_per_frame",
+                    "frames_per_launch", "frac_read_measured")
+            res["roofline"] = {k: (_r(rf[k], 5) if isinstance(rf[k], float) else rf[k]) for k in keep if k in rf}
+        else:
+            res["roofline"] = None
+        cb = main_res.get("cpu_baseline")
+        res["cpu_baseline"] = ({k: (_r(v) if isinstance(v, float) else v) for k, v in cb.items()
+                                if k not in ("sample_O0",)} if cb else None)
+        res["parity"] = _compact_parity(main_res.get("parity"))
+        res["output_checksum"] = main_res["output_checksum"]
         if "mix" in main_res:
             res["mix"] = main_res["mix"]
-        if world == 1 and args.cpu_seconds > 0 and args.workload == "chorus":
-            res["cpu_c1"] = cpu_c1(args.sample_rate, args.block)
+        full = dict(res, roofline=rf, cpu_baseline=cb, parity=main_res.get("parity"))
+        if world == 1 and args.cpu_seconds > 0 and args.workload == "chorus" and not args.stub:
+            c1 = cpu_c1(args.sample_rate, args.block)
+            full["cpu_c1"] = c1
+            res["cpu_c1"] = {"value": _r(c1["value"]), "value_O0": _r(c1["value_O0"]), "cores": 1, "kind": "port"}
         if also_res:
-            res["also"] = also_res
+            full["also"] = also_res
+            res["also"] = {k: compact_leg(v) for k, v in also_res.items()}
+            res["all_parity_ok"] = all((v.get("parity") or {}).get("ok", False) for v in
+                                       [main_res] + list(also_res.values())) if not args.no_parity else None
+        if args.full_json:
+            try:
+                os.makedirs(os.path.dirname(args.full_json), exist_ok=True)
+                with open(args.full_json, "w") as f:
+                    json.dump(full, f, indent=1, default=str)
+                res["full_json"] = os.path.relpath(args.full_json, ROOT)
+            except OSError:
+                pass
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()

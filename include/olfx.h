@@ -219,7 +219,11 @@ int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32
                 olfx_engine **out);
 int olfx_destroy(olfx_engine *e);
 
-/* Zero all state and restore defaults (== destroy + create, without reallocating). */
+/* Zero all state and restore defaults (== destroy + create, without reallocating).  Like
+   olfx_destroy and olfx_sync it waits for THIS engine's queued work only (the stream of its latest
+   olfx_process / olfx_mix, its own streams, its control packets), never for the whole device:
+   other engines and the host's own kernels keep running.  The caller keeps the stream it passed
+   last alive until then, and orders its own streams when it switches them between blocks. */
 int olfx_reset(olfx_engine *e);
 
 /* Set parameters of instances [first, first+count): `values` is field-major
@@ -285,7 +289,7 @@ int olfx_mix_config(olfx_engine *e, uint32_t n_buses, const uint32_t *offsets, c
 int olfx_mix(olfx_engine *e, const float *voice_out, float *bus_out, uint32_t n_frames, int io_flags,
              void *stream);
 
-/* Block until all work queued by this engine is done. */
+/* Block until all work queued by this engine is done (engine-scoped, see olfx_reset). */
 int olfx_sync(olfx_engine *e);
 /* The engine's own non-blocking hipStream_t (valid until olfx_destroy). */
 void *olfx_stream(const olfx_engine *e);

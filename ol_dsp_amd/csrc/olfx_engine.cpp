@@ -400,6 +400,10 @@ struct olfx_engine {
     int pending[kGroup] = {};                   // slots used since the last marker, all on pending_stream
     int n_pending = 0;
     hipStream_t pending_stream = nullptr;
+    // the stream of the engine's latest launch (olfx_process / olfx_mix): what reset, sync and
+    // destroy wait for (engine-scoped; the caller keeps that stream alive until then, olfx.h)
+    hipStream_t last_stream = nullptr;
+    bool have_last = false;
     std::vector<int32_t> ev_slot;         // voice -> its record in `folded` during fold_events, else -1
     struct Folded { uint32_t inst, op, freq, pad; };
     std::vector<Folded> folded;
@@ -694,7 +698,11 @@ int grow_slot(olfx_engine *e, olfx_engine::Slot &sl, size_t words, bool device_h
         if (sl.h) (void)hipHostFree(sl.h);
         sl.h = nullptr; sl.hd = nullptr; sl.cap = 0;
         const size_t cap = std::max<size_t>(words, 4096);
-        HIPCHK(e, hipHostMalloc((void **)&sl.h, cap * 4, hipHostMallocDefault));
+        // zero-copy slots (read by the kernels over the host link, rewritten 16 blocks later) are
+        // coherent: no GPU cache may hold a stale line of them whatever HIP_HOST_COHERENT says;
+        // copied slots are only a copy source
+        HIPCHK(e, hipHostMalloc((void **)&sl.h, cap * 4,
+                                device_half ? hipHostMallocDefault : (hipHostMallocMapped | hipHostMallocCoherent)));
         void *dp = nullptr;
         HIPCHK(e, hipHostGetDevicePointer(&dp, sl.h, 0));
         sl.hd = (uint32_t *)dp;
@@ -815,9 +823,32 @@ int submit_control(olfx_engine *e, hipStream_t s, VoiceArgs *va, olfx_engine::Sl
     return OLFX_OK;
 }
 
+// Wait for this engine's queued work only -- not the device: its latest launch stream (the caller
+// orders its own streams, so that covers every earlier block), its own stream, and every control
+// slot's marker.  A slot whose marker failed to record falls back to a device-wide wait.
+int wait_engine(olfx_engine *e) {
+    HIPCHK(e, flush_markers(e));
+    bool unmarked = false;
+    e->each_slot([&](olfx_engine::Slot &sl) {
+        if (!sl.used) return;
+        if (sl.guard) {
+            if (hipEventSynchronize(sl.guard) != hipSuccess) unmarked = true;
+        } else {
+            unmarked = true;
+        }
+        if (sl.d && sl.copied && hipEventSynchronize(sl.copied) != hipSuccess) unmarked = true;
+    });
+    if (e->mix_done) HIPCHK(e, hipEventSynchronize(e->mix_done));
+    if (e->have_last) HIPCHK(e, hipStreamSynchronize(e->last_stream));
+    if (e->stream) HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->copy_stream) HIPCHK(e, hipStreamSynchronize(e->copy_stream));
+    if (unmarked) HIPCHK(e, hipDeviceSynchronize());
+    return OLFX_OK;
+}
+
+// Every instance back to the freshly created state.  The caller has made sure that none of the
+// engine's work is still queued (olfx_create: none was; olfx_reset: wait_engine).
 int init_state(olfx_engine *e) {
-    // all of the engine's earlier work (on any stream) is done: control slots included
-    HIPCHK(e, hipDeviceSynchronize());
     e->n_pending = 0;
     e->each_slot([](olfx_engine::Slot &sl) { sl.used = false; sl.guard = nullptr; });
     HIPCHK(e, hipMemsetAsync(e->d_mem, 0, e->d_bytes, e->stream));
@@ -1193,11 +1224,9 @@ int olfx_destroy(olfx_engine *e) {
                      (unsigned long long)e->tr_calls, e->tr[0] / e->tr_calls, e->tr[1] / e->tr_calls,
                      e->tr[2] / e->tr_calls, e->tr[3] / e->tr_calls, e->tr[4] / e->tr_calls, e->tr[5] / e->tr_calls);
     (void)hipSetDevice(e->device);
-    if (e->stream) (void)hipStreamSynchronize(e->stream);
-    // the engine's work may sit on any caller stream: wait for the device (no per-call marker on
-    // the caller's stream -- each one is a command-processor packet between two blocks' kernels)
-    (void)hipDeviceSynchronize();
-    if (e->mix_done) (void)hipEventSynchronize(e->mix_done);
+    // the engine's own work only (its latest launch stream, its streams, its slots' markers): other
+    // engines and the host application's kernels keep running
+    if (wait_engine(e) != OLFX_OK) (void)hipDeviceSynchronize();
     e->each_slot([](olfx_engine::Slot &sl) {
         if (sl.h) (void)hipHostFree(sl.h);
         if (sl.d) (void)hipFree(sl.d);
@@ -1222,8 +1251,7 @@ int olfx_destroy(olfx_engine *e) {
 int olfx_reset(olfx_engine *e) {
     if (!e) return OLFX_E_ARG;
     HIPCHK(e, hipSetDevice(e->device));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    HIPCHK(e, hipDeviceSynchronize());                          // the last block, on any stream
+    if (const int rc = wait_engine(e)) return rc;               // the last block, engine-scoped
     return init_state(e);
 }
 
@@ -1400,6 +1428,11 @@ int olfx_set_member(olfx_engine *e, uint32_t inst, uint32_t field, float value) 
     if (!is_voice_kind(e->kind)) return olfx_set_params(e, inst, 1, field, 1, &value);
     if (inst >= e->n || field >= e->n_params) return e->fail(OLFX_E_ARG, "olfx_set_member: out of range");
     if (const char *why = bad_value(e, field, value)) return e->fail(OLFX_E_ARG, "olfx_set_member: %s", why);
+    // after the first Update() the derived components follow the members (set_params); a member
+    // written then would take effect at the next block as if Update() had run, which SynthVoice
+    // does not do (SynthVoice.h:66-98): refused instead of silently diverging
+    if (e->configured[inst])
+        return e->fail(OLFX_E_STATE, "olfx_set_member: instance %u is already Update()d (use olfx_set_params)", inst);
     store_param(e, field, inst, value);                 // no Update(): `configured` unchanged
     mark_dirty(e, inst, 1);
     return OLFX_OK;
@@ -1478,6 +1511,8 @@ int olfx_process(olfx_engine *e, const float *in, float *out, uint32_t n_frames,
     } else {
         rc = run_frames(e, in, out, n_frames, s, ev);
     }
+    e->last_stream = s;
+    e->have_last = true;
     // the slot is free again once whatever was queued on `s` (the scatter, the kernels) is done --
     // recorded on the error paths too, so a later block never overwrites a packet still being read
     if (sl) {
@@ -1578,15 +1613,15 @@ int olfx_mix(olfx_engine *e, const float *voice_out, float *bus_out, uint32_t n_
     a.out = bus_out;
     if ((r = launch_mix(a, s)) != hipSuccess) return e->hip_fail(r, "mix launch");
     HIPCHK(e, hipEventRecord(e->mix_done, s));
+    e->last_stream = s;
+    e->have_last = true;
     return OLFX_OK;
 }
 
 int olfx_sync(olfx_engine *e) {
     if (!e) return OLFX_E_ARG;
     HIPCHK(e, hipSetDevice(e->device));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    HIPCHK(e, hipDeviceSynchronize());
-    return OLFX_OK;
+    return wait_engine(e);
 }
 
 void *olfx_stream(const olfx_engine *e) { return e ? (void *)e->stream : nullptr; }

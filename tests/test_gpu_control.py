@@ -289,3 +289,98 @@ def test_tiled_frames_equal_short_calls(cuda):
         assert big.frames_processed == small.frames_processed == frames
         del x, y, big, small
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("copy_bytes", [None, "0"])
+def test_chain_controls_slot_reuse_across_streams(cuda, monkeypatch, copy_bytes):
+    """40 blocks queued without a host wait, a parameter-list change before every block, the
+    caller's stream alternating every block (each new stream ordered after the previous one, as a
+    caller switching streams must): the 16 small zero-copy slots are reused (their group markers,
+    flush_markers on each stream switch).  With OLFX_COPY_BYTES=0 every packet is copied through the
+    two big slots: 40 large packets reuse them.  Bit-exact against the oracle given the same values
+    at the same block boundaries."""
+    import torch
+
+    from ol_dsp_amd.engine import PARAMS
+    if copy_bytes is not None:
+        monkeypatch.setenv("OLFX_COPY_BYTES", copy_bytes)
+    n, blocks = 96, 40
+    rng = np.random.default_rng(320)
+    pc, pp, pd = chorus_params(rng, n), chorus_params(rng, n)[[0, 7]], dt_params(rng, n, 0.05)
+    e = engine("chain", n)
+    e.set_params(0, np.concatenate([pc, pp, pd], 0))
+    c1, c2, d = _chain_oracle(n, pc, pp, pd)
+    names = PARAMS[e.kind]
+    fields = [("chorus_depth", .08, 1), ("verb_decay", .25, .95), ("pitch_shift", 0, 3), ("chorus_rate", .01, 1)]
+    x = fast_noise(n, 256 * blocks, seed=320)
+    xd = torch.from_numpy(x).to(cuda)
+    out = torch.empty((2, 256 * blocks, n), device=cuda)
+    streams = [torch.cuda.Stream(cuda), torch.cuda.Stream(cuda)]
+    torch.cuda.synchronize()
+    prev = torch.cuda.current_stream(cuda)
+    yrs = []
+    for b in range(blocks):
+        fname, lo, hi = fields[b % len(fields)]
+        sel = np.flatnonzero(rng.random(n) < 0.2).astype(np.uint32)
+        vals = rng.uniform(lo, hi, len(sel)).astype(np.float32)
+        e.set_param_list(fname, sel, vals)
+        f = names.index(fname)
+        for i, v in zip(sel, vals):
+            if f < 8:
+                c1.set(int(i), f, float(v))
+            elif f < 10:
+                c2.set(int(i), ("pitch", "window")[f - 8], float(v))
+            else:
+                d.set(int(i), f - 10, float(v))
+        s = streams[b & 1]
+        s.wait_stream(prev)
+        xb = xd[:, 256 * b:256 * (b + 1)].contiguous()
+        ob = out[:, 256 * b:256 * (b + 1)]
+        with torch.cuda.stream(s):
+            yb = e.process(xb, stream=s.cuda_stream)
+            ob.copy_(yb)
+        prev = s
+        yrs.append(d.process(c2.process(c1.process(x[:, 256 * b:256 * (b + 1)]))))
+    torch.cuda.synchronize()
+    y, yr = out.cpu().numpy(), np.concatenate(yrs, 1)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
+def test_reset_waits_for_the_engines_own_stream(cuda):
+    """olfx_reset waits engine-scoped (the stream of its latest block, not the device): blocks
+    queued on a caller stream without a host wait, then reset, then a block on the same stream --
+    bit-identical to a freshly created engine's first block."""
+    import torch
+    n = 128
+    rng = np.random.default_rng(321)
+    p = dt_params(rng, n, 0.02)
+    a, fresh = engine("dattorro", n), engine("dattorro", n)
+    for e in (a, fresh):
+        e.set_params(0, p)
+    s = torch.cuda.Stream(cuda)
+    x = torch.from_numpy(fast_noise(n, 256 * 8, seed=321)).to(cuda)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        for b in range(6):
+            a.process(x[:, 256 * b:256 * (b + 1)].contiguous(), stream=s.cuda_stream)
+    a.reset()
+    a.set_params(0, p)
+    with torch.cuda.stream(s):
+        ya = a.process(x[:, :256].contiguous(), stream=s.cuda_stream)
+    yf = fresh.process(x[:, :256].contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(ya.view(torch.int32), yf.view(torch.int32))
+
+
+def test_set_member_after_update_is_refused(cuda):
+    """olfx_set_member is the member write BEFORE Init/Update (the firmware's setup order); once a
+    voice has been Update()d, its components follow set_params, so a bare member write is refused
+    (OLFX_E_STATE) instead of acting like an Update() the reference would not run."""
+    from ol_dsp_amd import _lib
+    e = engine("voice", 4)
+    lib, h = e.lib, e.handle
+    assert lib.olfx_set_member(h, 1, 0, 500.0) == 0               # before Update: accepted
+    e.update(1, 1)
+    assert lib.olfx_set_member(h, 1, 0, 900.0) == _lib.OLFX_E_STATE    # after: refused, unchanged
+    assert e.get_param(1, "filter_cutoff") == np.float32(500.0)
+    assert lib.olfx_set_member(h, 2, 0, 900.0) == 0               # other voices untouched

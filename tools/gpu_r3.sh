@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# tools/gpu_r3.sh -- GPU-box steps for round 3.  Every GPU step has its own time limit; a crash,
+# tools/gpu_r3.sh -- GPU-box steps (rounds 3-4).  Every GPU step has its own time limit; a crash,
 # abort or timeout ends the script (no retries).
 # Usage (repo root, via gpurun):  bash tools/gpu_r3.sh <mode>...
 #   ctl_tests  the control-path / tiling GPU tests (tests/test_gpu_control.py)
@@ -44,16 +44,17 @@ for m in "$@"; do
     ctl_bench)
       step bench_ctl 600 python bench.py --steps 20 --warmup 5 --workload voice --also voice_events,chain,chain_cc \
           --cpu-seconds 0 ;;
-    ctl_ab)   # control-packet delivery A/B (OLFX_CTL_MODE 1: copy on the stream, 2: zero-copy)
-      for cm in ${CTL_MODES:-0}; do
-        step "pytest_ctl_m$cm" 600 env OLFX_CTL_MODE=$cm python -u -m pytest tests/test_gpu_control.py -m gpu -x -q \
+    ctl_ab)   # control-packet delivery A/B: OLFX_COPY_BYTES=0 copies every packet through the big
+              # slots, the default (64 KiB) reads small packets zero-copy from pinned host slots
+      for cb in ${COPY_BYTES_AB:-0 65536}; do
+        step "pytest_ctl_cb$cb" 600 env OLFX_COPY_BYTES=$cb python -u -m pytest tests/test_gpu_control.py -m gpu -x -q \
             -p no:cacheprovider --timeout 300 --timeout-method thread -k "not tiled"
-        step "bench_ctl_m$cm" 600 env OLFX_CTL_MODE=$cm OLFX_TRACE_CONTROL=1 python bench.py --steps 20 --warmup 5 \
-            --workload voice --also voice_events,chain,chain_cc --cpu-seconds 0
+        step "bench_ctl_cb$cb" 600 env OLFX_COPY_BYTES=$cb OLFX_TRACE_CONTROL=1 python bench.py --steps 20 --warmup 5 \
+            --workload voice --also voice_events,chain,chain_cc --cpu-seconds 0 --no-parity
         for w in voice_events chain_cc; do
-          step "prof_${w}_m$cm" 300 env OLFX_CTL_MODE=$cm rocprofv3 --kernel-trace --stats -d "$out/prof_${w}_m$cm" \
-              -o run --output-format csv -- python3 bench.py --workload $w --also "" --steps 20 --warmup 5 --cpu-seconds 0
-          find "$out/prof_${w}_m$cm" -name '*kernel_trace.csv' -delete
+          step "prof_${w}_cb$cb" 300 env OLFX_COPY_BYTES=$cb rocprofv3 --kernel-trace --stats -d "$out/prof_${w}_cb$cb" \
+              -o run --output-format csv -- python3 bench.py --workload $w --also "" --steps 20 --warmup 5 --cpu-seconds 0 --no-parity
+          find "$out/prof_${w}_cb$cb" -name '*kernel_trace.csv' -delete
         done
       done ;;
     timeline)   # runtime-API + kernel timeline of the control legs (no counters)
