@@ -1,9 +1,76 @@
 // ol_dsp_amd/csrc/chorus.hip -- RNBO stereo chorus and gen~ pitch-shifter kernel on gfx950.
 // The stage (spec, memory shape, line carry, software pipeline) is in chorus_stage_l.h, its
 // helpers in chorus_stage.h.
+#include <cstdlib>
+
+#include "chorus_block.h"
 #include "chorus_stage_l.h"
 
 namespace olfx {
+
+// chorus_block_v13 (chorus_block.h): one persistent workgroup per CU, 16 stereo instances per
+// round, the next round's rings / window / input rows prefetched into registers.  Rounds are
+// assigned XCD-aware: the groups of a workgroup's round sit next to those of the other workgroups
+// of its XCD (workgroups are dispatched to the XCDs round-robin), so the two 16-instance halves
+// of every 128-B input / output row line are fetched by one L2.
+template <bool FULL>
+__global__ __launch_bounds__(cb::kThreads, 1) void chorus_block_v13(ChorusArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    cb::Block<FULL> B(a, lds);
+    const uint32_t ngroups = (a.n + cb::kG - 1) / cb::kG;
+    const uint32_t grid = gridDim.x, b = blockIdx.x;
+    uint32_t g = (grid & 7u) == 0 ? (b & 7u) * (grid >> 3) + (b >> 3) : b;
+    if (g >= ngroups) return;
+    int buf = 0;
+    cb::Pre pre;
+    B.store_scalar(buf, B.load_scalar(g));
+    __syncthreads();
+    B.issue(g, buf, pre);
+    B.fill(buf, pre);
+    __syncthreads();
+    while (true) {
+        const uint32_t gn = g + grid;
+        const bool next = gn < ngroups;
+        uint32_t sv = 0;
+        if (next) sv = B.load_scalar(gn);
+        B.phase1(g, buf);
+        if (next) B.store_scalar(buf ^ 1, sv);
+        __syncthreads();
+        if (next) B.issue(gn, buf ^ 1, pre);        // in flight under phases 2, 3 and the outputs
+        if (FULL) {
+            B.phase2(buf);
+            __syncthreads();
+            B.phase3(g, buf);
+        }
+        B.phasors(g, buf);
+        __syncthreads();
+        B.out(g);
+        if (!next) break;
+        __syncthreads();
+        B.fill(buf ^ 1, pre);
+        buf ^= 1;
+        g = gn;
+        __syncthreads();
+    }
+}
+
+namespace {
+// OLFX_CHORUS_KERNEL=11 forces v11 (A/B diagnostic)
+bool v13_enabled() {
+    static const bool on = [] {
+        const char *v = std::getenv("OLFX_CHORUS_KERNEL");
+        return !(v && std::atoi(v) == 11);
+    }();
+    return on;
+}
+bool v13_geometry(uint32_t n, uint32_t psize, uint32_t csize) {
+    return v13_enabled() && (n & 3u) == 0 && psize == cb::kPsize && csize == cb::kCsize;
+}
+}  // namespace
+
+const char *chorus_kernel_name(uint32_t n, uint32_t psize, uint32_t csize) {
+    return v13_geometry(n, psize, csize) ? "chorus_block_v13" : "chorus_block_v11";
+}
 
 // chorus_block_v11: one wave = 32 instances x 2 channels over the line-carry stage
 // (chorus_stage_l.h); chunks alternate the line set (PAR), so the chunk loop is unrolled by two.
@@ -110,6 +177,24 @@ hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s) {
     const size_t lds_c = lds(T{}, T{}), lds_cl = lds(T{}, F{}), lds_p = lds(F{}, T{}), lds_pl = lds(F{}, F{});
     // cooperative rows need 16-B aligned rows that never straddle the last instance
     const bool coop = (a.n & 3u) == 0 && (a.plane & 3u) == 0 && (((uintptr_t)a.in | (uintptr_t)a.out) & 15u) == 0;
+    if (coop && v13_geometry(a.n, a.psize, a.csize)) {
+        // at most kS frames per launch (the LDS holds one block per instance); longer calls run as
+        // consecutive launches, whose boundaries order each launch's ring stores before the next
+        // one's ring loads
+        const uint32_t ngroups = (a.n + cb::kG - 1) / cb::kG;
+        const uint32_t grid = min(ngroups, a.cus ? a.cus : 256u);
+        const size_t lds = (size_t)cb::kLdsFloats * sizeof(float);
+        for (uint32_t f0 = 0; f0 < a.n_frames; f0 += (uint32_t)cb::kS) {
+            ChorusArgs sub = a;
+            sub.in = a.in + (size_t)f0 * a.n;
+            sub.out = a.out + (size_t)f0 * a.n;
+            sub.n_frames = min((uint32_t)cb::kS, a.n_frames - f0);
+            sub.t0 = a.t0 + f0;
+            if (a.mode == 0) hipLaunchKernelGGL((chorus_block_v13<true>), dim3(grid), dim3(cb::kThreads), lds, s, sub);
+            else hipLaunchKernelGGL((chorus_block_v13<false>), dim3(grid), dim3(cb::kThreads), lds, s, sub);
+        }
+        return hipGetLastError();
+    }
     if (a.mode == 0) {
         if (coop) hipLaunchKernelGGL((chorus_block_v11<true, true>), dim3(blocks), dim3(ch::kThreads), lds_c, s, a);
         else hipLaunchKernelGGL((chorus_block_v11<true, false>), dim3(blocks), dim3(ch::kThreads), lds_cl, s, a);

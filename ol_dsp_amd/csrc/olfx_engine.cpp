@@ -932,6 +932,7 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, uin
         a.psize = e->psize;
         a.csize = e->csize;
         a.mode = mode;
+        a.cus = (uint32_t)e->cus;
         return a;
     };
     switch (e->kind) {
@@ -1667,7 +1668,7 @@ const char *olfx_kernel_name(const olfx_engine *e) {
     switch (e->kind) {
     case OLFX_KIND_DATTORRO: return "dattorro_block_v4";
     case OLFX_KIND_CHORUS:
-    case OLFX_KIND_PITCHSHIFT: return "chorus_block_v11";
+    case OLFX_KIND_PITCHSHIFT: return chorus_kernel_name(e->n, e->psize, e->csize);
     case OLFX_KIND_VOICE: return "voice_block_v5";
     case OLFX_KIND_VOICE_MOOG: return "voice_block_v4";
     case OLFX_KIND_CHAIN: return "chain_block_v5";

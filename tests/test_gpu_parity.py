@@ -409,12 +409,13 @@ def test_chorus_line_carry_stress(cuda, kind):
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
 
-@pytest.mark.parametrize("kind", ["chorus", "pitchshift"])
-def test_chorus_long_run_many_wraps(cuda, kind):
+@pytest.mark.parametrize("kind,n", [("chorus", 70), ("pitchshift", 70), ("chorus", 72), ("pitchshift", 72)])
+def test_chorus_long_run_many_wraps(cuda, kind, n):
     """100,000 frames at the fastest pitch phasors (every instance's two pitch taps wrap 12 times,
     each wrap a generic chunk with direct ring reads), ragged blocks with partial chunks:
-    bit-exact against the oracle."""
-    n, frames = 70, 100000
+    bit-exact against the oracle.  n = 70 runs chorus_block_v11 (rows need n % 4 == 0), n = 72
+    chorus_block_v13 (4.5 groups of 16, launches of at most 256 frames)."""
+    frames = 100000
     rng = np.random.default_rng(93)
     p = chorus_params(rng, n)
     p[0] = rng.uniform(2.5, 3.0, n)                      # pitch phasor Hz
@@ -432,6 +433,38 @@ def test_chorus_long_run_many_wraps(cuda, kind):
             ref.set(i, "pitch", float(p[0, i]))
             ref.set(i, "window", float(p[7, i]))
     y = run_gpu(e, x, [4096] * 24 + [1408, 4, 12, 272], cuda)
+    yr = ref.process(x, threads=8)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
+@pytest.mark.parametrize("kind", ["chorus", "pitchshift"])
+@pytest.mark.parametrize("n", [4, 36, 1028])
+def test_chorus_block_kernel_edges(cuda, kind, n):
+    """chorus_block_v13 (n % 4 == 0): a single partial 16-instance group (4), a partial last group
+    (36, 1028: more groups than one per workgroup for none / some workgroups), calls of 252, 4, 8,
+    260 (two launches), 1000 and 2048 frames (blocks not a multiple of the 4-frame lores~ step
+    pairs, launches split at 256), extreme depth / rate corners (the chorus window bound):
+    bit-exact against the oracle; the engine reports the kernel it runs."""
+    rng = np.random.default_rng(500 + n)
+    p = chorus_params(rng, n)
+    p[5, ::3] = 1.0                                        # depth max
+    p[6, ::2] = 1.0                                        # rate max
+    blocks = [252, 4, 8, 260, 1000, 2048]
+    x = fast_noise(n, sum(blocks), seed=n)
+    e = engine(kind, n)
+    ref = O.Chorus(n, mode=0 if kind == "chorus" else 1)
+    if kind == "chorus":
+        e.set_params(0, p)
+        for i in range(n):
+            for f in range(8):
+                ref.set(i, f, float(p[f, i]))
+    else:
+        e.set_params(0, p[[0, 7]])
+        for i in range(n):
+            ref.set(i, "pitch", float(p[0, i]))
+            ref.set(i, "window", float(p[7, i]))
+    assert e.kernel_name == "chorus_block_v13"
+    y = run_gpu(e, x, blocks, cuda)
     yr = ref.process(x, threads=8)
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
