@@ -32,6 +32,11 @@
 #pragma once
 #include "chorus_stage_l.h"
 
+// diagnostic builds (wrong results; tools/build_variant.sh): bit 0 skips lores~, bit 1 the chorus tap
+#ifndef OLFX_CB_DIAG
+#define OLFX_CB_DIAG 0
+#endif
+
 namespace olfx {
 namespace cb {
 
@@ -266,6 +271,7 @@ struct Block {
 
     // ---- phase 2: the chorus tap, lanes = frames; w over the dead pitch-window history ----
     __device__ __forceinline__ void phase2(int buf) {
+        if (OLFX_CB_DIAG & 2) return;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint32_t j = 2u * wave + (uint32_t)h;
@@ -295,7 +301,7 @@ struct Block {
 
     // ---- phase 3: lores~ and the mix, one lane per (instance, channel): wave 0, lanes 0..31 ----
     __device__ __forceinline__ void phase3(uint32_t g, int buf) {
-        if (wave != 0 || lane >= 2u * kG) return;
+        if (wave != 0 || lane >= 2u * kG || (OLFX_CB_DIAG & 1)) return;
         const uint32_t j = lane >> 1, c = lane & 1u, i = g * kG + j;
         const float *s = sc(buf, j);
         const float b0 = s[CHC_B0], b1 = s[CHC_B1], b2 = s[CHC_B2], a1 = s[CHC_A1], a2 = s[CHC_A2];

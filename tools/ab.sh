@@ -10,7 +10,7 @@ for rep in 1 2; do
   for lib in "$@"; do
     [ "$lib" = main ] && lib=ol_dsp_amd/libolfx.so
     for w in $wls; do
-      OLFX_LIB=$PWD/$lib timeout -k 10 300 python bench.py --workload "$w" --steps 60 --warmup 5 --cpu-seconds 0 \
+      OLFX_LIB=$PWD/$lib timeout -k 10 300 python bench.py --workload "$w" --also "" --steps 60 --warmup 5 --cpu-seconds 0 --no-parity --full-json "" \
           > gpurun_out/ab.log 2>&1
       rc=$?; [ $rc -ne 0 ] && { tail -n 20 gpurun_out/ab.log; exit $rc; }
       python - "$w" "$lib" <<'PY'

@@ -1,0 +1,60 @@
+#!/usr/bin/env bash
+# tools/gpu_r4.sh -- GPU-box steps for round 4.  Every GPU step has its own time limit; a crash,
+# abort or timeout ends the script (no retries).
+# Usage (repo root, via gpurun):  bash tools/gpu_r4.sh <mode>...
+#   t:<pytest -k expr>   GPU tests matching the expression
+#   tests                every GPU test, then smoke()
+#   b:<workload>         one workload's bench line (20 steps, no CPU baseline)
+#   p:<workload>         rocprofv3 kernel stats of that bench line (-> gpurun_out/prof_<w>)
+#   tr:<workload>        HBM traffic passes (tools/traffic_r2.sh)
+#   bench                the driver's default line
+#   ab:<workload>        A/B: the workload under OLFX_CHORUS_KERNEL=11 and the default, twice each
+set -u
+out=gpurun_out
+mkdir -p "$out"
+export PYTHONUNBUFFERED=1
+export TMPDIR=/tmp
+
+step() {   # step <name> <seconds> <cmd...>
+    local name=$1 secs=$2; shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 "$secs" "$@" > "$out/$name.log" 2>&1
+    local rc=$?
+    echo "   rc=$rc"; tail -n 3 "$out/$name.log"
+    if [ $rc -ne 0 ]; then echo "!! $name failed (rc=$rc): stopping"; exit $rc; fi
+}
+
+for m in "$@"; do
+  case $m in
+    t:*)
+      k=${m#t:}
+      step "pytest_$(echo "$k" | tr -c 'a-zA-Z0-9_' '_')" 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider \
+          --timeout 120 --timeout-method thread -k "$k" ;;
+    tests)
+      step pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
+      step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    b:*)
+      w=${m#b:}
+      step "bench_$w" 300 python bench.py --workload "$w" --also "" --steps 20 --warmup 5 --cpu-seconds 0 --full-json "" ;;
+    p:*)
+      w=${m#p:}
+      step "prof_$w" 300 rocprofv3 --kernel-trace --stats -d "$out/prof_$w" -o run --output-format csv -- \
+          python3 bench.py --workload "$w" --also "" --steps 20 --warmup 5 --cpu-seconds 0 --no-parity --full-json ""
+      find "$out/prof_$w" -name '*kernel_trace.csv' -delete ;;
+    tr:*)
+      w=${m#tr:}
+      step "traffic_$w" 600 bash tools/traffic_r2.sh "$w" ;;
+    ab:*)
+      w=${m#ab:}
+      for r in 1 2; do
+        step "ab_${w}_v11_$r" 300 env OLFX_CHORUS_KERNEL=11 python bench.py --workload "$w" --also "" --steps 50 --warmup 5 \
+            --cpu-seconds 0 --no-parity --full-json ""
+        step "ab_${w}_new_$r" 300 python bench.py --workload "$w" --also "" --steps 50 --warmup 5 --cpu-seconds 0 \
+            --no-parity --full-json ""
+      done ;;
+    bench)
+      step bench_default 900 python bench.py --steps 20 --warmup 5 ;;
+    *) echo "unknown mode $m"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
