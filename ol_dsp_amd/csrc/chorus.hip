@@ -13,8 +13,25 @@ namespace olfx {
 // assigned XCD-aware: the groups of a workgroup's round sit next to those of the other workgroups
 // of its XCD (workgroups are dispatched to the XCDs round-robin), so the two 16-instance halves
 // of every 128-B input / output row line are fetched by one L2.
+#ifndef OLFX_CB_STAMP
+#define OLFX_CB_STAMP 0
+#endif
+#if OLFX_CB_STAMP
+// diagnostic: workgroup 0's phase boundaries (s_memtime), read back by olfx_debug_stamps
+__device__ uint64_t g_cb_stamps[512];
+#define CB_STAMP(k)                                                                        \
+    do {                                                                                   \
+        if (blockIdx.x == 0 && threadIdx.x == 0 && ns < 500u) g_cb_stamps[ns] = __builtin_amdgcn_s_memtime(); \
+        ++ns;                                                                              \
+    } while (0)
+#else
+#define CB_STAMP(k) do { } while (0)
+#endif
+
 template <bool FULL>
 __global__ __launch_bounds__(cb::kThreads, 1) void chorus_block_v13(ChorusArgs a) {
+    uint32_t ns = 0;
+    (void)ns;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     cb::Block<FULL> B(a, lds);
     const uint32_t ngroups = (a.n + cb::kG - 1) / cb::kG;
@@ -23,12 +40,14 @@ __global__ __launch_bounds__(cb::kThreads, 1) void chorus_block_v13(ChorusArgs a
     if (g >= ngroups) return;
     int buf = 0;
     cb::Pre pre;
+    CB_STAMP(0);
     B.store_scalar(buf, B.load_scalar(g));
     __syncthreads();
     B.issue(g, buf, pre);
     B.fill(buf, pre);
     __syncthreads();
     while (true) {
+        CB_STAMP(1);
         const uint32_t gn = g + grid;
         const bool next = gn < ngroups;
         uint32_t sv = 0;
@@ -36,21 +55,27 @@ __global__ __launch_bounds__(cb::kThreads, 1) void chorus_block_v13(ChorusArgs a
         B.phase1(g, buf);
         if (next) B.store_scalar(buf ^ 1, sv);
         __syncthreads();
+        CB_STAMP(2);
         if (next) B.issue(gn, buf ^ 1, pre);        // in flight under phases 2, 3 and the outputs
+        CB_STAMP(3);
         if (FULL) {
             B.phase2(buf);
             __syncthreads();
+            CB_STAMP(4);
             B.phase3(g, buf);
         }
         B.phasors(g, buf);
         __syncthreads();
+        CB_STAMP(5);
         B.out(g);
         if (!next) break;
         __syncthreads();
+        CB_STAMP(6);
         B.fill(buf ^ 1, pre);
         buf ^= 1;
         g = gn;
         __syncthreads();
+        CB_STAMP(7);
     }
 }
 
@@ -67,6 +92,12 @@ bool v13_geometry(uint32_t n, uint32_t psize, uint32_t csize) {
     return v13_enabled() && (n & 3u) == 0 && psize == cb::kPsize && csize == cb::kCsize;
 }
 }  // namespace
+
+#if OLFX_CB_STAMP
+extern "C" __attribute__((visibility("default"))) int olfx_debug_stamps(uint64_t *dst, uint32_t n) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_cb_stamps), (size_t)n * 8) == hipSuccess ? 0 : -1;
+}
+#endif
 
 const char *chorus_kernel_name(uint32_t n, uint32_t psize, uint32_t csize) {
     return v13_geometry(n, psize, csize) ? "chorus_block_v13" : "chorus_block_v11";

@@ -32,7 +32,7 @@ typedef struct {
 } ch64_t;
 
 struct oracle_chorus64 {
-    int n, mode, quantize;
+    int n, mode, quantize, f32;
     double sr;
     uint32_t psize, csize;
     uint64_t w;
@@ -74,10 +74,10 @@ static void derive64(const double *p, double sr, int quantize, ch64_t *c)
 
 oracle_chorus64 *oracle_chorus64_create(int n_inst, double sample_rate, int mode)
 {
-    if (n_inst <= 0 || (mode & ~3)) return NULL;
+    if (n_inst <= 0 || (mode & ~0x1FF)) return NULL;
     oracle_chorus64 *o = (oracle_chorus64 *)calloc(1, sizeof(*o));
     if (!o) return NULL;
-    o->n = n_inst; o->mode = mode & 1; o->quantize = mode >> 1; o->sr = sample_rate;
+    o->n = n_inst; o->mode = mode & 1; o->quantize = (mode >> 1) & 1; o->f32 = mode >> 2; o->sr = sample_rate;
     o->psize = pow2ge64((uint32_t)ceil(10.0 * sample_rate / 1000.0) + 2);
     o->csize = pow2ge64(2u * (uint32_t)ceil(12.0 * sample_rate / 1000.0) + 2);
     const size_t per = 2u * (o->psize + o->csize);
@@ -112,16 +112,42 @@ int oracle_chorus64_set(oracle_chorus64 *o, int inst, int field, double value)
     return 0;
 }
 
-static double read64(const double *ring, uint32_t mask, uint64_t w, double d, double dmin)
-{
-    d = d < dmin ? dmin : d;
-    const uint64_t di = (uint64_t)d;
-    const double fr = d - (double)di;
-    const double x0 = ring[(w - di) & mask], x1 = ring[(w - di - 1u) & mask];
-    return x0 + fr * (x1 - x0);
-}
-
 static double wrap1(double x) { return x - floor(x); }
+
+/* Stage-by-stage decomposition of the fp32 spec's deviation (tests/test_oracle.py
+   test_chorus_deviation_by_stage): mode bits 2.. select stages computed as the fp32 spec computes
+   them (chorus_ref.c chorus_frame), everything else in double:
+     F32_PDELAY   pitch tap delays: 24-bit phase (unit24), d = p W in fp32, fp32 split
+     F32_PGAIN    crossfade gains: the fp32 sin / cos polynomials (oracle_win_gains)
+     F32_PINTERP  pitch taps' interpolation and the crossfade sum in fp32
+     F32_CDELAY   chorus delay: cos2pi polynomial of the 24-bit phase, lfo D + D in fp32
+     F32_CINTERP  chorus tap interpolation in fp32
+     F32_LORES    lores~ coefficients and state in fp32
+     F32_MIX      x dry + lp mix in fp32 */
+enum { F32_PDELAY = 1, F32_PGAIN = 2, F32_PINTERP = 4, F32_CDELAY = 8, F32_CINTERP = 16, F32_LORES = 32, F32_MIX = 64 };
+
+static double unit24d(double ph) { return floor(ph * 16777216.0) / 16777216.0; }
+
+static double readf(const double *ring, uint32_t mask, uint64_t w, double d, double dmin, int f32d, int f32i)
+{
+    if (!f32d) {
+        d = d < dmin ? dmin : d;
+        const uint64_t di = (uint64_t)d;
+        const double fr = d - (double)di;
+        const double x0 = ring[(w - di) & mask], x1 = ring[(w - di - 1u) & mask];
+        if (!f32i) return x0 + fr * (x1 - x0);
+        const float x0f = (float)x0, x1f = (float)x1, frf = (float)fr;
+        return (double)(x0f + frf * (x1f - x0f));
+    }
+    float df = (float)d;
+    df = df < (float)dmin ? (float)dmin : df;
+    const uint32_t di = (uint32_t)df;
+    const float fr = df - (float)di;
+    const double x0 = ring[(w - di) & mask], x1 = ring[(w - di - 1u) & mask];
+    if (!f32i) return x0 + (double)fr * (x1 - x0);
+    const float x0f = (float)x0, x1f = (float)x1;
+    return (double)(x0f + fr * (x1f - x0f));
+}
 
 /* in: float [2][n_frames][n] (the same inputs as the fp32 oracle); out: double [2][n_frames][n] */
 int oracle_chorus64_process(oracle_chorus64 *o, const float *in, double *out, int n_frames)
@@ -134,25 +160,53 @@ int oracle_chorus64_process(oracle_chorus64 *o, const float *in, double *out, in
         ch64_t *s = &o->v[i];
         for (int f = 0; f < n_frames; f++) {
             const uint64_t w = o->w + (uint64_t)f;
-            const double lfo = cos(2.0 * pi * wrap1(s->lfo_ph + s->lfo_off));
+            const int F = o->f32;
+            const double lph = wrap1(s->lfo_ph + s->lfo_off);
+            double dch;
+            if (F & F32_CDELAY) {
+                const float lfo = oracle_cos2pi((float)unit24d(lph));
+                dch = (double)(lfo * (float)s->D + (float)s->D);
+            } else {
+                dch = cos(2.0 * pi * lph) * s->D + s->D;
+            }
             s->lfo_ph = wrap1(s->lfo_ph + s->lfo_inc);
-            const double dch = lfo * s->D + s->D;
             const double p0 = s->ps_ph, p1 = wrap1(s->ps_ph + 0.5);
             s->ps_ph = wrap1(s->ps_ph + s->ps_inc);
-            const double g0 = cos((p0 - 0.5) * pi), g1 = cos((p1 - 0.5) * pi);
+            double g0 = cos((p0 - 0.5) * pi), g1 = cos((p1 - 0.5) * pi);
+            if (F & F32_PGAIN) {
+                float a, b;
+                oracle_win_gains((float)unit24d(p0), &a, &b);
+                g0 = a; g1 = b;
+            }
+            double d0 = p0 * s->W, d1 = p1 * s->W;
+            if (F & F32_PDELAY) {
+                d0 = (double)((float)unit24d(p0) * (float)s->W);
+                d1 = (double)((float)unit24d(p1) * (float)s->W);
+            }
             for (int c = 0; c < 2; c++) {
                 const double x = in[c * plane + (long)f * n + i];
-                const double ps = read64(s->pring[c], pmask, w, p1 * s->W, 1.0) * g1 +
-                                  read64(s->pring[c], pmask, w, p0 * s->W, 1.0) * g0;
+                const double t1 = readf(s->pring[c], pmask, w, d1, 1.0, F & F32_PDELAY, F & F32_PINTERP);
+                const double t0 = readf(s->pring[c], pmask, w, d0, 1.0, F & F32_PDELAY, F & F32_PINTERP);
+                const double ps = (F & F32_PINTERP) ? (double)((float)t1 * (float)g1 + (float)t0 * (float)g0)
+                                                    : t1 * g1 + t0 * g0;
                 s->pring[c][w & pmask] = x;
                 double y = ps;
                 if (o->mode == 0) {
                     s->cring[c][w & cmask] = ps;
-                    const double wet = read64(s->cring[c], cmask, w, dch, 0.0);
-                    const double lp = s->b0 * wet + s->z1[c];
-                    s->z1[c] = (s->b1 * wet - s->a1 * lp) + s->z2[c];
-                    s->z2[c] = s->b2 * wet - s->a2 * lp;
-                    y = x * (1.0 - s->mix) + lp * s->mix;
+                    const double wet = readf(s->cring[c], cmask, w, dch, 0.0, F & F32_CDELAY, F & F32_CINTERP);
+                    double lp;
+                    if (F & F32_LORES) {
+                        const float wf = (float)wet, lpf = (float)s->b0 * wf + (float)s->z1[c];
+                        s->z1[c] = (double)(((float)s->b1 * wf - (float)s->a1 * lpf) + (float)s->z2[c]);
+                        s->z2[c] = (double)((float)s->b2 * wf - (float)s->a2 * lpf);
+                        lp = lpf;
+                    } else {
+                        lp = s->b0 * wet + s->z1[c];
+                        s->z1[c] = (s->b1 * wet - s->a1 * lp) + s->z2[c];
+                        s->z2[c] = s->b2 * wet - s->a2 * lp;
+                    }
+                    y = (F & F32_MIX) ? (double)((float)x * (1.0f - (float)s->mix) + (float)lp * (float)s->mix)
+                                      : x * (1.0 - s->mix) + lp * s->mix;
                 }
                 out[c * plane + (long)f * n + i] = y;
             }
