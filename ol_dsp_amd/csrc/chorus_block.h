@@ -25,9 +25,10 @@
 // group; groups 2k and 2k+1 (one 128-B line) run at the same time on the same XCD, so the line's
 // second half is an L2 hit.
 //
-// Frame arithmetic is v11's, operation for operation (so the output is bit-identical to the oracle
-// oracle/chorus_ref.c chorus_frame and to v11): phasor -> unit24 -> (ph >> 8) (W 2^-24) delays,
-// med3 clamps, float splits, x0 + fr (x1 - x0), psv = tB gB + tA gA, wet, the biquad, x dry + lp mix.
+// Frame arithmetic is the spec's, operation for operation (bit-identical to the oracle
+// oracle/chorus_ref.c chorus_frame and to v11): the precise tap delays of spec v2 (pitch_split,
+// chorus_split: olfx_internal.h), x0 + fr (x1 - x0), psv = tB gB + tA gA, wet, the biquad,
+// x dry + lp mix.
 // Geometry: psize 512 and csize 2048 (sample rates ~25.6 .. 51 kHz); others use v11.
 #pragma once
 #include "chorus_stage_l.h"
@@ -53,7 +54,7 @@ constexpr int kCParts = 144;                   // float4 (2 positions) loads per
 constexpr int kScW = 32;                       // scalar words per instance
 // scalar words: coefficient and state fields as on the device ([CHC_N] then [CHS_N]), then the
 // window geometry of the round
-constexpr int kScState = CHC_N;                // 15..22: CHS_* words
+constexpr int kScState = CHC_N;                // 17..24: CHS_* words
 constexpr int kScCoff = kScState + CHS_N;      // t0 - (first chorus window position)
 constexpr int kScCw = kScCoff + 1;             // chorus window width (positions)
 constexpr int kLdsFloats = kG * kPStride + kG * kCStride + 2 * kG * kScW;
@@ -64,8 +65,9 @@ static_assert(kLdsFloats * 4 <= 160 * 1024, "LDS budget");
 constexpr int kPParts = kG * (int)kPsize / 2 / kThreads;       // 8: float4 pieces of the pitch rings
 constexpr int kXParts = kG * 2 * kS / 4 / kThreads;           // 4: float4 pieces of the input rows
 constexpr int kCLoads = (kG * kCParts + kThreads - 1) / kThreads;   // 5
-constexpr int kScLoads = kG * (CHC_N + CHS_N);                // 368 lanes load one scalar word each
+constexpr int kScLoads = kG * (CHC_N + CHS_N);                // 400 lanes load one scalar word each
 static_assert(kScLoads <= kThreads, "scalar loads");
+static_assert(kScCw < kScW, "window geometry slots");
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void st2(ch::Rsrc r, uint32_t off, float2 v) {
@@ -93,7 +95,6 @@ struct Block {
     uint32_t tid, wave, lane;
     uint32_t n, S, t0;
     Rsrc rP, rC, rIn, rOut;
-    float pmax, cmax;
 
     __device__ __forceinline__ Block(const ChorusArgs &a_, float *lds) : a(a_) {
         P = lds;
@@ -109,15 +110,13 @@ struct Block {
         rC = rsrc(a.chorus_ring, (uint64_t)n * 2 * kCsize * 4);
         rIn = rsrc(a.in, (a.plane + (uint64_t)S * n) * 4);
         rOut = rsrc(a.out, (a.plane + (uint64_t)S * n) * 4);
-        pmax = (float)(kPsize - 2u);
-        cmax = (float)(kCsize - 2u);
     }
 
     __device__ __forceinline__ float *sc(int buf, uint32_t j) { return Sc + (buf * kG + j) * kScW; }
     __device__ __forceinline__ static uint64_t w64(uint32_t hi, uint32_t lo) { return ((uint64_t)hi << 32) | lo; }
     __device__ __forceinline__ static uint32_t u(float v) { return __float_as_uint(v); }
 
-    // ---- scalars of group g: lane tid < 368 loads word (tid % 23) of instance (tid / 23) ----
+    // ---- scalars of group g: lane tid < 400 loads word (tid % 25) of instance (tid / 25) ----
     __device__ __forceinline__ uint32_t load_scalar(uint32_t g) const {
         if (tid >= (uint32_t)kScLoads) return 0u;
         const uint32_t j = tid / (uint32_t)(CHC_N + CHS_N), w = tid % (uint32_t)(CHC_N + CHS_N);
@@ -135,15 +134,16 @@ struct Block {
     // between the delay stays within [min, max] of them up to the LFO's curvature over the block
     // (D (1 - cos(pi f S / sr)) < 0.04 samples for every legal depth and rate at sr >= 25.6 kHz),
     // so floor(min - .25) .. floor(max + .25) bounds every frame's floor delay; width <= S + 12.
+    __device__ __forceinline__ static double f64(float hi, float lo) { return __longlong_as_double((long long)w64(u(hi), u(lo))); }
     __device__ __forceinline__ void window(const float *s, int &coff, int &cw) const {
         const uint64_t lacc = w64(u(s[kScState + CHS_LFO_ACC]), u(s[kScState + CHS_LFO_LO]));
         const uint64_t linc = w64(u(s[CHC_LFO_INC]), u(s[CHC_LFO_INC_LO]));
         const uint64_t loff = w64(u(s[CHC_LFO_OFF]), u(s[CHC_LFO_OFF_LO]));
-        const float D = s[CHC_DEPTH];
-        const float e0 = cos2pi(ch::unit24h(lacc + loff)) * D + D;
-        const float e1 = cos2pi(ch::unit24h(lacc + (uint64_t)(S - 1u) * linc + loff)) * D + D;
-        const int dhi = ch::floor_delay(fmaxf(e0, e1) + 0.25f, 0.0f, cmax);
-        const int dlo = ch::floor_delay(fminf(e0, e1) - 0.25f, 0.0f, cmax);
+        const double D = f64(s[CHC_DEPTH], s[CHC_DEPTH_LO]);
+        const double e0 = chorus_delay(lacc + loff, D, (double)(kCsize - 2u));
+        const double e1 = chorus_delay(lacc + (uint64_t)(S - 1u) * linc + loff, D, (double)(kCsize - 2u));
+        const int dhi = min((int)(fmax(e0, e1) + 0.25), (int)kCsize - 2);
+        const int dlo = (int)fmax(fmin(e0, e1) - 0.25, 0.0);
         coff = (dhi + 2) & ~1;                     // t0 - first position (t0 is 4-aligned: even start)
         cw = coff + (int)S - dlo;                  // positions first .. t0 + S - 1 - dlo
     }
@@ -228,7 +228,7 @@ struct Block {
             const float *s = sc(buf, j);
             const uint64_t pacc = w64(u(s[kScState + CHS_PS_ACC]), u(s[kScState + CHS_PS_LO]));
             const uint64_t pinc = w64(u(s[CHC_PS_INC]), u(s[CHC_PS_INC_LO]));
-            const float Ws = s[CHC_WINDOW] * 5.9604644775390625e-8f;
+            const uint32_t wi = u(s[CHC_WINDOW]), wf = u(s[CHC_WINDOW_LO]);
             const float *pw = P + j * kPStride;
             float *cwin = C + j * kCStride;
             const int coff = FULL ? __float_as_int(s[kScCoff]) : 0;
@@ -241,12 +241,12 @@ struct Block {
                 const uint32_t ph = ch::hi32(pacc + (uint64_t)k * pinc);
                 float gA, gB;
                 win_gains(ch::unit24(ph), gA, gB);
-                int di;
+                uint32_t diA, diB;
                 float fA, fB;
-                ch::split_delay3((float)(ph >> 8) * Ws, 1.0f, pmax, di, fA);
-                const float *qA = pw + 2 * (kPOld + (int)k - di);
-                ch::split_delay3((float)((ph + 0x80000000u) >> 8) * Ws, 1.0f, pmax, di, fB);
-                const float *qB = pw + 2 * (kPOld + (int)k - di);
+                pitch_split(ph, wi, wf, kPsize - 2u, diA, fA);
+                pitch_split(ph + 0x80000000u, wi, wf, kPsize - 2u, diB, fB);   // p1 = (p0 + 1/2) % 1
+                const float *qA = pw + 2 * (kPOld + (int)k - (int)diA);
+                const float *qB = pw + 2 * (kPOld + (int)k - (int)diB);
                 const float2 a0 = *(const float2 *)qA, a1 = *(const float2 *)(qA - 2);
                 const float2 b0 = *(const float2 *)qB, b1 = *(const float2 *)(qB - 2);
                 const float tAL = ch::lerp_pair(a0.x, a1.x, fA), tAR = ch::lerp_pair(a0.y, a1.y, fA);
@@ -279,20 +279,19 @@ struct Block {
             const uint64_t lacc = w64(u(s[kScState + CHS_LFO_ACC]), u(s[kScState + CHS_LFO_LO]));
             const uint64_t linc = w64(u(s[CHC_LFO_INC]), u(s[CHC_LFO_INC_LO]));
             const uint64_t loff = w64(u(s[CHC_LFO_OFF]), u(s[CHC_LFO_OFF_LO]));
-            const float D = s[CHC_DEPTH];
+            const double D = f64(s[CHC_DEPTH], s[CHC_DEPTH_LO]);
             const int coff = __float_as_int(s[kScCoff]);
             const float *cwin = C + j * kCStride;
             float *wv = P + j * kPStride;
 #pragma unroll
             for (int m = 0; m < kS / 64; ++m) {
                 const uint32_t k = lane + 64u * (uint32_t)m;
-                const float lfo = cos2pi(ch::unit24h(lacc + (uint64_t)k * linc + loff));
-                int di;
+                uint32_t di;
                 float fr;
-                ch::split_delay3(lfo * D + D, 0.0f, cmax, di, fr);
+                chorus_split(lacc + (uint64_t)k * linc + loff, D, (double)(kCsize - 2u), di, fr);
                 // (a slot outside [1, kCWin - 2] would mean the window bound failed: clamped, never
                 // out of the instance's region)
-                const int slot = min(max(coff + (int)k - di, 1), kCWin - 2);
+                const int slot = min(max(coff + (int)k - (int)di, 1), kCWin - 2);
                 const float2 c0 = *(const float2 *)(cwin + 2 * slot), c1 = *(const float2 *)(cwin + 2 * slot - 2);
                 *(float2 *)(wv + 2u * k) = make_float2(ch::lerp_pair(c0.x, c1.x, fr), ch::lerp_pair(c0.y, c1.y, fr));
             }

@@ -70,18 +70,6 @@ __device__ __forceinline__ float unit24(uint32_t acc) {
     return (float)(acc >> 8) * 5.9604644775390625e-8f;   // exact: 24-bit fraction in [0,1)
 }
 
-// floor of a clamped fractional delay: di, fr with d in [dmin, dmax]
-__device__ __forceinline__ void split_delay(float d, float dmin, float dmax, int &di, float &fr) {
-    d = fminf(fmaxf(d, dmin), dmax);
-    const uint32_t u = (uint32_t)d;
-    di = (int)u;
-    fr = d - (float)u;
-}
-
-__device__ __forceinline__ int floor_delay(float d, float dmin, float dmax) {
-    return (int)(uint32_t)fminf(fmaxf(d, dmin), dmax);
-}
-
 __device__ __forceinline__ float lerp_pair(float x0, float x1, float fr) { return x0 + fr * (x1 - x0); }
 
 // a value of lane 2j (EVEN) or 2j+1 (odd) to both lanes of the pair: DPP quad_perm [0,0,2,2] / [1,1,3,3]
@@ -93,15 +81,6 @@ __device__ __forceinline__ float pair_odd(float v) {
 }
 __device__ __forceinline__ int pair_even_i(int v) { return __builtin_amdgcn_mov_dpp(v, 0xA0, 0xF, 0xF, false); }
 __device__ __forceinline__ int pair_odd_i(int v) { return __builtin_amdgcn_mov_dpp(v, 0xF5, 0xF, 0xF, false); }
-// split_delay with the clamp as one v_med3 (identical to fminf(fmaxf()) for non-NaN delays,
-// and delays here are phasor arithmetic, never NaN)
-__device__ __forceinline__ void split_delay3(float d, float dmin, float dmax, int &di, float &fr) {
-    d = __builtin_amdgcn_fmed3f(d, dmin, dmax);
-    const uint32_t u = (uint32_t)d;
-    di = (int)u;
-    fr = d - (float)u;
-}
-
 
 }  // namespace ch
 }  // namespace olfx

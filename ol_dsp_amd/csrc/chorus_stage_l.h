@@ -61,22 +61,27 @@ constexpr uint64_t kHalfCycle = 0x8000000000000000ull;
 
 template <int kWin>
 __device__ __forceinline__ PlanL plan_chunk_l(uint64_t lfo_acc, uint64_t lfo_inc, uint64_t lfo_off, uint64_t ps_acc,
-                                              uint64_t ps_inc, int C, float D, float W, float pmax, float cmax,
-                                              bool full) {
+                                              uint64_t ps_inc, int C, double D, uint32_t wi, uint32_t wf,
+                                              uint32_t pmaxu, double cmaxd, bool full) {
     PlanL p;
     const uint32_t last = (uint32_t)(C - 1);
-    // pitch taps: the floor delay is non-decreasing over the chunk unless the phasor wraps
+    // pitch taps: the floor delay is non-decreasing over the chunk unless the phasor wraps (the
+    // delays are the frames' own: pitch_split, spec v2)
+    uint32_t d0, d1;
+    float fr;
     {
         const uint64_t a0 = ps_acc, a1 = ps_acc + last * ps_inc;
-        const int d0 = floor_delay(unit24h(a0) * W, 1.0f, pmax), d1 = floor_delay(unit24h(a1) * W, 1.0f, pmax);
-        const int lo = -d1 - 1, hi = (int)last - d0;
+        pitch_split(hi32(a0), wi, wf, pmaxu, d0, fr);
+        pitch_split(hi32(a1), wi, wf, pmaxu, d1, fr);
+        const int lo = -(int)d1 - 1, hi = (int)last - (int)d0;
         p.sA = lo & ~3;
         p.okA = a1 >= a0 && hi - p.sA < kWin;
     }
     {
         const uint64_t a0 = ps_acc + kHalfCycle, a1 = a0 + last * ps_inc;
-        const int d0 = floor_delay(unit24h(a0) * W, 1.0f, pmax), d1 = floor_delay(unit24h(a1) * W, 1.0f, pmax);
-        const int lo = -d1 - 1, hi = (int)last - d0;
+        pitch_split(hi32(a0), wi, wf, pmaxu, d0, fr);
+        pitch_split(hi32(a1), wi, wf, pmaxu, d1, fr);
+        const int lo = -(int)d1 - 1, hi = (int)last - (int)d0;
         p.sB = lo & ~3;
         p.okB = a1 >= a0 && hi - p.sB < kWin;
     }
@@ -86,10 +91,10 @@ __device__ __forceinline__ PlanL plan_chunk_l(uint64_t lfo_acc, uint64_t lfo_inc
     // frame's floor delay, and those two differ by at most one (|d'| <= 0.038 frame/frame)
     p.sC = 0; p.hiC = 0;
     if (full) {
-        const float e0 = cos2pi(unit24h(lfo_acc + lfo_off)) * D + D;
-        const float e1 = cos2pi(unit24h(lfo_acc + last * lfo_inc + lfo_off)) * D + D;
-        const int dhi = floor_delay(fmaxf(e0, e1) + 0.01f, 0.0f, cmax);
-        const int dlo = floor_delay(fminf(e0, e1) - 0.01f, 0.0f, cmax);
+        const double e0 = chorus_delay(lfo_acc + lfo_off, D, cmaxd);
+        const double e1 = chorus_delay(lfo_acc + last * lfo_inc + lfo_off, D, cmaxd);
+        const int dhi = min((int)(fmax(e0, e1) + 0.01), (int)cmaxd);
+        const int dlo = (int)fmax(fmin(e0, e1) - 0.01, 0.0);
         p.sC = (-dhi - 1) & ~3;
         p.hiC = (int)last - dlo;
     }
@@ -129,11 +134,14 @@ struct ChStageL {
     uint32_t lane, j, ch, inst0, n, i;
     bool valid;
     uint64_t lfo_inc, lfo_off, ps_inc;
-    float D, W, b0, b1, b2, a1, a2, mix, dry;
+    double D;                 // chorus depth in samples (spec v2: the delay is formed in double)
+    uint32_t wi, wf;          // pitch window W in 32.32 fixed point
+    float b0, b1, b2, a1, a2, mix, dry;
     uint64_t lfo_acc, ps_acc;
     float z1, z2;
     uint32_t pmask, cmask, pshift, cshift;   // ring sizes are powers of two: instance offset = i << shift
-    float pmax, cmax;
+    uint32_t pmaxu;                          // delay clamps: psize - 2, csize - 2
+    double cmaxd;
     Rsrc rP, rC;
     float *region;
     float4 ln[3][2][4];       // [tap][line set][part]: piece lane/8 of a line of instance part*8 + (lane & 7)
@@ -153,8 +161,9 @@ struct ChStageL {
         lfo_inc = word64(a.coef[CHC_LFO_INC * n + i], a.coef[CHC_LFO_INC_LO * n + i]);
         lfo_off = word64(a.coef[CHC_LFO_OFF * n + i], a.coef[CHC_LFO_OFF_LO * n + i]);
         ps_inc = word64(a.coef[CHC_PS_INC * n + i], a.coef[CHC_PS_INC_LO * n + i]);
-        D = __uint_as_float(a.coef[CHC_DEPTH * n + i]);
-        W = __uint_as_float(a.coef[CHC_WINDOW * n + i]);
+        D = __longlong_as_double((long long)word64(a.coef[CHC_DEPTH * n + i], a.coef[CHC_DEPTH_LO * n + i]));
+        wi = a.coef[CHC_WINDOW * n + i];
+        wf = a.coef[CHC_WINDOW_LO * n + i];
         b0 = __uint_as_float(a.coef[CHC_B0 * n + i]);
         b1 = __uint_as_float(a.coef[CHC_B1 * n + i]);
         b2 = __uint_as_float(a.coef[CHC_B2 * n + i]);
@@ -167,7 +176,7 @@ struct ChStageL {
         z1 = __uint_as_float(a.state[(ch ? CHS_Z1R : CHS_Z1L) * n + i]);
         z2 = __uint_as_float(a.state[(ch ? CHS_Z2R : CHS_Z2L) * n + i]);
         pmask = a.psize - 1u; cmask = a.csize - 1u;
-        pmax = (float)(a.psize - 2u); cmax = (float)(a.csize - 2u);
+        pmaxu = a.psize - 2u; cmaxd = (double)(a.csize - 2u);
         rP = rsrc(a.pitch_ring, (uint64_t)n * 2 * a.psize * 4);
         rC = rsrc(a.chorus_ring, (uint64_t)n * 2 * a.csize * 4);
         pshift = (uint32_t)__builtin_ctz(a.psize) + 3u; cshift = (uint32_t)__builtin_ctz(a.csize) + 3u;
@@ -349,7 +358,7 @@ struct ChStageL {
             stage_run(x, 0);
             coop_store(true, 0, wpos, C);
         }
-        pl = plan_chunk_l<kWin>(lfo_acc, lfo_inc, lfo_off, ps_acc, ps_inc, C, D, W, pmax, cmax, FULL);
+        pl = plan_chunk_l<kWin>(lfo_acc, lfo_inc, lfo_off, ps_acc, ps_inc, C, D, wi, wf, pmaxu, cmaxd, FULL);
         load_lines<0>(pl, wpos, true);
     }
     __device__ __forceinline__ void begin(float (&x)[kChunk], int C) {
@@ -380,7 +389,7 @@ struct ChStageL {
             coop_store(true, 0, w0 + (uint32_t)C, Cn);
         }
         pl = plan_chunk_l<kWin>(lfo0 + (uint64_t)C * lfo_inc, lfo_inc, lfo_off, ps0 + (uint64_t)C * ps_inc,
-                                ps_inc, Cn > 0 ? Cn : 4, D, W, pmax, cmax, FULL);
+                                ps_inc, Cn > 0 ? Cn : 4, D, wi, wf, pmaxu, cmaxd, FULL);
         // the line loads below read positions the stores above just wrote (other lanes of this
         // wave): vector memory operations of a wave reach the L1/L2 in issue order, as for the
         // v10 chunk-start input store and the loads after it
@@ -488,12 +497,11 @@ struct ChStageL {
             //     never reads a position newer than its own, so writing them all first is the same
             //     as writing each just before its frame;
             //  (C, the chorus tap, follows the ring stores and chunk c+1's line loads below)
-            // p W == (hi >> 8) (W 2^-24) exactly (scaling by a power of two is exact).  L and R
+            // the tap delays of spec v2 (pitch_split: 32.32 fixed point, olfx_internal.h).  L and R
             // lanes share every tap delay: per pair of frames each lane computes its own frame's
             // (k + ch) gains and delay splits once, and DPP hands both frames' values to both lanes;
             // slot offsets are kept relative to the pair's first frame, whose part of the address
             // is an immediate offset
-            const float Ws = W * 5.9604644775390625e-8f;
             const int chA = (int)ch - cur.sA, chB = (int)ch - cur.sB;
             float gA0 = 0.f, gA1 = 0.f, gB0 = 0.f, gB1 = 0.f, fA0 = 0.f, fA1 = 0.f, fB0 = 0.f, fB1 = 0.f;
             int rA0 = 0, rA1 = 0, rB0 = 0, rB1 = 0;
@@ -506,13 +514,13 @@ struct ChStageL {
                     win_gains(unit24(ph), m_gA, m_gB);
                     gA0 = pair_even(m_gA); gA1 = pair_odd(m_gA);
                     gB0 = pair_even(m_gB); gB1 = pair_odd(m_gB);
-                    int di; float fr;
-                    split_delay3((float)(ph >> 8) * Ws, 1.0f, pmax, di, fr);
-                    const int ra = chA - di;
+                    uint32_t di; float fr;
+                    pitch_split(ph, wi, wf, pmaxu, di, fr);
+                    const int ra = chA - (int)di;
                     rA0 = pair_even_i(ra); rA1 = pair_odd_i(ra);
                     fA0 = pair_even(fr); fA1 = pair_odd(fr);
-                    split_delay3((float)((ph + 0x80000000u) >> 8) * Ws, 1.0f, pmax, di, fr);
-                    const int rb = chB - di;
+                    pitch_split(ph + 0x80000000u, wi, wf, pmaxu, di, fr);   // p1 = (p0 + 1/2) % 1
+                    const int rb = chB - (int)di;
                     rB0 = pair_even_i(rb); rB1 = pair_odd_i(rb);
                     fB0 = pair_even(fr); fB1 = pair_odd(fr);
                 }
@@ -531,45 +539,41 @@ struct ChStageL {
         } else {
             // generic chunk (partial, or a pitch window the lines cannot cover): per frame, with
             // per-frame guards and direct ring reads for the uncovered pitch taps
-            float pl_lfo[2], pl_gA[2], pl_gB[2];
+            float pl_gA[2], pl_gB[2];
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) {
                 if (OUT_LDS && FULL) yo[k] = 0.f;
                 if ((k & 1) == 0) {
-                    const uint64_t la = lfo_acc + (ch ? lfo_inc : 0ull), pa = ps_acc + (ch ? ps_inc : 0ull);
-                    const float m_lfo = cos2pi(unit24h(la + lfo_off));
+                    const uint64_t pa = ps_acc + (ch ? ps_inc : 0ull);
                     float m_gA, m_gB;
                     win_gains(unit24h(pa), m_gA, m_gB);
-                    const float o_lfo = swap_pair(m_lfo), o_gA = swap_pair(m_gA), o_gB = swap_pair(m_gB);
-                    pl_lfo[0] = ch ? o_lfo : m_lfo; pl_lfo[1] = ch ? m_lfo : o_lfo;
+                    const float o_gA = swap_pair(m_gA), o_gB = swap_pair(m_gB);
                     pl_gA[0] = ch ? o_gA : m_gA;    pl_gA[1] = ch ? m_gA : o_gA;
                     pl_gB[0] = ch ? o_gB : m_gB;    pl_gB[1] = ch ? m_gB : o_gB;
                 }
                 if (k >= C) { psv[k] = 0.f; continue; }
-                const float lfo = pl_lfo[k & 1];
-                const float dch = lfo * D + D;
-                const float p0 = unit24h(ps_acc);
-                const float p1 = unit24h(ps_acc + kHalfCycle);
+                const uint64_t lfo_k = lfo_acc + lfo_off;
+                const uint32_t ph = hi32(ps_acc);
                 const float gA = pl_gA[k & 1];
                 const float gB = pl_gB[k & 1];
                 lfo_acc += lfo_inc;
                 ps_acc += ps_inc;
-                int di; float fr;
+                uint32_t di; float fr;
                 float tA, tB;
-                split_delay(p0 * W, 1.0f, pmax, di, fr);
+                pitch_split(ph, wi, wf, pmaxu, di, fr);
                 if (!cur.okA) {
                     const uint32_t q = w0 + k - di;
                     tA = lerp_pair(ld1(rP, own_pb() + (q & pmask) * 8u, 0), ld1(rP, own_pb() + ((q - 1u) & pmask) * 8u, 0), fr);
                 } else {
-                    const int jw = k - di - cur.sA;
+                    const int jw = k - (int)di - cur.sA;
                     tA = lerp_pair(wP0[jw * kRow], wP0[(jw - 1) * kRow], fr);
                 }
-                split_delay(p1 * W, 1.0f, pmax, di, fr);
+                pitch_split(ph + 0x80000000u, wi, wf, pmaxu, di, fr);
                 if (!cur.okB) {
                     const uint32_t q = w0 + k - di;
                     tB = lerp_pair(ld1(rP, own_pb() + (q & pmask) * 8u, 0), ld1(rP, own_pb() + ((q - 1u) & pmask) * 8u, 0), fr);
                 } else {
-                    const int jw = k - di - cur.sB;
+                    const int jw = k - (int)di - cur.sB;
                     tB = lerp_pair(wP1[jw * kRow], wP1[(jw - 1) * kRow], fr);
                 }
                 const float p = tB * gB + tA * gA;
@@ -577,8 +581,8 @@ struct ChStageL {
                 float out = p;
                 if (FULL) {
                     wC[min(k - cur.sC, kWin) * kRow] = p;
-                    split_delay(dch, 0.0f, cmax, di, fr);
-                    const int jw = k - di - cur.sC;
+                    chorus_split(lfo_k, D, cmaxd, di, fr);
+                    const int jw = k - (int)di - cur.sC;
                     const float wet = lerp_pair(wC[jw * kRow], wC[(jw - 1) * kRow], fr);
                     const float lp = b0 * wet + z1;
                     z1 = (b1 * wet - a1 * lp) + z2;
@@ -611,10 +615,9 @@ struct ChStageL {
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) {
                     if ((k & 1) == 0) {
-                        const float m_lfo = cos2pi(unit24h(lfo_acc + (ch ? lfo_inc : 0ull) + lfo_off));
-                        int di; float fr;
-                        split_delay3(m_lfo * D + D, 0.0f, cmax, di, fr);
-                        const int rc = chC - di;
+                        uint32_t di; float fr;
+                        chorus_split(lfo_acc + (ch ? lfo_inc : 0ull) + lfo_off, D, cmaxd, di, fr);
+                        const int rc = chC - (int)di;
                         r0 = pair_even_i(rc); r1 = pair_odd_i(rc);
                         f0 = pair_even(fr); f1 = pair_odd(fr);
                     }

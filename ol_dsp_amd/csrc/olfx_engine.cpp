@@ -215,8 +215,16 @@ void derive_chorus(const float *p, double sr, uint32_t *c) {
     c[CHC_LFO_OFF_LO] = (uint32_t)lfo_off;
     c[CHC_PS_INC] = (uint32_t)(ps_inc >> 32);
     c[CHC_PS_INC_LO] = (uint32_t)ps_inc;
-    c[CHC_DEPTH] = as_u32((float)(depth_ms * sr / 1000.0));       // mstosamps (:3897)
-    c[CHC_WINDOW] = as_u32((float)(window * sr / 1000.0));        // mstosamps(window)
+    // D = mstosamps (:3897) as a double; W = mstosamps(window) in 32.32 fixed point (spec v2,
+    // olfx_internal.h pitch_split / chorus_split)
+    const double D = depth_ms * sr / 1000.0;
+    uint64_t Dbits;
+    std::memcpy(&Dbits, &D, 8);
+    c[CHC_DEPTH] = (uint32_t)(Dbits >> 32);
+    c[CHC_DEPTH_LO] = (uint32_t)Dbits;
+    const uint64_t Wfix = (uint64_t)std::floor(window * sr / 1000.0 * 4294967296.0 + 0.5);
+    c[CHC_WINDOW] = (uint32_t)(Wfix >> 32);
+    c[CHC_WINDOW_LO] = (uint32_t)Wfix;
     // lores~ -> RBJ biquad low-pass, Q = 1/sqrt(2) + 20 q^3 (declared)
     const double Q = 0.70710678118654752 + 20.0 * q * q * q;
     const double w0 = 2.0 * 3.14159265358979323846 * fc / sr;

@@ -129,11 +129,13 @@ enum {
     CHC_LFO_INC = 0,    // high word of cycle~'s phase increment
     CHC_LFO_OFF,        // high word of cycle~'s phase offset
     CHC_PS_INC,         // high word of the pitch-shifter phasor's increment
-    CHC_DEPTH,          // D = mstosamps(1 + 11 depth)       (float)
-    CHC_WINDOW,         // W = mstosamps(window)             (float)
+    CHC_DEPTH,          // D = mstosamps(1 + 11 depth): high word of the double
+    CHC_WINDOW,         // W = mstosamps(window) in 32.32 fixed point: integer part
     CHC_B0, CHC_B1, CHC_B2, CHC_A1, CHC_A2,   // lores~ (RBJ biquad LP, normalised by a0)
     CHC_MIX, CHC_DRY,   // mix, 1 - mix
     CHC_LFO_INC_LO, CHC_LFO_OFF_LO, CHC_PS_INC_LO,   // low words of the three above
+    CHC_DEPTH_LO,       // low word of D
+    CHC_WINDOW_LO,      // fraction of W (32.32)
     CHC_N
 };
 enum {
@@ -143,6 +145,55 @@ enum {
     CHS_LFO_LO, CHS_PS_LO,                // low words of the two phases
     CHS_N
 };
+
+// Tap delays (spec v2, round 4).  Round 3 formed both delays in fp32 from the
+// phasors' top 24 bits: the pitch delay p W (W up to 480 samples) to 2^-15 sample, the chorus delay
+// D cos + D (D up to 576) from a cosine good to 2e-7, i.e. to ~1e-4 sample -- that, not the fp32
+// signal arithmetic, was the spec's deviation from double precision (1.3e-4 / 1.6e-4 of the signal,
+// tests/test_oracle.py test_chorus_deviation_by_stage).  Now:
+//   pitch-shifter: d = p W in 32.32 fixed point, p = the phasor's high word / 2^32 and W in 32.32
+//     (exact integer arithmetic), clamped to [1, pmax]; the fraction rounded once to fp32;
+//   chorus: the LFO phase to 53 bits, cos(2 pi x) by a double Taylor polynomial (|err| < 4e-15),
+//     d = cos D + D in double (D double), clamped to [0, cmax]; the fraction rounded once to fp32.
+// Gains, interpolation, lores~ and the mix stay fp32.  Host and gfx950 evaluate these identically
+// (integer ops, IEEE double + and * in a fixed order, no contraction).
+OLFX_HD void pitch_split(uint32_t ph, uint32_t wi, uint32_t wf, uint32_t pmax, uint32_t &di, float &fr) {
+    const uint64_t d = (uint64_t)ph * wi + (((uint64_t)ph * wf) >> 32);     // p W, 32.32
+    const uint64_t lo = 1ull << 32, hi = (uint64_t)pmax << 32;
+    const uint64_t c = d < lo ? lo : (d > hi ? hi : d);
+    di = (uint32_t)(c >> 32);
+    fr = (float)(uint32_t)c * 2.3283064365386963e-10f;                   // 2^-32: exact scaling
+}
+OLFX_HD double cos2pi_d(double x) {
+    const double u = x - rint(x);                  // exact, u in [-0.5, 0.5]
+    const double a = u < 0.0 ? -u : u;
+    const bool hi = a > 0.25;
+    const double b = hi ? 0.5 - a : a;             // exact
+    const double th = b * 6.283185307179586;
+    const double t2 = th * th;
+    // cos(th) = sum (-1)^k th^2k / (2k)!, k <= 9 (th <= pi/2: truncation < 4e-15), Horner in th^2
+    double r = -1.5619206968586225e-16;            // -1 / 18!
+    r = r * t2 + 4.779477332387385e-14;            //  1 / 16!
+    r = r * t2 - 1.1470745597729725e-11;           // -1 / 14!
+    r = r * t2 + 2.08767569878681e-09;             //  1 / 12!
+    r = r * t2 - 2.755731922398589e-07;            // -1 / 10!
+    r = r * t2 + 2.48015873015873e-05;             //  1 / 8!
+    r = r * t2 - 0.001388888888888889;             // -1 / 6!
+    r = r * t2 + 0.041666666666666664;             //  1 / 4!
+    r = r * t2 - 0.5;
+    r = r * t2 + 1.0;
+    return hi ? -r : r;
+}
+OLFX_HD double chorus_delay(uint64_t phase, double D, double cmax) {
+    const double x = (double)(phase >> 11) * 1.1102230246251565e-16;         // 53-bit phase (2^-53: exact)
+    const double d = cos2pi_d(x) * D + D;
+    return d < 0.0 ? 0.0 : (d > cmax ? cmax : d);
+}
+OLFX_HD void chorus_split(uint64_t phase, double D, double cmax, uint32_t &di, float &fr) {
+    const double d = chorus_delay(phase, D, cmax);
+    di = (uint32_t)d;
+    fr = (float)(d - (double)di);                  // the subtraction is exact
+}
 
 struct ChorusArgs {
     float *pitch_ring;          // [n][psize][2]  (stereo-interleaved: L and R share every tap)

@@ -54,7 +54,7 @@ struct PStageS {
     bool valid;
     uint32_t i;
     uint64_t lfo_inc, ps_inc, lfo_acc, ps_acc;
-    float W, pmax;
+    uint32_t wi, wf, pmaxu;   // pitch window W in 32.32 fixed point; delay clamp psize - 2
     uint32_t pmask, pshift;
     Rsrc rP;
     float *region;
@@ -74,11 +74,12 @@ struct PStageS {
         i = valid ? i_raw : n - 1;
         lfo_inc = word64(a.coef[CHC_LFO_INC * n + i], a.coef[CHC_LFO_INC_LO * n + i]);
         ps_inc = word64(a.coef[CHC_PS_INC * n + i], a.coef[CHC_PS_INC_LO * n + i]);
-        W = __uint_as_float(a.coef[CHC_WINDOW * n + i]);
+        wi = a.coef[CHC_WINDOW * n + i];
+        wf = a.coef[CHC_WINDOW_LO * n + i];
         lfo_acc = word64(a.state[CHS_LFO_ACC * n + i], a.state[CHS_LFO_LO * n + i]);
         ps_acc = word64(a.state[CHS_PS_ACC * n + i], a.state[CHS_PS_LO * n + i]);
         pmask = a.psize - 1u;
-        pmax = (float)(a.psize - 2u);
+        pmaxu = a.psize - 2u;
         rP = rsrc(a.pitch_ring, (uint64_t)n * 2 * a.psize * 4);
         pshift = (uint32_t)__builtin_ctz(a.psize) + 3u;
         region = lds_region;
@@ -157,7 +158,7 @@ struct PStageS {
     }
 
     __device__ __forceinline__ void begin(int C) {
-        pl = plan_chunk_l<kWin>(0ull, 0ull, 0ull, ps_acc, ps_inc, C, 0.0f, W, pmax, 0.0f, false);
+        pl = plan_chunk_l<kWin>(0ull, 0ull, 0ull, ps_acc, ps_inc, C, 0.0, wi, wf, pmaxu, 0.0, false);
         load_lines<0>(pl, wpos, true);
     }
 
@@ -210,21 +211,20 @@ struct PStageS {
         float2 psv[kChunk];
         const bool fast = C == kChunk && __all(cur.okA && cur.okB);
         if (fast) {
-            // p W == (hi >> 8) (W 2^-24) exactly (scaling by a power of two is exact)
-            const float Ws = W * 5.9604644775390625e-8f;
+            // the tap delays of spec v2 (pitch_split: 32.32 fixed point)
             const int rA = -cur.sA, rB = -cur.sB;
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) {
                 const uint32_t ph = hi32(ps_acc);
                 float gA, gB;
                 win_gains(unit24(ph), gA, gB);
-                int di;
+                uint32_t di;
                 float fr;
-                split_delay3((float)(ph >> 8) * Ws, 1.0f, pmax, di, fr);
-                const float *qA = wP0 + (k + rA - di) * kRow2;
+                pitch_split(ph, wi, wf, pmaxu, di, fr);
+                const float *qA = wP0 + (k + rA - (int)di) * kRow2;
                 const float2 tA = lerp2(*(const float2 *)qA, *(const float2 *)(qA - kRow2), fr);
-                split_delay3((float)((ph + 0x80000000u) >> 8) * Ws, 1.0f, pmax, di, fr);
-                const float *qB = wP1 + (k + rB - di) * kRow2;
+                pitch_split(ph + 0x80000000u, wi, wf, pmaxu, di, fr);     // p1 = (p0 + 1/2) % 1
+                const float *qB = wP1 + (k + rB - (int)di) * kRow2;
                 const float2 tB = lerp2(*(const float2 *)qB, *(const float2 *)(qB - kRow2), fr);
                 psv[k] = make_float2(tB.x * gB + tA.x * gA, tB.y * gB + tA.y * gA);
                 ps_acc += ps_inc;
@@ -242,27 +242,26 @@ struct PStageS {
                 if (k >= C) { psv[k] = make_float2(0.f, 0.f); continue; }
                 float gA, gB;
                 win_gains(unit24h(ps_acc), gA, gB);
-                const float p0 = unit24h(ps_acc);
-                const float p1 = unit24h(ps_acc + kHalfCycle);
+                const uint32_t ph = hi32(ps_acc);
                 lfo_acc += lfo_inc;
                 ps_acc += ps_inc;
-                int di;
+                uint32_t di;
                 float fr;
                 float2 tA, tB;
-                split_delay(p0 * W, 1.0f, pmax, di, fr);
+                pitch_split(ph, wi, wf, pmaxu, di, fr);
                 if (!cur.okA) {
                     const uint32_t q = w0 + k - di;
                     tA = lerp2(ld2(rP, own_pb() + (q & pmask) * 8u), ld2(rP, own_pb() + ((q - 1u) & pmask) * 8u), fr);
                 } else {
-                    const int jw = k - di - cur.sA;
+                    const int jw = k - (int)di - cur.sA;
                     tA = lerp2(*(const float2 *)(wP0 + jw * kRow2), *(const float2 *)(wP0 + (jw - 1) * kRow2), fr);
                 }
-                split_delay(p1 * W, 1.0f, pmax, di, fr);
+                pitch_split(ph + 0x80000000u, wi, wf, pmaxu, di, fr);
                 if (!cur.okB) {
                     const uint32_t q = w0 + k - di;
                     tB = lerp2(ld2(rP, own_pb() + (q & pmask) * 8u), ld2(rP, own_pb() + ((q - 1u) & pmask) * 8u), fr);
                 } else {
-                    const int jw = k - di - cur.sB;
+                    const int jw = k - (int)di - cur.sB;
                     tB = lerp2(*(const float2 *)(wP1 + jw * kRow2), *(const float2 *)(wP1 + (jw - 1) * kRow2), fr);
                 }
                 psv[k] = make_float2(tB.x * gB + tA.x * gA, tB.y * gB + tA.y * gA);
@@ -279,8 +278,8 @@ struct PStageS {
         }
         // chunk c+1's plan and line loads (they see the store above: a wave's vector memory
         // operations reach the caches in issue order)
-        pl = plan_chunk_l<kWin>(0ull, 0ull, 0ull, ps0 + (uint64_t)C * ps_inc, ps_inc, Cn > 0 ? Cn : 4, 0.0f, W, pmax,
-                                0.0f, false);
+        pl = plan_chunk_l<kWin>(0ull, 0ull, 0ull, ps0 + (uint64_t)C * ps_inc, ps_inc, Cn > 0 ? Cn : 4, 0.0, wi, wf,
+                                pmaxu, 0.0, false);
         load_lines<PAR ^ 1>(pl, w0 + (uint32_t)C, false);
 #pragma unroll
         for (int k = 0; k < kChunk; ++k)

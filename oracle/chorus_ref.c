@@ -9,9 +9,15 @@
  * git-ignored (modules/rnbo/patcher/.gitignore:1).  No reference test, fixture or golden vector
  * covers them.  This file restates the patch dataflow exactly as written (per-object citations
  * below) with the build's declared spec choices:
- *   - fp32 arithmetic (gen~/RNBO compute in double);
+ *   - fp32 signal arithmetic (gen~/RNBO compute in double);
  *   - phasors as 64-bit fixed-point accumulators (2^64 = one cycle; the increment rounding drifts a
- *     phase by < 2^-64 cycle per sample), their top 24 bits -> the float phase (exact);
+ *     phase by < 2^-64 cycle per sample), their top 24 bits -> the float phase of the crossfade
+ *     gains (exact);
+ *   - tap delays precise (spec v2, round 4): the pitch-shifter's p W in 32.32 fixed point from the
+ *     phasor's high word (pitch_split), the chorus's D cos(2 pi x) + D in double from a 53-bit phase
+ *     and a double Taylor cosine (chorus_split); each split into an integer delay and an fp32
+ *     fraction.  Round 3 formed both delays in fp32 (2^-15 .. 1e-4 sample of error), which was the
+ *     whole of the spec's 1.3e-4 / 1.6e-4 deviation from double arithmetic;
  *   - cos(2 pi x) by a fixed minimax polynomial (oracle_cos2pi below), standing in for cycle~'s
  *     wavetable, and the crossfade windows cos((p - .5) pi) by sin / cos polynomials of one
  *     argument (oracle_win_gains), standing in for gen~'s cos;
@@ -91,8 +97,9 @@ void oracle_win_gains(float p, float *g0, float *g1)
 }
 
 typedef struct {
-    uint64_t lfo_inc, lfo_off, ps_inc;
-    float D, W, b0, b1, b2, a1, a2, mix, dry;
+    uint64_t lfo_inc, lfo_off, ps_inc, Wfix;   /* Wfix: W in 32.32 fixed point */
+    double D;
+    float b0, b1, b2, a1, a2, mix, dry;
 } chcoef_t;
 
 typedef struct {
@@ -128,8 +135,8 @@ static void derive(const float *p, double sr, chcoef_t *c)
     c->lfo_inc = fix64(rate_hz / sr);
     c->lfo_off = fix64(phase);                 /* phase 1.0 wraps to 0: L and R share the LFO */
     c->ps_inc = fix64(pitch / sr);
-    c->D = (float)(depth_ms * sr / 1000.0);
-    c->W = (float)(window * sr / 1000.0);
+    c->D = depth_ms * sr / 1000.0;
+    c->Wfix = (uint64_t)floor(window * sr / 1000.0 * 4294967296.0 + 0.5);
     const double Q = 0.70710678118654752 + 20.0 * q * q * q;
     const double w0 = 2.0 * 3.14159265358979323846 * fc / sr;
     const double cw = cos(w0), sw = sin(w0);
@@ -192,14 +199,57 @@ int oracle_chorus_set(oracle_chorus *o, int inst, int field, float value)
     return 0;
 }
 
-static float read_frac(const float *ring, uint32_t mask, uint32_t w, float d, float dmin, float dmax)
+/* linear interpolation at delay di + fr (gen Delay.read / delay~): x0 + fr (x1 - x0) */
+static float read_split(const float *ring, uint32_t mask, uint32_t w, uint32_t di, float fr)
 {
-    d = fminf(fmaxf(d, dmin), dmax);
-    uint32_t di = (uint32_t)d;
-    float fr = d - (float)di;
-    float x0 = ring[(w - di) & mask];
-    float x1 = ring[(w - di - 1u) & mask];
+    const float x0 = ring[(w - di) & mask];
+    const float x1 = ring[(w - di - 1u) & mask];
     return x0 + fr * (x1 - x0);
+}
+
+/* the pitch-shifter's tap delay p W, p = ph / 2^32 (the phasor's high word), W = Wfix / 2^32:
+   32.32 fixed point by exact integer arithmetic, clamped to [1, pmax], fraction rounded to fp32 */
+static void pitch_split(uint32_t ph, uint64_t Wfix, uint32_t pmax, uint32_t *di, float *fr)
+{
+    const uint64_t d = (uint64_t)ph * (uint32_t)(Wfix >> 32) + (((uint64_t)ph * (uint32_t)Wfix) >> 32);
+    const uint64_t lo = 1ull << 32, hi = (uint64_t)pmax << 32;
+    const uint64_t c = d < lo ? lo : (d > hi ? hi : d);
+    *di = (uint32_t)(c >> 32);
+    *fr = (float)(uint32_t)c * 2.3283064365386963e-10f;
+}
+
+/* cos(2 pi x) in double: exact reduction to b in [0, 1/4], Taylor series of cos to th^18 in th^2
+   (|err| < 4e-15), Horner, no contraction -- the same operations as the GPU */
+double oracle_cos2pi_d(double x)
+{
+    const double u = x - rint(x);
+    const double a = u < 0.0 ? -u : u;
+    const int hi = a > 0.25;
+    const double b = hi ? 0.5 - a : a;
+    const double th = b * 6.283185307179586;
+    const double t2 = th * th;
+    double r = -1.5619206968586225e-16;
+    r = r * t2 + 4.779477332387385e-14;
+    r = r * t2 - 1.1470745597729725e-11;
+    r = r * t2 + 2.08767569878681e-09;
+    r = r * t2 - 2.755731922398589e-07;
+    r = r * t2 + 2.48015873015873e-05;
+    r = r * t2 - 0.001388888888888889;
+    r = r * t2 + 0.041666666666666664;
+    r = r * t2 - 0.5;
+    r = r * t2 + 1.0;
+    return hi ? -r : r;
+}
+
+/* the chorus tap delay D cos(2 pi x) + D from the LFO's 64-bit phase (53 bits used), in double,
+   clamped to [0, cmax]; integer part and fp32 fraction */
+static void chorus_split(uint64_t phase, double D, double cmax, uint32_t *di, float *fr)
+{
+    const double x = (double)(phase >> 11) * 1.1102230246251565e-16;
+    double d = oracle_cos2pi_d(x) * D + D;
+    d = d < 0.0 ? 0.0 : (d > cmax ? cmax : d);
+    *di = (uint32_t)d;
+    *fr = (float)(d - (double)*di);
 }
 
 /* One frame of one instance (both channels): the per-sample operator body shared by the bank
@@ -208,24 +258,25 @@ static void chorus_frame(const oracle_chorus *o, const chcoef_t *k, chstate_t *s
                          const float x[2], float y[2])
 {
     const uint32_t pmask = o->psize - 1, cmask = o->csize - 1;
-    const float pmax = (float)(o->psize - 2), cmax = (float)(o->csize - 2);
-    const float lfo = oracle_cos2pi(unit24(s->lfo_acc + k->lfo_off));
+    uint32_t cdi, di0, di1;
+    float cfr, fr0, fr1;
+    chorus_split(s->lfo_acc + k->lfo_off, k->D, (double)(o->csize - 2), &cdi, &cfr);
     s->lfo_acc += k->lfo_inc;
-    const float dch = lfo * k->D + k->D;
+    const uint32_t ph = (uint32_t)(s->ps_acc >> 32);
     const float p0 = unit24(s->ps_acc);
-    const float p1 = unit24(s->ps_acc + 0x8000000000000000ull);
     s->ps_acc += k->ps_inc;
     float g0, g1;
     oracle_win_gains(p0, &g0, &g1);
-    const float d0 = p0 * k->W, d1 = p1 * k->W;
+    pitch_split(ph, k->Wfix, o->psize - 2, &di0, &fr0);
+    pitch_split(ph + 0x80000000u, k->Wfix, o->psize - 2, &di1, &fr1);   /* p1 = (p0 + 1/2) % 1 */
     for (int c = 0; c < 2; c++) {
-        const float t0 = read_frac(s->pring[c], pmask, w, d0, 1.0f, pmax);
-        const float t1 = read_frac(s->pring[c], pmask, w, d1, 1.0f, pmax);
+        const float t0 = read_split(s->pring[c], pmask, w, di0, fr0);
+        const float t1 = read_split(s->pring[c], pmask, w, di1, fr1);
         const float ps = t1 * g1 + t0 * g0;
         s->pring[c][w & pmask] = x[c];
         if (o->mode == 0) {
             s->cring[c][w & cmask] = ps;
-            const float wet = read_frac(s->cring[c], cmask, w, dch, 0.0f, cmax);
+            const float wet = read_split(s->cring[c], cmask, w, cdi, cfr);
             const float lp = k->b0 * wet + s->z1[c];
             s->z1[c] = (k->b1 * wet - k->a1 * lp) + s->z2[c];
             s->z2[c] = k->b2 * wet - k->a2 * lp;

@@ -74,7 +74,7 @@ static void derive64(const double *p, double sr, int quantize, ch64_t *c)
 
 oracle_chorus64 *oracle_chorus64_create(int n_inst, double sample_rate, int mode)
 {
-    if (n_inst <= 0 || (mode & ~0x1FF)) return NULL;
+    if (n_inst <= 0 || (mode & ~0x7FF)) return NULL;
     oracle_chorus64 *o = (oracle_chorus64 *)calloc(1, sizeof(*o));
     if (!o) return NULL;
     o->n = n_inst; o->mode = mode & 1; o->quantize = (mode >> 1) & 1; o->f32 = mode >> 2; o->sr = sample_rate;
@@ -124,7 +124,32 @@ static double wrap1(double x) { return x - floor(x); }
      F32_CINTERP  chorus tap interpolation in fp32
      F32_LORES    lores~ coefficients and state in fp32
      F32_MIX      x dry + lp mix in fp32 */
-enum { F32_PDELAY = 1, F32_PGAIN = 2, F32_PINTERP = 4, F32_CDELAY = 8, F32_CINTERP = 16, F32_LORES = 32, F32_MIX = 64 };
+enum { F32_PDELAY = 1, F32_PGAIN = 2, F32_PINTERP = 4, F32_CDELAY = 8, F32_CINTERP = 16, F32_LORES = 32, F32_MIX = 64,
+       /* candidate precise delays: the pitch delay in 32.32 fixed point (the phasor's top 32 bits x W
+          in 32.32), the chorus delay from a 53-bit phase in double; both split into an integer and
+          an fp32 fraction */
+       FIX_PDELAY = 128, DBL_CDELAY = 256 };
+
+/* split of a non-negative delay given as an integer and a fraction in [0, 1) */
+static double readsplit(const double *ring, uint32_t mask, uint64_t w, uint32_t di, float fr, int f32i)
+{
+    const double x0 = ring[(w - di) & mask], x1 = ring[(w - di - 1u) & mask];
+    if (!f32i) return x0 + (double)fr * (x1 - x0);
+    const float x0f = (float)x0, x1f = (float)x1;
+    return (double)(x0f + fr * (x1f - x0f));
+}
+/* 32.32 fixed-point pitch delay of phase p (cycles) and window W (samples), clamped to [1, pmax] */
+static void pdelay_fix(double p, double W, double pmax, uint32_t *di, float *fr)
+{
+    const uint64_t ph = (uint64_t)floor(p * 4294967296.0);
+    const unsigned __int128 wf = (unsigned __int128)(uint64_t)floor(W * 4294967296.0 + 0.5);
+    uint64_t d = (uint64_t)(((unsigned __int128)ph * wf) >> 32);
+    const uint64_t lo = 1ull << 32, hi = (uint64_t)pmax << 32;
+    d = d < lo ? lo : (d > hi ? hi : d);
+    *di = (uint32_t)(d >> 32);
+    *fr = (float)(uint32_t)d * 2.3283064365386963e-10f;
+}
+
 
 static double unit24d(double ph) { return floor(ph * 16777216.0) / 16777216.0; }
 
@@ -163,7 +188,17 @@ int oracle_chorus64_process(oracle_chorus64 *o, const float *in, double *out, in
             const int F = o->f32;
             const double lph = wrap1(s->lfo_ph + s->lfo_off);
             double dch;
-            if (F & F32_CDELAY) {
+            uint32_t cdi = 0;
+            float cfr = 0.f;
+            if (F & DBL_CDELAY) {
+                const double ph53 = floor(lph * 9007199254740992.0) / 9007199254740992.0;
+                double dd = cos(2.0 * pi * ph53) * s->D + s->D;
+                const double cmaxd = (double)(o->csize - 2);
+                dd = dd < 0.0 ? 0.0 : (dd > cmaxd ? cmaxd : dd);
+                cdi = (uint32_t)dd;
+                cfr = (float)(dd - (double)cdi);
+                dch = dd;
+            } else if (F & F32_CDELAY) {
                 const float lfo = oracle_cos2pi((float)unit24d(lph));
                 dch = (double)(lfo * (float)s->D + (float)s->D);
             } else {
@@ -185,15 +220,26 @@ int oracle_chorus64_process(oracle_chorus64 *o, const float *in, double *out, in
             }
             for (int c = 0; c < 2; c++) {
                 const double x = in[c * plane + (long)f * n + i];
-                const double t1 = readf(s->pring[c], pmask, w, d1, 1.0, F & F32_PDELAY, F & F32_PINTERP);
-                const double t0 = readf(s->pring[c], pmask, w, d0, 1.0, F & F32_PDELAY, F & F32_PINTERP);
+                double t1, t0;
+                if (F & FIX_PDELAY) {
+                    uint32_t di; float fr;
+                    const double pmaxd = (double)(o->psize - 2);
+                    pdelay_fix(p1, s->W, pmaxd, &di, &fr);
+                    t1 = readsplit(s->pring[c], pmask, w, di, fr, F & F32_PINTERP);
+                    pdelay_fix(p0, s->W, pmaxd, &di, &fr);
+                    t0 = readsplit(s->pring[c], pmask, w, di, fr, F & F32_PINTERP);
+                } else {
+                    t1 = readf(s->pring[c], pmask, w, d1, 1.0, F & F32_PDELAY, F & F32_PINTERP);
+                    t0 = readf(s->pring[c], pmask, w, d0, 1.0, F & F32_PDELAY, F & F32_PINTERP);
+                }
                 const double ps = (F & F32_PINTERP) ? (double)((float)t1 * (float)g1 + (float)t0 * (float)g0)
                                                     : t1 * g1 + t0 * g0;
                 s->pring[c][w & pmask] = x;
                 double y = ps;
                 if (o->mode == 0) {
                     s->cring[c][w & cmask] = ps;
-                    const double wet = readf(s->cring[c], cmask, w, dch, 0.0, F & F32_CDELAY, F & F32_CINTERP);
+                    const double wet = (F & DBL_CDELAY) ? readsplit(s->cring[c], cmask, w, cdi, cfr, F & F32_CINTERP)
+                                                        : readf(s->cring[c], cmask, w, dch, 0.0, F & F32_CDELAY, F & F32_CINTERP);
                     double lp;
                     if (F & F32_LORES) {
                         const float wf = (float)wet, lpf = (float)s->b0 * wf + (float)s->z1[c];

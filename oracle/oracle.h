@@ -45,6 +45,7 @@ enum {
 };
 typedef struct oracle_chorus oracle_chorus;
 float oracle_cos2pi(float x);
+double oracle_cos2pi_d(double x);
 void oracle_win_gains(float p, float *g0, float *g1);
 /* mode 0 = full chorus, 1 = pitch-shift stage only (params OCH_PITCH = shift Hz, OCH_WINDOW) */
 oracle_chorus *oracle_chorus_create(int n_inst, float sample_rate, int mode);

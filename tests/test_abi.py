@@ -65,8 +65,9 @@ def test_abi_version_and_kind_info():
     assert info.state_bytes_per_instance == (42368 + 3 + 8) * 4
     ch = ofx.kind_info(ofx.KIND_CHORUS, 48000.0)
     assert (ch.n_params, ch.in_channels, ch.out_channels) == (8, 2, 2)
-    # rings + 8 state words (two 64-bit phasors, 4 biquad floats) + 15 coefficient words
-    assert ch.state_bytes_per_instance == (2 * (512 + 2048) + 8 + 15) * 4
+    # rings + 8 state words (two 64-bit phasors, 4 biquad floats) + 17 coefficient words (spec v2:
+    # D as a double, W in 32.32 fixed point)
+    assert ch.state_bytes_per_instance == (2 * (512 + 2048) + 8 + 17) * 4
     vc = ofx.kind_info(ofx.KIND_VOICE)
     assert (vc.n_params, vc.in_channels, vc.out_channels) == (16, 0, 1)
     assert vc.state_bytes_per_instance == (8 + 19) * 4
