@@ -1040,6 +1040,35 @@ def test_mix_buses_bit_exact(cuda):
     assert bits_equal(e.mix(y), O.mix_ref(y, [back]))
 
 
+@pytest.mark.parametrize("n,sizes", [(300, [8]), (3000, [8]), (2100, [1, 7, 0, 12, 3])])
+def test_mix_contiguous_buses_bit_exact(cuda, n, sizes):
+    """Buses that are contiguous voice runs in voice order (voice_mix_v3: staged coalesced rows):
+    buses of 8 (the bench's Polyvoice layout; 3000 voices -> 375 buses, more than one block of 256),
+    and ragged runs with empty buses; frame counts on and off the four-frame step: bit-identical to
+    Polyvoice's in-order adds into a non-zero bus buffer."""
+    import torch
+    rng = np.random.default_rng(n)
+    cfg = voice_configs(rng, n)
+    cfg[2] *= 0.25
+    notes = [int(v) for v in rng.integers(36, 97, n)]
+    e, _ = _voice_pair(n, cfg, notes)
+    buses, v, k = [], 0, 0
+    while v < n:
+        m = min(sizes[k % len(sizes)], n - v)
+        buses.append(list(range(v, v + m)))
+        v += m
+        k += 1
+    e.mix_config(buses)
+    y = _voice_run(e, 256, cuda)
+    assert np.all(np.isfinite(y))
+    init = rng.standard_normal((256, len(buses))).astype(np.float32)
+    want = O.mix_ref(y, buses, init)
+    dev = e.mix(torch.from_numpy(y).to(cuda), torch.from_numpy(init.copy()).to(cuda))
+    torch.cuda.synchronize()
+    assert bits_equal(dev.cpu().numpy(), want)
+    assert bits_equal(e.mix(np.ascontiguousarray(y[..., :250, :]), init[:250].copy()), want[:250])
+
+
 def test_mix_config_rejects_bad_lists(cuda):
     import ol_dsp_amd as ofx
     e = engine("voice", 16)
