@@ -4,6 +4,7 @@
 #include <cstdlib>
 
 #include "chorus_block.h"
+#include "chorus_pc.h"
 #include "chorus_stage_l.h"
 
 namespace olfx {
@@ -79,17 +80,77 @@ __global__ __launch_bounds__(cb::kThreads, 1) void chorus_block_v13(ChorusArgs a
     }
 }
 
+// chorus_block_v14 (chorus_pc.h): v13 with lores~ on its own wave (wave 7), fed through its own
+// LDS region and synchronised by LDS counters, so it overlaps the next group's loads and phases.
+__global__ __launch_bounds__(pc::kThreads, 1) void chorus_block_v14(ChorusArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    pc::Block B(a, lds);
+    const uint32_t ngroups = (a.n + pc::kG - 1) / pc::kG;
+    const uint32_t grid = gridDim.x, b = blockIdx.x;
+    const uint32_t g0 = (grid & 7u) == 0 ? (b & 7u) * (grid >> 3) + (b >> 3) : b;
+    if (g0 >= ngroups) return;
+    if (threadIdx.x < (uint32_t)pc::kFlags) B.flags[threadIdx.x] = 0u;
+    __syncthreads();                                   // the only workgroup barrier
+    if (B.wave == (uint32_t)pc::kProd) {               // the consumer: lores~, round by round
+        uint32_t r = 0;
+        for (uint32_t g = g0; g < ngroups; g += grid, ++r) {
+            B.wait_flag(1, r + 1);
+            B.phase3(g, (int)(r % pc::kNBuf));
+            B.signal(2, r + 1);
+        }
+        return;
+    }
+    pc::Pre pre;
+    uint32_t g = g0, r = 0;
+    int buf = 0;
+    B.store_scalar(buf, B.load_scalar(g));
+    B.producer_barrier();
+    B.issue(g, buf, pre);
+    B.fill(buf, pre);
+    B.producer_barrier();
+    while (true) {
+        const uint32_t gn = g + grid;
+        const bool next = gn < ngroups;
+        const int nb = buf == pc::kNBuf - 1 ? 0 : buf + 1;
+        uint32_t sv = 0;
+        if (next) sv = B.load_scalar(gn);
+        B.phase1(g, buf);
+        if (next) B.store_scalar(nb, sv);
+        B.producer_barrier();
+        if (next) B.issue(gn, nb, pre);               // in flight until the fill below
+        B.wait_flag(2, r);                            // lores~ of the previous group done: W free
+        B.out(g - grid, r > 0);
+        B.producer_barrier();
+        B.phase2(buf);
+        B.producer_barrier();
+        if (B.wave == 0) B.signal(1, r + 1);          // W holds this group's taps
+        if (!next) break;
+        B.fill(nb, pre);
+        B.producer_barrier();
+        g = gn;
+        buf = nb;
+        ++r;
+    }
+    B.wait_flag(2, r + 1);
+    B.out(g, true);
+}
+
 namespace {
-// OLFX_CHORUS_KERNEL=11 forces v11 (A/B diagnostic)
-bool v13_enabled() {
-    static const bool on = [] {
+// OLFX_CHORUS_KERNEL=11 / 13 / 14 forces that chorus kernel (A/B diagnostic)
+int forced_kernel() {
+    static const int k = [] {
         const char *v = std::getenv("OLFX_CHORUS_KERNEL");
-        return !(v && std::atoi(v) == 11);
+        return v ? std::atoi(v) : 0;
     }();
-    return on;
+    return k;
 }
 bool v13_geometry(uint32_t n, uint32_t psize, uint32_t csize) {
-    return v13_enabled() && (n & 3u) == 0 && psize == cb::kPsize && csize == cb::kCsize;
+    return forced_kernel() != 11 && (n & 3u) == 0 && psize == cb::kPsize && csize == cb::kCsize;
+}
+// the block-at-once kernel for a mode: the chorus v14 (v13 when forced), the pitch-shifter v13
+int block_kernel(uint32_t mode) {
+    if (mode == 0) return forced_kernel() == 13 ? 13 : 14;
+    return 13;
 }
 }  // namespace
 
@@ -99,8 +160,9 @@ extern "C" __attribute__((visibility("default"))) int olfx_debug_stamps(uint64_t
 }
 #endif
 
-const char *chorus_kernel_name(uint32_t n, uint32_t psize, uint32_t csize) {
-    return v13_geometry(n, psize, csize) ? "chorus_block_v13" : "chorus_block_v11";
+const char *chorus_kernel_name(uint32_t n, uint32_t psize, uint32_t csize, uint32_t mode) {
+    if (!v13_geometry(n, psize, csize)) return "chorus_block_v11";
+    return block_kernel(mode) == 14 ? "chorus_block_v14" : "chorus_block_v13";
 }
 
 // chorus_block_v11: one wave = 32 instances x 2 channels over the line-carry stage
@@ -212,17 +274,25 @@ hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s) {
         // at most kS frames per launch (the LDS holds one block per instance); longer calls run as
         // consecutive launches, whose boundaries order each launch's ring stores before the next
         // one's ring loads
-        const uint32_t ngroups = (a.n + cb::kG - 1) / cb::kG;
+        const bool v14 = block_kernel(a.mode) == 14;
+        const uint32_t gsize = v14 ? (uint32_t)pc::kG : (uint32_t)cb::kG;
+        const uint32_t ngroups = (a.n + gsize - 1) / gsize;
         const uint32_t grid = min(ngroups, a.cus ? a.cus : 256u);
-        const size_t lds = (size_t)cb::kLdsFloats * sizeof(float);
         for (uint32_t f0 = 0; f0 < a.n_frames; f0 += (uint32_t)cb::kS) {
             ChorusArgs sub = a;
             sub.in = a.in + (size_t)f0 * a.n;
             sub.out = a.out + (size_t)f0 * a.n;
             sub.n_frames = min((uint32_t)cb::kS, a.n_frames - f0);
             sub.t0 = a.t0 + f0;
-            if (a.mode == 0) hipLaunchKernelGGL((chorus_block_v13<true>), dim3(grid), dim3(cb::kThreads), lds, s, sub);
-            else hipLaunchKernelGGL((chorus_block_v13<false>), dim3(grid), dim3(cb::kThreads), lds, s, sub);
+            if (v14)
+                hipLaunchKernelGGL(chorus_block_v14, dim3(grid), dim3(pc::kThreads),
+                                   (size_t)pc::kLdsFloats * sizeof(float), s, sub);
+            else if (a.mode == 0)
+                hipLaunchKernelGGL((chorus_block_v13<true>), dim3(grid), dim3(cb::kThreads),
+                                   (size_t)cb::kLdsFloats * sizeof(float), s, sub);
+            else
+                hipLaunchKernelGGL((chorus_block_v13<false>), dim3(grid), dim3(cb::kThreads),
+                                   (size_t)cb::kLdsFloats * sizeof(float), s, sub);
         }
         return hipGetLastError();
     }

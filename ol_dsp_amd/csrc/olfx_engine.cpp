@@ -1691,8 +1691,8 @@ const char *olfx_kernel_name(const olfx_engine *e) {
     if (!e) return "";
     switch (e->kind) {
     case OLFX_KIND_DATTORRO: return "dattorro_block_v4";
-    case OLFX_KIND_CHORUS:
-    case OLFX_KIND_PITCHSHIFT: return chorus_kernel_name(e->n, e->psize, e->csize);
+    case OLFX_KIND_CHORUS: return chorus_kernel_name(e->n, e->psize, e->csize, 0);
+    case OLFX_KIND_PITCHSHIFT: return chorus_kernel_name(e->n, e->psize, e->csize, 1);
     case OLFX_KIND_VOICE: return "voice_block_v5";
     case OLFX_KIND_VOICE_MOOG: return "voice_block_v4";
     case OLFX_KIND_CHAIN: return "chain_block_v5";

@@ -331,7 +331,7 @@ hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s);
 hipError_t launch_chain(const ChainArgs &a, hipStream_t s);
 hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s);
 // the chorus kernel launch_chorus picks for n instances, ring sizes and cooperative I/O
-const char *chorus_kernel_name(uint32_t n, uint32_t psize, uint32_t csize);
+const char *chorus_kernel_name(uint32_t n, uint32_t psize, uint32_t csize, uint32_t mode);
 hipError_t launch_voice(const VoiceArgs &a, hipStream_t s);
 
 // ----------------------------------------------------------------------------------------------

@@ -463,7 +463,7 @@ def test_chorus_block_kernel_edges(cuda, kind, n):
         for i in range(n):
             ref.set(i, "pitch", float(p[0, i]))
             ref.set(i, "window", float(p[7, i]))
-    assert e.kernel_name == "chorus_block_v13"
+    assert e.kernel_name == ("chorus_block_v14" if kind == "chorus" else "chorus_block_v13")
     y = run_gpu(e, x, blocks, cuda)
     yr = ref.process(x, threads=8)
     assert bits_equal(y, yr), first_mismatch(y, yr)
