@@ -316,14 +316,18 @@ def parity_check(job: dict, sr: float) -> dict:
 # ------------------------------------------------------------------------------------------------
 # GPU workloads
 # ------------------------------------------------------------------------------------------------
-def _traffic(name: str, n: int, B: int, override: str = ""):
+def _traffic(name: str, n: int, B: int, override: str = "", kernel: str = ""):
+    """The PMC traffic summary of this workload's kernel (tools/pmc_traffic.py), if one was recorded
+    for the same instance count, block and kernel (a summary of another kernel is never used)."""
     for tj in ([override] if override else []) + [os.path.join(ROOT, "profiles", f"traffic_{name}_{n}.json"),
                                                   os.path.join(ROOT, "profiles", f"traffic_{name}.json")]:
         if tj and os.path.exists(tj):
             try:
                 with open(tj) as f:
                     tr = json.load(f)
-                if tr.get("instances") == n and tr.get("block") == B:
+                kernels = tr.get("counters_per_kernel") or {}
+                same_kernel = not kernel or any(kernel in k for k in kernels)
+                if tr.get("instances") == n and tr.get("block") == B and same_kernel:
                     return tr
             except Exception:
                 pass
@@ -538,7 +542,7 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
     per_launch = n * B
     achieved = bpf * per_launch / (kern_ms * 1e-3) / 1e9
     achieved_r = rbpf * per_launch / (kern_ms * 1e-3) / 1e9
-    tr = _traffic(name, n, B, args.traffic_json if name == args.workload else "")
+    tr = _traffic(name, n, B, args.traffic_json if name == args.workload else "", kname)
     traffic = tr.get("hbm_bytes_per_launch") if tr else None
     # the PMC-measured HBM bytes of the same kernel (profiles/traffic_<workload>.json, separate
     # --pmc passes) over this run's kernel time: what HBM actually moved, against the peak
