@@ -21,6 +21,8 @@
 // program order.  No MFMA: scalar recurrences.
 // Bound: HBM.
 #pragma once
+#include <type_traits>
+
 #include "olfx_internal.h"
 
 namespace olfx {
@@ -182,6 +184,36 @@ struct PreTap {
 #pragma unroll
         for (int k = 0; k < 4; ++k) { x2[k] = x1[k]; x1[k] = xin[k]; }
     }
+    // the chunk's input into the ring: one 16-B group per lane, position-major (coalesced)
+    __device__ __forceinline__ void write(const DattorroArgs &a, uint32_t gw, uint32_t i, const float (&xin)[4]) const {
+        *grpu<DT_PRE>(a, gw, i) = make_float4(xin[0], xin[1], xin[2], xin[3]);
+    }
+};
+
+// Gather mode (per-instance pre-delays, verb.cpp:137-139): dattorro_predelay_v1 has already written
+// the block's pre-delayed input, group by group, to a.pre_block ([n_frames/4][n][4]: 16 B per lane
+// and chunk, coalesced) and kept the ring itself, instance-major.  The network reads that stream:
+// no gather across lines here, and no ring write.
+struct PreBlock {
+    float4 cur, pre;
+    uint32_t t0, last;
+    __device__ __forceinline__ void prime(const DattorroArgs &a, uint32_t t0_, uint32_t d, uint32_t i) {
+        (void)d;
+        t0 = t0_;
+        last = a.n_frames / 4u - 1u;
+        cur = ((const float4 *)a.pre_block)[i];
+    }
+    __device__ __forceinline__ void prefetch(const DattorroArgs &a, uint32_t t, uint32_t d, uint32_t i) {
+        (void)d;
+        const uint32_t g = min(((t - t0) >> 2) + 1u, last);
+        pre = ((const float4 *)a.pre_block)[(size_t)g * a.n + i];
+    }
+    __device__ __forceinline__ void resolve(const float (&xin)[4], uint32_t d, float (&xpd)[4]) const {
+        (void)xin; (void)d;
+        xpd[0] = cur.x; xpd[1] = cur.y; xpd[2] = cur.z; xpd[3] = cur.w;
+    }
+    __device__ __forceinline__ void advance(const float (&xin)[4]) { (void)xin; cur = pre; }
+    __device__ __forceinline__ void write(const DattorroArgs &, uint32_t, uint32_t, const float (&)[4]) const {}
 };
 
 // The body of one 4-frame chunk (verb.cpp:273-299, 302-325).  Taps come by reference, so after
@@ -191,14 +223,15 @@ struct PreTap {
 
 template <class TIN0, class TIN1, class TIN2, class TIN3, class TFBA, class TFBB, class TDL1A, class TDL1B,
           class TAP2A, class TAP2B, class TL1, class TL2, class TL3, class TL4, class TL5, class TL6, class TL7,
-          class TR1, class TR2, class TR3, class TR4, class TR5, class TR6, class TR7, class TM1A, class TM1B>
+          class TR1, class TR2, class TR3, class TR4, class TR5, class TR6, class TR7, class TM1A, class TM1B,
+          class TPRE>
 __device__ __forceinline__ void step_body(
     const DattorroArgs &a, uint32_t i, uint32_t t0, bool has_next, const float (&xin)[4], float (&o_l)[4],
     float (&o_r)[4], uint32_t dpre, float g_pre, float g_in1, float g_in2, float g_dd1, float g_damp, float g_decay,
     float g_dd2, float &lp_pre, float &lp_a, float &lp_b, TIN0 &in0, TIN1 &in1, TIN2 &in2, TIN3 &in3, TFBA &fbA,
     TFBB &fbB, TDL1A &dl1a, TDL1B &dl1b, TAP2A &ap2a, TAP2B &ap2b, TL1 &oL1, TL2 &oL2, TL3 &oL3, TL4 &oL4,
     TL5 &oL5, TL6 &oL6, TL7 &oL7, TR1 &oR1, TR2 &oR2, TR3 &oR3, TR4 &oR4, TR5 &oR5, TR6 &oR6, TR7 &oR7,
-    TM1A &ap1a, TM1B &ap1b, PreTap &pre) {
+    TM1A &ap1a, TM1B &ap1b, TPRE &pre) {
     // Prefetch unconditionally (the last chunk's prefetch reads valid ring memory and is
     // dropped): loads under a branch cost precise waitcnt tracking at the merge.
     (void)has_next;
@@ -259,7 +292,7 @@ __device__ __forceinline__ void step_body(
 
     // ---- writes: one 16-B group per line ----
     const uint32_t gw = t0 >> 2;
-    *grpu<DT_PRE>(a, gw, i) = make_float4(xin[0], xin[1], xin[2], xin[3]);
+    pre.write(a, gw, i, xin);
     *grpu<DT_IN0>(a, gw, i) = make_float4(w_in0[0], w_in0[1], w_in0[2], w_in0[3]);
     *grpu<DT_IN1>(a, gw, i) = make_float4(w_in1[0], w_in1[1], w_in1[2], w_in1[3]);
     *grpu<DT_IN2>(a, gw, i) = make_float4(w_in2[0], w_in2[1], w_in2[2], w_in2[3]);
@@ -293,7 +326,8 @@ __device__ __forceinline__ void step_body(
 //   dt_step(t0, has_next, xin[4], o_l[4], o_r[4])  one 4-frame chunk, mono in -> L/R out
 //   dt_finish()                                    writes the recursive scalars back
 #define DT_PRIME_OP(T) T.prime(dt_args, t0, dt_i);
-#define DT_STAGE(A, I)                                                                                   \
+#define DT_STAGE(A, I) DT_STAGE_PRE(A, I, olfx::dt::PreTap)
+#define DT_STAGE_PRE(A, I, PRE_T)                                                                        \
     const DattorroArgs &dt_args = (A);                                                                   \
     const uint32_t dt_n = dt_args.n, dt_i = (I);                                                         \
     const float g_pre = dt_args.coef[DTC_PREFILTER * dt_n + dt_i];                                       \
@@ -322,7 +356,7 @@ __device__ __forceinline__ void step_body(
     olfx::dt::Tap<DT_DL2B, kDl2B_o1, 1> oR7;                                                             \
     olfx::dt::ModTap<DT_AP1A, kDtDelay[DT_AP1A]> ap1a;                                                   \
     olfx::dt::ModTap<DT_AP1B, kDtDelay[DT_AP1B]> ap1b;                                                   \
-    olfx::dt::PreTap pre;                                                                                \
+    PRE_T pre;                                                                                           \
     auto dt_prime = [&](uint32_t t0) {                                                                   \
         DT_ALL_TAPS(DT_PRIME_OP)                                                                         \
         ap1a.prime(dt_args, t0, dt_i);                                                                   \

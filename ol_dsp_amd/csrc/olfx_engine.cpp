@@ -435,6 +435,11 @@ struct olfx_engine {
     uint32_t *fr_state = nullptr, *fr_coef = nullptr;
     uint32_t n_dt = 0;           // reverb-stage instances: n, or n rounded up to 64 for the chain
     float *dt_rings = nullptr;
+    // standalone reverb, per-instance pre-delays (dattorro.hip gather mode): the instance-major
+    // pre-delay ring and the block's pre-delayed input, allocated on first need
+    float *dt_pre_im = nullptr, *dt_pre_blk = nullptr;
+    bool dt_gather = false;      // the pre-delay ring's content is instance-major (dt_pre_im)
+    bool dt_pre_check = true;    // a pre-delay changed: re-decide the mode at the next block
     float *dt_state = nullptr;
     float *dt_coef = nullptr;
 
@@ -871,6 +876,8 @@ int init_state(olfx_engine *e) {
         std::fill(e->params.begin() + (size_t)f * e->n, e->params.begin() + (size_t)(f + 1) * e->n, d[f]);
     e->configured.assign(e->n, 0);
     e->n_components = 0;
+    e->dt_gather = false;          // the zeroed ring is position-major again
+    e->dt_pre_check = true;
     e->events.clear();
     e->ev_slot.assign(e->n, -1);
     e->frames = 0;
@@ -945,7 +952,42 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, uin
         return a;
     };
     switch (e->kind) {
-    case OLFX_KIND_DATTORRO: r = launch_dattorro(dt_args(din, dout), s); break;
+    case OLFX_KIND_DATTORRO: {
+        if (e->dt_pre_check) {
+            // one pre-delay for all instances: the position-major ring and its coalesced tap;
+            // several: gather mode (dattorro.hip), its ring instance-major
+            e->dt_pre_check = false;
+            const float *pd = e->params.data() + (size_t)OLFX_DT_PREDELAY * e->n;
+            const uint32_t d0 = dattorro_predelay_samples(pd[0]);
+            bool uniform = true;
+            for (uint32_t i = 1; i < e->n && uniform; ++i) uniform = dattorro_predelay_samples(pd[i]) == d0;
+            if (uniform == e->dt_gather) {
+                if (!e->dt_pre_im) {
+                    HIPCHK(e, hipMalloc((void **)&e->dt_pre_im, (size_t)kDtSize[DT_PRE] * e->n * 4));
+                    HIPCHK(e, hipMalloc((void **)&e->dt_pre_blk, (size_t)256 * e->n * 4));
+                }
+                DattorroArgs ca = dt_args(nullptr, nullptr);
+                ca.pre_im = e->dt_pre_im;
+                // the ring's content into the other layout, on the stream, ahead of this block
+                r = launch_dattorro_pre_convert(ca, !uniform, s);
+                if (r != hipSuccess) return e->hip_fail(r, "pre-delay ring conversion");
+                e->dt_gather = !uniform;
+            }
+        }
+        if (!e->dt_gather) {
+            r = launch_dattorro(dt_args(din, dout), s);
+            break;
+        }
+        for (uint32_t f0 = 0; f0 < n_frames && r == hipSuccess; f0 += 256) {   // dt_pre_blk holds 256 frames
+            DattorroArgs ga = dt_args(din + (size_t)f0 * e->n, dout + (size_t)f0 * e->n);
+            ga.n_frames = std::min(256u, n_frames - f0);
+            ga.t0 = (t0 + f0) & 0xFFFFu;
+            ga.pre_im = e->dt_pre_im;
+            ga.pre_block = e->dt_pre_blk;
+            r = launch_dattorro(ga, s);
+        }
+        break;
+    }
     case OLFX_KIND_CHORUS:
         r = launch_chorus(ch_args(e->ch_pring, e->ch_cring, e->ch_state, e->ch_coef, din, dout, 0), s);
         break;
@@ -1042,7 +1084,9 @@ int run_frames(olfx_engine *e, const float *in, float *out, uint32_t n_frames, h
     const uint32_t ich = in_channels(e->kind), och = out_channels(e->kind);
     const uint32_t F = (uint32_t)std::max<uint64_t>(4, std::min<uint64_t>(n_frames, ((1ull << 26) / (2 * n)) & ~3ull));
     if (e->tile_floats < (size_t)2 * F * n) {
-        if (e->tile_in) (void)hipFree(e->tile_in);
+        if (e->dt_pre_im) (void)hipFree(e->dt_pre_im);
+    if (e->dt_pre_blk) (void)hipFree(e->dt_pre_blk);
+    if (e->tile_in) (void)hipFree(e->tile_in);
         if (e->tile_out) (void)hipFree(e->tile_out);
         e->tile_in = e->tile_out = nullptr;
         e->tile_floats = 0;
@@ -1244,6 +1288,8 @@ int olfx_destroy(olfx_engine *e) {
         if (sl.consumed) (void)hipEventDestroy(sl.consumed);
     });
     if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
+    if (e->dt_pre_im) (void)hipFree(e->dt_pre_im);
+    if (e->dt_pre_blk) (void)hipFree(e->dt_pre_blk);
     if (e->tile_in) (void)hipFree(e->tile_in);
     if (e->tile_out) (void)hipFree(e->tile_out);
     if (e->d_mem) (void)hipFree(e->d_mem);
@@ -1285,6 +1331,7 @@ const char *bad_value(const olfx_engine *e, uint32_t field, float v) {
 // kernel variant that serves them) follows its topology field.
 void store_param(olfx_engine *e, uint32_t field, uint32_t inst, float v) {
     float &slot = e->params[(size_t)field * e->n + inst];
+    if (e->kind == OLFX_KIND_DATTORRO && field == OLFX_DT_PREDELAY) e->dt_pre_check = true;
     if (e->kind == OLFX_KIND_FXRACK && field == OLFX_FR_TOPOLOGY)
         e->n_components += (v >= 2.f ? 1 : 0) - (slot >= 2.f ? 1 : 0);
     slot = v;

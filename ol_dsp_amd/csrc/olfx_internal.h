@@ -80,7 +80,16 @@ struct DattorroArgs {
     uint32_t n_frames;
     uint32_t t0;                // stream time (frames since create) of the first frame, mod 2^16
     uint32_t in_ch;             // 1 or 2
+    // gather mode (standalone reverb with per-instance pre-delays, dattorro.hip): the pre-delay
+    // ring instance-major ([n][8192]) and the block's pre-delayed input ([n_frames/4][n][4]),
+    // written by dattorro_predelay_v1 ahead of the block; nullptr otherwise
+    float *pre_im;
+    float *pre_block;
 };
+// standalone reverb: the pre-delay ring's layout changed between position-major (uniform
+// pre-delays, dattorro_block_v4's own tap) and instance-major (gather mode): the ring's content
+// is copied into the other layout (to_im: position-major -> instance-major)
+hipError_t launch_dattorro_pre_convert(const DattorroArgs &a, bool to_im, hipStream_t s);
 
 // ----------------------------------------------------------------------------------------------
 // Deterministic cos(2*pi*x): used by the chorus LFO (RNBO cycle~).  Branch-free (selects only, no

@@ -109,6 +109,52 @@ def test_dattorro_per_instance_predelay(cuda):
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
 
+def test_dattorro_predelay_gather_mode_switches(cuda):
+    """The standalone reverb switches its pre-delay ring between the position-major tap (one
+    pre-delay for every instance) and gather mode (per-instance pre-delays: dattorro_predelay_v1,
+    instance-major ring) whenever the pre-delays become equal or differ; the ring's content is
+    carried across each switch.  Uniform -> per instance (edges 0..8, 255..257, 4800, past the max)
+    -> uniform -> per instance, calls of 256, 4, 1028 (gather mode splits at 256) and 60 frames,
+    bit-exact against the oracle throughout; reset() returns to the position-major ring."""
+    n = 96
+    rng = np.random.default_rng(81)
+    p = dt_params(rng, n, 0.2)
+    e = engine("dattorro", n)
+    e.set_params(0, p)
+    ref = O.Dattorro(n)
+    for i in range(n):
+        for f in range(7):
+            ref.set(i, f, float(p[f, i]))
+    edge = np.array([0, 1, 2, 3, 4, 7, 8, 255, 256, 257, 4800, 8191, 8193], np.float64) / 4800
+    ys, yrs = [], []
+    for step in range(6):
+        if step in (1, 4):                                  # per instance: gather mode
+            pd = rng.uniform(0, 1, n).astype(np.float32)
+            pd[:len(edge)] = edge.astype(np.float32)
+        elif step == 2:                                     # one value for all: the position-major tap
+            pd = np.full(n, 0.05, np.float32)
+        else:
+            pd = None
+        if pd is not None:
+            e.set_params("pre_delay", pd[None, :])
+            for i in range(n):
+                ref.set(i, 0, float(pd[i]))
+        x = fast_noise(n, 1348, seed=81 + step)
+        ys.append(run_gpu(e, x, [256, 4, 1028, 60], cuda))
+        yrs.append(ref.process(x, threads=8))
+    y, yr = np.concatenate(ys, 1), np.concatenate(yrs, 1)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+    e.reset()
+    ref2 = O.Dattorro(n)
+    e.set_params(0, p)
+    for i in range(n):
+        for f in range(7):
+            ref2.set(i, f, float(p[f, i]))
+    x = fast_noise(n, 512, seed=99)
+    y2, yr2 = run_gpu(e, x, [512], cuda), ref2.process(x)
+    assert bits_equal(y2, yr2), first_mismatch(y2, yr2)
+
+
 def test_dattorro_predelay_beyond_max(cuda):
     """Pre-delays past MAX_PREDELAY: the reference accepts any value whose product with 4800 fits
     uint16 (verb.cpp:137-139); DelayBuffer_setDelay's offset mask + 1 - delay (verb.cpp:59-61) on
