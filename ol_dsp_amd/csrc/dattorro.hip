@@ -11,9 +11,9 @@
 // successive chunks of a lane touch one line eight times after it has left the caches: the gather
 // read 8x its bytes (dattorro_rpd +30 %, round 3).  Gather mode (the engine switches when the
 // pre-delays differ) keeps that ring instance-major and runs dattorro_predelay_v1 ahead of the
-// block: one lane per instance writes the block's mono input into its ring and reads its
-// pre-delayed block back as whole lines, in order, and hands the network a coalesced stream
-// (PreBlock).  The network itself then reads no input and writes no pre-delay ring.
+// block: one lane per instance walks its own ring in stream order (whole lines, in order) and
+// hands the network its pre-delayed block as a coalesced stream (PreBlock).  The network itself
+// then reads no input and writes no pre-delay ring.
 #include "dattorro_stage.h"
 
 namespace olfx {
@@ -68,12 +68,13 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v4(DattorroArgs a) {
     dt_finish();
 }
 
-// Gather mode's pre-pass: one lane per instance.  (1) the block's mono input (l + r) / 2 into the
-// instance's own ring (positions t0 .. t0 + F - 1; a lane's 16-B pieces of one line leave back to
-// back, so the L2 merges them into whole lines); (2) the pre-delayed block, positions t0 - d + k,
-// read back from that ring in order (a line's eight pieces in consecutive iterations: one fetch)
-// and written as [F/4][n][4] (coalesced).  Reading after writing covers d < F: the positions of
-// this block are in the ring by then (a lane reads its own writes, in program order).
+// Gather mode's pre-pass: one lane per instance, chunk by chunk in stream order as
+// DelayBuffer_process (verb.cpp:107-110: write position t, then read t - d): the chunk's
+// pre-delayed samples are read first -- the positions before the chunk from the instance's own
+// ring (two aligned 16-B pieces: consecutive chunks hit the same line back to back, one fetch per
+// line), those inside it (d < 4) from the chunk's input -- then the chunk's mono input (l + r) / 2
+// is written (a lane's pieces of one line leave back to back: the L2 merges them into whole lines).
+// The pre-delayed block goes out as [F/4][n][4] (coalesced) for the network.
 constexpr uint32_t kPreSize = kDtSize[DT_PRE];
 __global__ __launch_bounds__(256) void dattorro_predelay_v1(DattorroArgs a) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -81,8 +82,10 @@ __global__ __launch_bounds__(256) void dattorro_predelay_v1(DattorroArgs a) {
     const uint32_t n = a.n;
     const size_t plane = a.plane;
     const bool stereo = a.in_ch == 2;
-    const uint32_t d = (uint32_t)a.coef[DTC_PREDELAY * n + i];         // exact integer 0..4800
+    const uint32_t d = (uint32_t)a.coef[DTC_PREDELAY * n + i];         // exact integer 0..8191
+    const float *ring_r = a.pre_im + (size_t)i * kPreSize;
     float *ring = a.pre_im + (size_t)i * kPreSize;
+    float4 *blk = (float4 *)a.pre_block;
     for (uint32_t f0 = 0; f0 < a.n_frames; f0 += 4) {
         float x[4];
 #pragma unroll
@@ -90,17 +93,17 @@ __global__ __launch_bounds__(256) void dattorro_predelay_v1(DattorroArgs a) {
             const float l = a.in[(size_t)(f0 + k) * n + i];
             x[k] = stereo ? (l + a.in[plane + (size_t)(f0 + k) * n + i]) / 2 : l;
         }
-        *(float4 *)(ring + ((a.t0 + f0) & (kPreSize - 1u))) = make_float4(x[0], x[1], x[2], x[3]);
-    }
-    float4 *blk = (float4 *)a.pre_block;
-    uint32_t q = a.t0 - d;
-    float4 cur = *(const float4 *)(ring + (q & ~3u & (kPreSize - 1u)));
-    for (uint32_t f0 = 0; f0 < a.n_frames; f0 += 4, q += 4) {
-        const float4 nxt = *(const float4 *)(ring + ((q & ~3u) + 4u & (kPreSize - 1u)));
+        const uint32_t t = a.t0 + f0, q = t - d, g = q & ~3u;
+        const float4 pa = *(const float4 *)(ring_r + (g & (kPreSize - 1u)));
+        const float4 pb = *(const float4 *)(ring_r + ((g + 4u) & (kPreSize - 1u)));
         float v[4];
-        olfx::dt::shift4(q & 3u, cur, nxt, v);
+        olfx::dt::shift4(q & 3u, pa, pb, v);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {                  // positions inside this chunk: d <= k
+            if (d <= (uint32_t)k) v[k] = x[k - (int)d];
+        }
         blk[(size_t)(f0 >> 2) * n + i] = make_float4(v[0], v[1], v[2], v[3]);
-        cur = nxt;
+        *(float4 *)(ring + (t & (kPreSize - 1u))) = make_float4(x[0], x[1], x[2], x[3]);
     }
 }
 
