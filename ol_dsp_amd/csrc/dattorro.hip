@@ -98,10 +98,11 @@ __global__ __launch_bounds__(256) void dattorro_predelay_v1(DattorroArgs a) {
         const float4 pb = *(const float4 *)(ring_r + ((g + 4u) & (kPreSize - 1u)));
         float v[4];
         olfx::dt::shift4(q & 3u, pa, pb, v);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {                  // positions inside this chunk: d <= k
-            if (d <= (uint32_t)k) v[k] = x[k - (int)d];
-        }
+        // positions inside this chunk (d <= k): x[k - d], by selects (no indexed register access)
+        v[0] = d == 0u ? x[0] : v[0];
+        v[1] = d == 0u ? x[1] : (d == 1u ? x[0] : v[1]);
+        v[2] = d == 0u ? x[2] : (d == 1u ? x[1] : (d == 2u ? x[0] : v[2]));
+        v[3] = d == 0u ? x[3] : (d == 1u ? x[2] : (d == 2u ? x[1] : (d == 3u ? x[0] : v[3])));
         blk[(size_t)(f0 >> 2) * n + i] = make_float4(v[0], v[1], v[2], v[3]);
         *(float4 *)(ring + (t & (kPreSize - 1u))) = make_float4(x[0], x[1], x[2], x[3]);
     }
