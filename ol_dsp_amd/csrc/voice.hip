@@ -35,6 +35,17 @@ __device__ __forceinline__ float polyblep(float dt, float t) {
     return lo ? rlo : (hi ? rhi : 0.0f);
 }
 
+// the same residual with the quadratics contracted (voice_block_v5 under OLFX_VOICE_FMA)
+__device__ __forceinline__ float polyblep_fma(float dt, float t) {
+    const bool lo = t < dt, hi = !lo && t > 1.0f - dt;
+    const float q = (lo ? t : t - 1.0f) * __builtin_amdgcn_rcpf(dt);
+    const float q2 = q + q;
+    float rlo = __builtin_fmaf(-q, q, q2) - 1.0f;
+    float rhi = __builtin_fmaf(q, q, q2) + 1.0f;
+    asm volatile("" : "+v"(rlo), "+v"(rhi));
+    return lo ? rlo : (hi ? rhi : 0.0f);
+}
+
 // sin(x) for x in [0, pi/4] (Svf::SetFreq's argument pi * min(0.25, fc / 2sr)): odd Taylor
 // polynomial to x^9, truncation < 2e-9, i.e. within an ulp of sinf; branch-free.  The voice's
 // parity tolerance (1e-5 of max(|ref|, rms), tests/test_gpu_parity.py) covers ulp-level
@@ -46,6 +57,13 @@ __device__ __forceinline__ float sin_quarter(float x) {
     p = p * x2 + 8.3333333e-3f;              // 1/5!
     p = p * x2 + -1.6666667e-1f;             // -1/3!
     return x + (x * x2) * p;
+}
+__device__ __forceinline__ float sin_quarter_fma(float x) {
+    const float x2 = x * x;
+    float p = __builtin_fmaf(2.7557319e-6f, x2, -1.9841270e-4f);
+    p = __builtin_fmaf(p, x2, 8.3333333e-3f);
+    p = __builtin_fmaf(p, x2, -1.6666667e-1f);
+    return __builtin_fmaf(x * x2, p, x);
 }
 
 // packed FP32 (v_pk_mul_f32 / v_pk_add_f32: two IEEE operations per lane and instruction, the same
@@ -170,7 +188,11 @@ struct Env {
         return x;
     }
     __device__ __forceinline__ float step() {
+#if OLFX_VOICE_FMA
+        const float xn = __builtin_fmaf(d0, tgt - x, x);
+#else
         const float xn = x + d0 * (tgt - x);
+#endif
         const bool ends = xn > hi || xn < lo;
         x = __builtin_amdgcn_fmed3f(xn, lo, hi);
         if (__builtin_amdgcn_ballot_w64(ends)) {       // rare, wave-uniform: a segment ended
@@ -195,6 +217,9 @@ struct Env {
 #define OLFX_VC_CHUNK 8
 #endif
 constexpr int kVcChunk = OLFX_VC_CHUNK;
+#ifndef OLFX_VOICE_FMA
+#define OLFX_VOICE_FMA 0
+#endif
 
 // Runs f(j) for the m samples of a chunk: unrolled when the chunk is full, so the off-recurrence
 // work of neighbouring samples interleaves (ILP for a wave that is alone on its SIMD).
@@ -377,19 +402,20 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
 // voice_block_v5 (SvfFilter voices): v4's arithmetic, operation for operation, over
 // FOUR role waves per workgroup of 64 voices (two workgroups per CU, two waves per SIMD):
 //   ENV  : the amp and filter Adsr, the cutoff sum                            -> (amp, fc_in)
-//   OSC  : Port, the oscillator's phase, the polyBLEP saw                     -> (src, amp)
+//   OSC  : Port, the oscillator's phase, the polyBLEP saw                     -> src
 //   FREQ : Svf::SetFreq(fc_in)                                                -> (-damp, fq)
 //   FILT : the two Svf passes, Low() * amp, the output store
 // A three-stage pipeline over 8-sample chunks (kVcChunk): at step k ENV makes chunk k, OSC and FREQ chunk
-// k-1, FILT chunk k-2; one barrier per step; 24 KB of LDS per workgroup.  Measured per role (16-sample chunks,
+// k-1, FILT chunk k-2 (and reads that chunk's amp straight from ENV's queue, which holds three
+// chunks); one barrier per step; 24 KB of LDS per workgroup.  Measured per role (16-sample chunks,
 // 18 steps; the others skipping their arithmetic): the skeleton (launch, state,
 // 18 barriers) 9.7 us, FREQ 10.0, FILT 15, OSC 20, ENV 26 of the kernel's 43.6 us.  The envelopes
 // of a full chunk run speculatively (Env::step_spec, no per-sample lane vote and branch) and the
 // chunk is redone exactly when a lane's segment ended in it.  Roles are assigned by SIMD (below).
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
-    __shared__ float2 eq[2][kVcChunk][64];      // ENV -> OSC, FREQ: (amp, fc_in)
-    __shared__ float2 sq[2][kVcChunk][64];      // OSC -> FILT: (src, amp)
+    __shared__ float2 eq[3][kVcChunk][64];      // ENV -> OSC, FREQ (fc_in), FILT (amp): three chunks live
+    __shared__ float sq[2][kVcChunk][64];       // OSC -> FILT: src
     __shared__ float2 fdq[2][kVcChunk][64];     // FREQ -> FILT: (-damp, fq)
     __shared__ uint2 evslot[64];                // ENV's staging of the block's events (OSC reads it)
     __shared__ uint32_t hw_simd[5];             // the SIMD of each wave; [4]: wave 0's slot parity
@@ -453,7 +479,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                  c[VCC_ATK_TGT_F * n + i], c[VCC_DEC_D0F * n + i], c[VCC_REL_D0F * n + i], c[VCC_SUS_F * n + i]);
         for (uint32_t k = 0; k < nsteps; ++k) {
             if (k + 2 < nsteps) {
-                float2 *qo = &eq[k & 1][0][lane];
+                float2 *qo = &eq[k % 3][0][lane];
                 if (len(k) == (uint32_t)kVcChunk) {
                     // Full chunk: the envelopes run speculatively with no per-sample segment test
                     // (a branch on a lane vote per sample serialised the chunk); if any lane's
@@ -467,11 +493,19 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     const f2 D0 = {ea.d0, ef.d0}, T = {ea.tgt, ef.tgt}, AMT = {amp_amt, 20000.0f};
 #pragma unroll
                     for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) {
+#if OLFX_VOICE_FMA
+                        const f2 xn = __builtin_elementwise_fma(D0, T - X, X);
+#else
                         const f2 xn = X + D0 * (T - X);
+#endif
                         ended = ended || xn.x > ea.hi || xn.x < ea.lo || xn.y > ef.hi || xn.y < ef.lo;
                         X = xn;
                         const f2 m = X * AMT;
+#if OLFX_VOICE_FMA
+                        qo[j * 64] = make_float2(m.x, __builtin_fmaf(m.y, fenv_amt, cutoff));
+#else
                         qo[j * 64] = make_float2(m.x, cutoff + m.y * fenv_amt);
+#endif
                     }
                     ea.x = X.x;
                     ef.x = X.y;
@@ -481,14 +515,22 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                         for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) {
                             const float amp = ea.step() * amp_amt;
                             const float fe = ef.step();
+#if OLFX_VOICE_FMA
+                            qo[j * 64] = make_float2(amp, __builtin_fmaf(fe * 20000.0f, fenv_amt, cutoff));
+#else
                             qo[j * 64] = make_float2(amp, cutoff + ((fe * 20000.0f) * fenv_amt));
+#endif
                         }
                     }
                 } else {
                     for_chunk(len(k), [&](uint32_t j) {
                         const float amp = ea.step() * amp_amt;
                         const float fe = ef.step();
+#if OLFX_VOICE_FMA
+                        qo[j * 64] = make_float2(amp, __builtin_fmaf(fe * 20000.0f, fenv_amt, cutoff));
+#else
                         qo[j * 64] = make_float2(amp, cutoff + ((fe * 20000.0f) * fenv_amt));
+#endif
                     });
                 }
             }
@@ -516,8 +558,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                 }
             }
             if (k >= 1 && k + 1 < nsteps) {
-                const float2 *qi = &eq[(k - 1) & 1][0][lane];
-                float2 *qo = &sq[(k - 1) & 1][0][lane];
+                float *qo = &sq[(k - 1) & 1][0][lane];
                 if (len(k - 1) == (uint32_t)kVcChunk) {
                     // only Port and the phase are recurrences: run them for the chunk, then the
                     // polyBLEP saw per sample over four packed sample pairs (stage by stage, as FREQ)
@@ -527,7 +568,11 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     for (int q = 0; q < P; ++q) {
 #pragma unroll
                         for (int h = 0; h < 2; ++h) {
+#if OLFX_VOICE_FMA
+                            port_z = __builtin_fmaf(port_c, port_z - freq, freq);   // Port::Process (Portamento.h:218-221)
+#else
                             port_z = freq + port_c * (port_z - freq);     // Port::Process (Portamento.h:218-221)
+#endif
                             const float inc = port_z * inv_sr;             // Oscillator::SetFreq
                             t[q][h] = phase;                               // Oscillator::Process reads, then advances
                             dt[q][h] = inc;
@@ -551,6 +596,25 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
 #pragma unroll
                     for (int q = 0; q < P; ++q)
                         qv[q] = num[q] * (f2){__builtin_amdgcn_rcpf(dt[q].x), __builtin_amdgcn_rcpf(dt[q].y)};
+#if OLFX_VOICE_FMA
+                    // q + q - q q - 1 and q q + q + q + 1 as fma(-q, q, 2q) - 1 and fma(q, q, 2q) + 1
+#pragma unroll
+                    for (int q = 0; q < P; ++q) qq[q] = qv[q] + qv[q];
+#pragma unroll
+                    for (int q = 0; q < P; ++q) {
+                        rlo[q] = __builtin_elementwise_fma(-qv[q], qv[q], qq[q]);
+                        rhi[q] = __builtin_elementwise_fma(qv[q], qv[q], qq[q]);
+                    }
+#pragma unroll
+                    for (int q = 0; q < P; ++q) { rlo[q] = rlo[q] - 1.0f; rhi[q] = rhi[q] + 1.0f; o[q] = __builtin_elementwise_fma((f2)2.0f, t[q], (f2)-1.0f); }
+#pragma unroll
+                    for (int q = 0; q < P; ++q) {
+                        f2 blep;
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) blep[h] = lo[q][h] ? rlo[q][h] : (hi[q][h] ? rhi[q][h] : 0.0f);
+                        o[q] = o[q] - blep;
+                    }
+#else
 #pragma unroll
                     for (int q = 0; q < P; ++q) qq[q] = qv[q] * qv[q];
 #pragma unroll
@@ -566,24 +630,33 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                         for (int h = 0; h < 2; ++h) blep[h] = lo[q][h] ? rlo[q][h] : (hi[q][h] ? rhi[q][h] : 0.0f);
                         o[q] = (o[q] - 1.0f) - blep;
                     }
+#endif
 #pragma unroll
                     for (int q = 0; q < P; ++q) {
                         // o *= -1; o * 0.5 (== o * -0.5 exactly)
                         const f2 y = (-o[q]) * 0.5f;
-                        qo[(2 * q) * 64] = make_float2(y.x, qi[(2 * q) * 64].x);
-                        qo[(2 * q + 1) * 64] = make_float2(y.y, qi[(2 * q + 1) * 64].x);
+                        qo[(2 * q) * 64] = y.x;
+                        qo[(2 * q + 1) * 64] = y.y;
                     }
                 } else {
                     for (uint32_t j = 0; j < len(k - 1); ++j) {
+#if OLFX_VOICE_FMA
+                        port_z = __builtin_fmaf(port_c, port_z - freq, freq);
+#else
                         port_z = freq + port_c * (port_z - freq);
+#endif
                         const float inc = port_z * inv_sr;
                         const float t = phase;
                         phase += inc;
                         phase = phase > 1.0f ? phase - 1.0f : phase;
                         float o = (2.0f * t) - 1.0f;
+#if OLFX_VOICE_FMA
+                        o -= polyblep_fma(inc, t);
+#else
                         o -= polyblep(inc, t);
+#endif
                         o *= -1.0f;
-                        qo[j * 64] = make_float2(o * 0.5f, qi[j * 64].x);
+                        qo[j * 64] = o * 0.5f;
                     }
                 }
             }
@@ -597,7 +670,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
         const float inv_2sr = 1.0f / (c[VCC_SR * n + i] * 2.0f);
         for (uint32_t k = 0; k < nsteps; ++k) {
             if (k >= 1 && k + 1 < nsteps) {
-                const float2 *qi = &eq[(k - 1) & 1][0][lane];
+                const float2 *qi = &eq[(k - 1) % 3][0][lane];
                 float2 *qo = &fdq[(k - 1) & 1][0][lane];
                 // hands FILT (-damp, fq): its notch src - damp band is src + (-damp) band, exactly
                 if (len(k - 1) == (uint32_t)kVcChunk) {
@@ -608,14 +681,40 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     f2 x[P], x2[P], pp[P], fq[P];
 #pragma unroll
                     for (int q = 0; q < P; ++q) {
+#if OLFX_VOICE_FMA
+                        // fminf(fmaxf(x, 1e-6), fc_max) for 1e-6 <= fc_max and a non-NaN cutoff sum
+                        const float c0 = __builtin_amdgcn_fmed3f(qi[(2 * q) * 64].y, 1.0e-6f, fc_max);
+                        const float c1 = __builtin_amdgcn_fmed3f(qi[(2 * q + 1) * 64].y, 1.0e-6f, fc_max);
+#else
                         const float c0 = fminf(fmaxf(qi[(2 * q) * 64].y, 1.0e-6f), fc_max);
                         const float c1 = fminf(fmaxf(qi[(2 * q + 1) * 64].y, 1.0e-6f), fc_max);
+#endif
                         const f2 fcn = (f2){c0, c1} * inv_2sr;
                         const f2 arg = {0.25f < fcn.x ? 0.25f : fcn.x, 0.25f < fcn.y ? 0.25f : fcn.y};
                         x[q] = 3.1415927410125732f * arg;
                     }
 #pragma unroll
                     for (int q = 0; q < P; ++q) x2[q] = x[q] * x[q];
+#if OLFX_VOICE_FMA
+#pragma unroll
+                    for (int q = 0; q < P; ++q) pp[q] = __builtin_elementwise_fma((f2)2.7557319e-6f, x2[q], (f2)-1.9841270e-4f);
+#pragma unroll
+                    for (int q = 0; q < P; ++q) pp[q] = __builtin_elementwise_fma(pp[q], x2[q], (f2)8.3333333e-3f);
+#pragma unroll
+                    for (int q = 0; q < P; ++q) pp[q] = __builtin_elementwise_fma(pp[q], x2[q], (f2)-1.6666667e-1f);
+#pragma unroll
+                    for (int q = 0; q < P; ++q) x2[q] = x[q] * x2[q];
+#pragma unroll
+                    for (int q = 0; q < P; ++q) fq[q] = 2.0f * __builtin_elementwise_fma(x2[q], pp[q], x[q]);
+#pragma unroll
+                    for (int q = 0; q < P; ++q) {
+                        const f2 rq = {__builtin_amdgcn_rcpf(fq[q].x), __builtin_amdgcn_rcpf(fq[q].y)};
+                        const f2 lim = __builtin_elementwise_fma((f2)2.0f, rq, fq[q] * -0.5f);
+                        const float d0 = 2.0f < lim.x ? 2.0f : lim.x, d1 = 2.0f < lim.y ? 2.0f : lim.y;
+                        qo[(2 * q) * 64] = make_float2(-(damp_res < d0 ? damp_res : d0), fq[q].x);
+                        qo[(2 * q + 1) * 64] = make_float2(-(damp_res < d1 ? damp_res : d1), fq[q].y);
+                    }
+#else
 #pragma unroll
                     for (int q = 0; q < P; ++q) pp[q] = (f2)2.7557319e-6f * x2[q];
 #pragma unroll
@@ -642,13 +741,22 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                         qo[(2 * q) * 64] = make_float2(-(damp_res < d0 ? damp_res : d0), fq[q].x);
                         qo[(2 * q + 1) * 64] = make_float2(-(damp_res < d1 ? damp_res : d1), fq[q].y);
                     }
+#endif
                 } else {
                     for (uint32_t j = 0; j < len(k - 1); ++j) {
+#if OLFX_VOICE_FMA
+                        const float fc = __builtin_amdgcn_fmed3f(qi[j * 64].y, 1.0e-6f, fc_max);
+                        const float fcn = fc * inv_2sr;
+                        const float arg = 0.25f < fcn ? 0.25f : fcn;
+                        const float fq = 2.0f * sin_quarter_fma(3.1415927410125732f * arg);
+                        const float lim = __builtin_fmaf(2.0f, __builtin_amdgcn_rcpf(fq), fq * -0.5f);
+#else
                         const float fc = fminf(fmaxf(qi[j * 64].y, 1.0e-6f), fc_max);
                         const float fcn = fc * inv_2sr;
                         const float arg = 0.25f < fcn ? 0.25f : fcn;
                         const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
                         const float lim = 2.0f * __builtin_amdgcn_rcpf(fq) - fq * 0.5f;
+#endif
                         const float dlim = 2.0f < lim ? 2.0f : lim;
                         qo[j * 64] = make_float2(-(damp_res < dlim ? damp_res : dlim), fq);
                     }
@@ -664,13 +772,28 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
         for (uint32_t k = 0; k < nsteps; ++k) {
             if (k >= 2) {
                 const uint32_t f0 = (k - 2) * kVcChunk;
-                const float2 *qs = &sq[k & 1][0][lane];        // chunk k-2: (k-2) & 1 == k & 1
+                const float *qs = &sq[k & 1][0][lane];         // chunk k-2: (k-2) & 1 == k & 1
+                const float2 *qa = &eq[(k - 2) % 3][0][lane];
                 const float2 *qf = &fdq[k & 1][0][lane];
                 for_chunk(len(k - 2), [&](uint32_t j) {
-                    const float2 sa = qs[j * 64], fd = qf[j * 64];
+                    const float2 fd = qf[j * 64];
+                    const float2 sa = make_float2(qs[j * 64], qa[j * 64].x);
                     // (packing this serial recurrence's paired products cost as many register
                     // moves as it saved operations: scalar)
                     const float src = sa.x, ndamp = fd.x, fq = fd.y;     // FREQ hands over -damp
+#if OLFX_VOICE_FMA
+                    // contracted as the firmware's compiler contracts a * b + c (7 operations a pass)
+                    float notch = __builtin_fmaf(ndamp, band, src);
+                    low = __builtin_fmaf(fq, band, low);
+                    float high = notch - low;
+                    band = __builtin_fmaf(-((drive * band) * band), band, __builtin_fmaf(fq, high, band));
+                    float out_low = 0.5f * low;
+                    notch = __builtin_fmaf(ndamp, band, src);
+                    low = __builtin_fmaf(fq, band, low);
+                    high = notch - low;
+                    band = __builtin_fmaf(-((drive * band) * band), band, __builtin_fmaf(fq, high, band));
+                    out_low = __builtin_fmaf(0.5f, low, out_low);
+#else
                     float notch = src + ndamp * band;                    // == src - damp * band
                     low = low + fq * band;
                     float high = notch - low;
@@ -681,6 +804,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     high = notch - low;
                     band = fq * high + band - drive * band * band * band;
                     out_low += 0.5f * low;
+#endif
                     out[(size_t)(f0 + j) * n] = out_low * sa.y;
                 });
             }

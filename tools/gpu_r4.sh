@@ -9,6 +9,8 @@
 #   tr:<workload>        HBM traffic passes (tools/traffic_r2.sh)
 #   bench                the driver's default line
 #   ab:<workload>        A/B: the workload under OLFX_CHORUS_KERNEL=11 and the default, twice each
+#   tl:<lib>:<k>         GPU tests matching <k> against an experimental build (OLFX_LIB=<lib>)
+#   abl:<workload>:<lib> A/B of the main build against <lib> (tools/ab.sh)
 set -u
 out=gpurun_out
 mkdir -p "$out"
@@ -30,6 +32,14 @@ for m in "$@"; do
       k=${m#t:}
       step "pytest_$(echo "$k" | tr -c 'a-zA-Z0-9_' '_')" 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider \
           --timeout 120 --timeout-method thread -k "$k" ;;
+    tl:*)
+      r=${m#tl:}; lib=${r%%:*}; k=${r#*:}
+      step "pytest_lib_$(echo "$k" | tr -c 'a-zA-Z0-9_' '_')" 600 env OLFX_LIB=$PWD/$lib python -u -m pytest tests -m gpu -x -v \
+          -p no:cacheprovider --timeout 120 --timeout-method thread -k "$k" ;;
+    abl:*)
+      r=${m#abl:}; w=${r%%:*}; lib=${r#*:}
+      step "abl_$w" 600 bash tools/ab.sh "$w" main "$lib"
+      cat "$out/abl_$w.log" ;;
     tests)
       step pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
       step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
