@@ -768,10 +768,13 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
         // ---- FILT: Svf::Process; Low() = the average of the two passes' low outputs; * amp ----
         const float drive = c[VCC_DRIVE * n + i];
         float low = s[VCS_LOW * n + i], band = s[VCS_BAND * n + i];
-        float *out = a.out + i;
         for (uint32_t k = 0; k < nsteps; ++k) {
             if (k >= 2) {
                 const uint32_t f0 = (k - 2) * kVcChunk;
+                // the chunk's output rows through a buffer resource based at row f0: the row offset
+                // j n 4 is a scalar (soffset), so a store costs no vector address arithmetic
+                const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+                    a.out + (size_t)f0 * n, (short)0, (int)((uint32_t)kVcChunk * n * 4u), 0x00020000);
                 const float *qs = &sq[k & 1][0][lane];         // chunk k-2: (k-2) & 1 == k & 1
                 const float2 *qa = &eq[(k - 2) % 3][0][lane];
                 const float2 *qf = &fdq[k & 1][0][lane];
@@ -805,7 +808,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     band = fq * high + band - drive * band * band * band;
                     out_low += 0.5f * low;
 #endif
-                    out[(size_t)(f0 + j) * n] = out_low * sa.y;
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(out_low * sa.y), ro, i * 4u, j * n * 4u, 0);
                 });
             }
             __syncthreads();
@@ -817,6 +820,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
 
 hipError_t launch_voice(const VoiceArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
+    if ((uint64_t)kVcChunk * a.n * 4u > 0xFFFFFFFFull) return hipErrorInvalidValue;   // v5's chunk output resource
     const dim3 grid((a.n + 63) / 64);     // 64 voices per workgroup, one wave per role
     if (a.moog) hipLaunchKernelGGL(voice_block_v4, grid, dim3(128), 0, s, a);
     else hipLaunchKernelGGL(voice_block_v5, grid, dim3(256), 0, s, a);
