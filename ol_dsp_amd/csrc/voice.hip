@@ -299,11 +299,19 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
                     if constexpr (AMP) {
                         const float amp = ea.step() * amp_amt;
                         // Port::Process (Portamento.h:218-221), Oscillator::SetFreq: inc = f * sr_recip
+#if OLFX_VOICE_FMA
+                        port_z = __builtin_fmaf(port_c, port_z - freq, freq);
+#else
                         port_z = freq + port_c * (port_z - freq);
+#endif
                         const float inc = port_z * inv_sr;
                         // Oscillator::Process, WAVE_POLYBLEP_SAW
                         float o = (2.0f * phase) - 1.0f;
+#if OLFX_VOICE_FMA
+                        o -= polyblep_fma(inc, phase);
+#else
                         o -= polyblep(inc, phase);
+#endif
                         o *= -1.0f;
                         phase += inc;
                         phase = phase > 1.0f ? phase - 1.0f : phase;
@@ -312,12 +320,21 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
                     }
                     if constexpr (CUT) {
                         const float fe = ef.step();
+#if OLFX_VOICE_FMA
+                        const float fc_in = __builtin_fmaf(fe * 20000.0f, fenv_amt, cutoff);
+                        const float wc = fc_in * 2.0f * 3.1415927410125732f * fc_max;
+                        const float wc2 = wc * wc;
+                        // the same polynomials in Horner form
+                        cd.x = wc * __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(-0.0202f, wc, 0.1381f), wc, -0.4324f), wc, 0.9892f);
+                        cd.y = __builtin_fmaf(__builtin_fmaf(-0.05f, wc2, -0.095f), wc2, __builtin_fmaf(0.0536f, wc, 1.006f));
+#else
                         const float fc_in = cutoff + ((fe * 20000.0f) * fenv_amt);
                         // LadderFilter::SetFreq (unclamped) -> SetAlpha
                         const float wc = fc_in * 2.0f * 3.1415927410125732f * fc_max;
                         const float wc2 = wc * wc;
                         cd.x = 0.9892f * wc - 0.4324f * wc2 + 0.1381f * wc * wc2 - 0.0202f * wc2 * wc2;
                         cd.y = 1.006f + 0.0536f * wc - 0.095f * wc2 - 0.05f * wc2 * wc2;
+#endif
                     }
                     if constexpr (AMP && CUT) {
                         qb[j * 64] = make_float4(ab.x, ab.y, cd.x, cd.y);
@@ -364,6 +381,36 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
                 for_chunk(m, [&](uint32_t j) {
                     const float4 v = qb[j * 64];
                     float y;
+#if OLFX_VOICE_FMA
+                    {
+                        // contracted as the firmware's compiler contracts a * b + c; the Pade tanh
+                        // as r(med3(x, -3, 3)) (r(+-3) = +-1 exactly: the saturation, branch-free)
+                        // with a hardware reciprocal
+                        const float input = v.x, alpha = v.z, kq = k_or_unused * v.w;
+                        const float fb0 = -0.5f * input;
+                        float total = 0.0f;
+#pragma unroll
+                        for (int os = 0; os < 4; ++os) {
+                            const float interp = 0.25f * (float)os;
+                            const float mixin = __builtin_fmaf(interp, L.old, (1.0f - interp) * input);
+                            float x = __builtin_fmaf(-(L.z1[3] + fb0), kq, mixin);
+                            x = __builtin_amdgcn_fmed3f(x, -3.0f, 3.0f);
+                            const float x2 = x * x;
+                            float u = (x * (27.0f + x2)) * __builtin_amdgcn_rcpf(__builtin_fmaf(9.0f, x2, 27.0f));
+#pragma unroll
+                            for (int st = 0; st < 4; ++st) {
+                                float ft = __builtin_fmaf(u, 1.0f / 1.3f, __builtin_fmaf(0.3f / 1.3f, L.z0[st], -L.z1[st]));
+                                ft = __builtin_fmaf(ft, alpha, L.z1[st]);
+                                L.z1[st] = ft;
+                                L.z0[st] = u;
+                                u = ft;
+                            }
+                            total = __builtin_fmaf(u, 0.25f, total);
+                        }
+                        L.old = input;
+                        y = total * v.y;
+                    }
+#else
                     {
                         // LadderFilter::Process, LP24
                         const float input = v.x, alpha = v.z, qadj = v.w;
@@ -383,6 +430,7 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
                         L.old = input;
                         y = total * v.y;
                     }
+#endif
                     out[(size_t)(f0 + j) * n] = y;
                 });
             }
