@@ -144,8 +144,11 @@ int forced_kernel() {
     }();
     return k;
 }
+// The block-at-once kernels run only when forced: measured on MI355X (65,536 instances, same box)
+// the chorus v14 takes 0.324-0.328 ms against v11's 0.234-0.241.
 bool v13_geometry(uint32_t n, uint32_t psize, uint32_t csize) {
-    return forced_kernel() != 11 && (n & 3u) == 0 && psize == cb::kPsize && csize == cb::kCsize;
+    const int f = forced_kernel();
+    return (f == 13 || f == 14) && (n & 3u) == 0 && psize == cb::kPsize && csize == cb::kCsize;
 }
 // the block-at-once kernel for a mode: the chorus v14 (v13 when forced), the pitch-shifter v13
 int block_kernel(uint32_t mode) {

@@ -15,6 +15,9 @@
 // hands the network its pre-delayed block as a coalesced stream (PreBlock).  The network itself
 // then reads no input and writes no pre-delay ring.
 #include "dattorro_stage.h"
+#include "chorus_stage.h"
+
+#include <cstdlib>
 
 namespace olfx {
 
@@ -108,6 +111,143 @@ __global__ __launch_bounds__(256) void dattorro_predelay_v1(DattorroArgs a) {
     }
 }
 
+// dattorro_predelay_v2: v1's pass with whole 128-B lines.  v1 moved 16-B pieces, one per lane and
+// 4-frame chunk, each in its own line (64 lines per instruction; a line touched by 8 chunks):
+// 0.78 ms for the gather-mode reverb against 0.54 uniform.  One wave per workgroup = 64 instances,
+// 32-frame chunks aligned to the ring's lines (chunk positions [T, T + 32), T % 32 == 0):
+//   - a chunk's ring write is exactly one line per instance, stored cooperatively (8 lanes x 16 B
+//     per line, 8 lines per instruction) from the LDS history `hist`;
+//   - its pre-delayed reads [T - d, T - d + 32) lie in two lines Lq = (T - d) / 32 and Lq + 1; the
+//     window `win` holds both in LDS, and each chunk loads only the next one (Lq + 2, cooperatively,
+//     one chunk ahead), since the window advances by exactly one line per chunk;
+//   - positions >= T - 32 (d <= k + 32) come from `hist`, which holds the previous chunk's and this
+//     chunk's inputs.  The line prefetched during chunk c was issued before chunk c's ring store:
+//     every earlier chunk's store precedes it, so its only possibly stale positions are chunk c's
+//     own line [T, T + 32) -- when it is that line, hist's copy replaces it.
+// Frames outside [t0, t0 + n_frames) in the first and last chunks are neither stored nor output;
+// the first chunk's history positions [T, t0) and [T - 32, T) are loaded into `hist` from the ring.
+// The pre-delayed block goes out as [F/4][n][4] (coalesced), as v1's.
+namespace {
+constexpr uint32_t kPdLine = 32;                   // positions per 128-B line
+constexpr uint32_t kPdLines = kPreSize / kPdLine;   // 256
+constexpr uint32_t kPdRow = 65;                    // LDS floats per instance row (odd: lanes spread over banks)
+}
+
+__global__ __launch_bounds__(64) void dattorro_predelay_v2(DattorroArgs a) {
+    __shared__ float hist[64 * kPdRow];            // [instance][P & 63]: inputs of positions [T - 32, T + 32)
+    __shared__ float win[64 * kPdRow];             // [instance][P & 63]: ring lines Lq, Lq + 1
+    const uint32_t lane = threadIdx.x, n = a.n, F = a.n_frames, t0 = a.t0;
+    const uint32_t i0 = blockIdx.x * 64u, i = i0 + lane, nv = min(n - i0, 64u);
+    const bool live = i < n;
+    const bool stereo = a.in_ch == 2;
+    const uint32_t d = (uint32_t)a.coef[DTC_PREDELAY * n + min(i, n - 1u)];
+    // cooperative line accesses: in instruction m, lane L serves instance 8 m + L / 8, piece L % 8
+    const uint32_t pc = lane & 7u;
+    uint32_t dj[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) dj[m] = (uint32_t)a.coef[DTC_PREDELAY * n + min(i0 + 8u * m + (lane >> 3), n - 1u)];
+    const ch::Rsrc rRing = ch::rsrc(a.pre_im + (size_t)i0 * kPreSize, (uint64_t)nv * kPreSize * 4u);
+    auto line_off = [&](int m, uint32_t line) {    // byte offset of piece pc of instance 8 m + L / 8's line
+        const uint32_t j = 8u * (uint32_t)m + (lane >> 3);
+        return j < nv ? j * kPreSize * 4u + (line & (kPdLines - 1u)) * 128u + pc * 16u : 0xFFFFFFF0u;
+    };
+    auto to_lds = [&](float *dst, int m, uint32_t line, float4 v) {   // piece -> row slot (line & 1) * 32 + 4 pc
+        float *r = dst + (8u * (uint32_t)m + (lane >> 3)) * kPdRow + (line & 1u) * kPdLine + 4u * pc;
+        r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+    };
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // input frame rows: f = T + k - t0, loaded when 0 <= f < F (else 0 through an out-of-range offset)
+    const ch::Rsrc rIn0 = ch::rsrc(a.in, ((uint64_t)F * n) * 4u);
+    const ch::Rsrc rIn1 = ch::rsrc(stereo ? a.in + a.plane : a.in, ((uint64_t)F * n) * 4u);
+    auto load_x = [&](uint32_t T, float (&x0)[kPdLine], float (&x1)[kPdLine]) {
+#pragma unroll
+        for (uint32_t k = 0; k < kPdLine; ++k) {
+            const uint32_t f = T + k - t0;                 // wraps above F when T + k < t0
+            const uint32_t off = f < F && live ? (f * n + i) * 4u : 0xFFFFFFF0u;
+            x0[k] = ch::ld1(rIn0, off, 0);
+            x1[k] = ch::ld1(rIn1, off, 0);
+        }
+    };
+    const uint32_t T0 = t0 & ~(kPdLine - 1u);
+    const uint32_t nch = (t0 + F - T0 + kPdLine - 1u) / kPdLine;
+    // history lines T0 / 32 - 1 and T0 / 32, window lines Lq and Lq + 1 of the first chunk
+    {
+        float4 h[2][8], w[2][8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            h[0][m] = ch::ld4(rRing, line_off(m, T0 / kPdLine - 1u));
+            h[1][m] = ch::ld4(rRing, line_off(m, T0 / kPdLine));
+            w[0][m] = ch::ld4(rRing, line_off(m, (T0 - dj[m]) / kPdLine));
+            w[1][m] = ch::ld4(rRing, line_off(m, (T0 - dj[m]) / kPdLine + 1u));
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            to_lds(hist, m, T0 / kPdLine - 1u, h[0][m]);
+            to_lds(hist, m, T0 / kPdLine, h[1][m]);
+            to_lds(win, m, (T0 - dj[m]) / kPdLine, w[0][m]);
+            to_lds(win, m, (T0 - dj[m]) / kPdLine + 1u, w[1][m]);
+        }
+    }
+    float x0[kPdLine], x1[kPdLine];
+    load_x(T0, x0, x1);
+    const ch::Rsrc rBlk = ch::rsrc(a.pre_block, (uint64_t)F * n * 4u);
+    float *hrow = hist + lane * kPdRow, *wrow = win + lane * kPdRow;
+    for (uint32_t c = 0; c < nch; ++c) {
+        const uint32_t T = T0 + c * kPdLine;
+        // the next chunk's window line and inputs, issued before this chunk's ring store
+        float4 nl[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) nl[m] = ch::ld4(rRing, line_off(m, (T - dj[m]) / kPdLine + 2u));
+        float n0[kPdLine], n1[kPdLine];
+        load_x(T + kPdLine, n0, n1);
+        // this chunk's mono input (l + r) / 2 into the history (positions before t0 keep the ring's)
+#pragma unroll
+        for (uint32_t k = 0; k < kPdLine; ++k) {
+            const float xm = stereo ? (x0[k] + x1[k]) / 2 : x0[k];
+            if (T + k - t0 < F) hrow[(T + k) & 63u] = xm;
+        }
+        wave_sync();
+        // the pre-delayed samples: positions T + k - d, from the history when >= T - 32
+        float v[kPdLine];
+        const uint32_t q = T - d;
+#pragma unroll
+        for (uint32_t k = 0; k < kPdLine; ++k) {
+            const float *src = d <= k + kPdLine ? hrow + ((T + k - d) & 63u) : wrow + ((q + k) & 63u);
+            v[k] = *src;
+        }
+#pragma unroll
+        for (uint32_t g = 0; g < kPdLine / 4u; ++g) {
+            const uint32_t f = T + 4u * g - t0;            // a group is wholly inside or outside (t0 % 4 == 0)
+            ch::st4(rBlk, f < F && live ? ((f >> 2) * n + i) * 16u : 0xFFFFFFF0u,
+                make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]));
+        }
+        // the chunk's ring line, cooperatively from the history (pieces outside the block dropped)
+        float4 hv[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const float *r = hist + (8u * (uint32_t)m + (lane >> 3)) * kPdRow + (T & 63u) + 4u * pc;
+            hv[m] = make_float4(r[0], r[1], r[2], r[3]);
+            const uint32_t f = T + 4u * pc - t0;
+            ch::st4(rRing, f < F ? line_off(m, T / kPdLine) : 0xFFFFFFF0u, hv[m]);
+        }
+        wave_sync();
+        // the window advances one line: Lq + 2 replaces Lq (its reads are done); if Lq + 2 is this
+        // chunk's own line, its prefetch predates the store above: hist's copy instead
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const uint32_t l2 = (T - dj[m]) / kPdLine + 2u;
+            to_lds(win, m, l2, ((l2 ^ (T / kPdLine)) & (kPdLines - 1u)) == 0u ? hv[m] : nl[m]);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kPdLine; ++k) { x0[k] = n0[k]; x1[k] = n1[k]; }
+        wave_sync();
+    }
+}
+
 // the pre-delay ring between layouts: position-major groups [size/4][n][4] <-> instance-major
 // [n][size]; one thread per (group, instance), reads or writes coalesced on the position-major side
 __global__ __launch_bounds__(256) void dattorro_pre_convert(DattorroArgs a, int to_im) {
@@ -119,6 +259,17 @@ __global__ __launch_bounds__(256) void dattorro_pre_convert(DattorroArgs a, int 
     else *pm = *im;
 }
 
+namespace {
+// OLFX_PREDELAY_KERNEL=1 runs v1 (A/B diagnostic)
+bool predelay_v1() {
+    static const bool v = [] {
+        const char *e = std::getenv("OLFX_PREDELAY_KERNEL");
+        return e && std::atoi(e) == 1;
+    }();
+    return v;
+}
+}  // namespace
+
 hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
     if ((a.t0 & 3u) || (a.n_frames & 3u)) return hipErrorInvalidValue;   // 4-frame chunks
@@ -128,7 +279,12 @@ hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s) {
     const uint32_t threads = 64;      // one wave per workgroup: spreads small engines over all CUs
     const uint32_t blocks = (a.n + threads - 1) / threads;
     if (a.pre_im) {
-        hipLaunchKernelGGL(dattorro_predelay_v1, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+        // per-workgroup ring resources: 64 instances x 32 KB; inputs and the block by 32-bit offsets
+        if ((uint64_t)a.n_frames * a.n * 4u >= (1ull << 32)) return hipErrorInvalidValue;
+        if (predelay_v1())
+            hipLaunchKernelGGL(dattorro_predelay_v1, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL(dattorro_predelay_v2, dim3((a.n + 63) / 64), dim3(64), 0, s, a);
         hipLaunchKernelGGL(dattorro_block_v4<true>, dim3(blocks), dim3(threads), 0, s, a);
     } else {
         hipLaunchKernelGGL(dattorro_block_v4<false>, dim3(blocks), dim3(threads), 0, s, a);

@@ -188,11 +188,7 @@ struct Env {
         return x;
     }
     __device__ __forceinline__ float step() {
-#if OLFX_VOICE_FMA
-        const float xn = __builtin_fmaf(d0, tgt - x, x);
-#else
         const float xn = x + d0 * (tgt - x);
-#endif
         const bool ends = xn > hi || xn < lo;
         x = __builtin_amdgcn_fmed3f(xn, lo, hi);
         if (__builtin_amdgcn_ballot_w64(ends)) {       // rare, wave-uniform: a segment ended
@@ -299,11 +295,7 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
                     if constexpr (AMP) {
                         const float amp = ea.step() * amp_amt;
                         // Port::Process (Portamento.h:218-221), Oscillator::SetFreq: inc = f * sr_recip
-#if OLFX_VOICE_FMA
-                        port_z = __builtin_fmaf(port_c, port_z - freq, freq);
-#else
                         port_z = freq + port_c * (port_z - freq);
-#endif
                         const float inc = port_z * inv_sr;
                         // Oscillator::Process, WAVE_POLYBLEP_SAW
                         float o = (2.0f * phase) - 1.0f;
@@ -541,11 +533,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     const f2 D0 = {ea.d0, ef.d0}, T = {ea.tgt, ef.tgt}, AMT = {amp_amt, 20000.0f};
 #pragma unroll
                     for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) {
-#if OLFX_VOICE_FMA
-                        const f2 xn = __builtin_elementwise_fma(D0, T - X, X);
-#else
                         const f2 xn = X + D0 * (T - X);
-#endif
                         ended = ended || xn.x > ea.hi || xn.x < ea.lo || xn.y > ef.hi || xn.y < ef.lo;
                         X = xn;
                         const f2 m = X * AMT;
@@ -616,11 +604,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     for (int q = 0; q < P; ++q) {
 #pragma unroll
                         for (int h = 0; h < 2; ++h) {
-#if OLFX_VOICE_FMA
-                            port_z = __builtin_fmaf(port_c, port_z - freq, freq);   // Port::Process (Portamento.h:218-221)
-#else
                             port_z = freq + port_c * (port_z - freq);     // Port::Process (Portamento.h:218-221)
-#endif
                             const float inc = port_z * inv_sr;             // Oscillator::SetFreq
                             t[q][h] = phase;                               // Oscillator::Process reads, then advances
                             dt[q][h] = inc;
@@ -688,11 +672,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     }
                 } else {
                     for (uint32_t j = 0; j < len(k - 1); ++j) {
-#if OLFX_VOICE_FMA
-                        port_z = __builtin_fmaf(port_c, port_z - freq, freq);
-#else
                         port_z = freq + port_c * (port_z - freq);
-#endif
                         const float inc = port_z * inv_sr;
                         const float t = phase;
                         phase += inc;

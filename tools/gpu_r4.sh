@@ -8,8 +8,9 @@
 #   p:<workload>         rocprofv3 kernel stats of that bench line (-> gpurun_out/prof_<w>)
 #   tr:<workload>        HBM traffic passes (tools/traffic_r2.sh)
 #   bench                the driver's default line
-#   ab:<workload>        A/B: the workload under OLFX_CHORUS_KERNEL=11 and the default, twice each
+#   ab:<workload>:<k>    A/B: the workload under the default and OLFX_CHORUS_KERNEL=<k>, twice each
 #   tl:<lib>:<k>         GPU tests matching <k> against an experimental build (OLFX_LIB=<lib>)
+#   te:<VAR=v>:<k>       GPU tests matching <k> with the environment variable VAR=v
 #   abl:<workload>:<lib> A/B of the main build against <lib> (tools/ab.sh)
 set -u
 out=gpurun_out
@@ -36,6 +37,10 @@ for m in "$@"; do
       r=${m#tl:}; lib=${r%%:*}; k=${r#*:}
       step "pytest_lib_$(echo "$k" | tr -c 'a-zA-Z0-9_' '_')" 600 env OLFX_LIB=$PWD/$lib python -u -m pytest tests -m gpu -x -v \
           -p no:cacheprovider --timeout 120 --timeout-method thread -k "$k" ;;
+    te:*)
+      r=${m#te:}; kv=${r%%:*}; k=${r#*:}
+      step "pytest_env_$(echo "$kv$k" | tr -c 'a-zA-Z0-9_' '_')" 600 env "$kv" python -u -m pytest tests -m gpu -x -v \
+          -p no:cacheprovider --timeout 120 --timeout-method thread -k "$k" ;;
     abl:*)
       r=${m#abl:}; w=${r%%:*}; lib=${r#*:}
       step "abl_$w" 600 bash tools/ab.sh "$w" main "$lib"
@@ -55,11 +60,11 @@ for m in "$@"; do
       w=${m#tr:}
       step "traffic_$w" 600 bash tools/traffic_r2.sh "$w" ;;
     ab:*)
-      w=${m#ab:}
+      r=${m#ab:}; w=${r%%:*}; kv=${r#*:}
       for r in 1 2; do
-        step "ab_${w}_v11_$r" 300 env OLFX_CHORUS_KERNEL=11 python bench.py --workload "$w" --also "" --steps 50 --warmup 5 \
+        step "ab_${w}_default_$r" 300 python bench.py --workload "$w" --also "" --steps 50 --warmup 5 \
             --cpu-seconds 0 --no-parity --full-json ""
-        step "ab_${w}_new_$r" 300 python bench.py --workload "$w" --also "" --steps 50 --warmup 5 --cpu-seconds 0 \
+        step "ab_${w}_k${kv}_$r" 300 env OLFX_CHORUS_KERNEL=$kv python bench.py --workload "$w" --also "" --steps 50 --warmup 5 --cpu-seconds 0 \
             --no-parity --full-json ""
       done ;;
     bench)
