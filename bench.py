@@ -326,7 +326,8 @@ def _traffic(name: str, n: int, B: int, override: str = "", kernel: str = ""):
                 with open(tj) as f:
                     tr = json.load(f)
                 kernels = tr.get("counters_per_kernel") or {}
-                same_kernel = not kernel or any(kernel in k for k in kernels)
+                # a launch sequence ("a+b") needs a summary of every kernel in it
+                same_kernel = not kernel or all(any(part in k for k in kernels) for part in kernel.split("+"))
                 if tr.get("instances") == n and tr.get("block") == B and same_kernel:
                     return tr
             except Exception:

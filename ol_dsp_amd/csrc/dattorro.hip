@@ -10,10 +10,11 @@
 // per-instance pre-delays, those groups lie in 64 different 128-B lines per wave instruction, and
 // successive chunks of a lane touch one line eight times after it has left the caches: the gather
 // read 8x its bytes (dattorro_rpd +30 %, round 3).  Gather mode (the engine switches when the
-// pre-delays differ) keeps that ring instance-major and runs dattorro_predelay_v1 ahead of the
-// block: one lane per instance walks its own ring in stream order (whole lines, in order) and
-// hands the network its pre-delayed block as a coalesced stream (PreBlock).  The network itself
-// then reads no input and writes no pre-delay ring.
+// pre-delays differ) keeps that ring instance-major and runs dattorro_predelay_v2 ahead of the
+// block: each instance's ring is read and written in whole 128-B lines (below) and the network
+// gets its pre-delayed block as a coalesced stream (PreBlock).  The network itself then reads no
+// input and writes no pre-delay ring.  Measured (65,536 instances, random pre-delays): pre-pass
+// 0.073 ms + network 0.479 ms = 0.552 ms against the uniform reverb's 0.514 ms (1.07x).
 #include "dattorro_stage.h"
 #include "chorus_stage.h"
 
@@ -259,16 +260,14 @@ __global__ __launch_bounds__(256) void dattorro_pre_convert(DattorroArgs a, int 
     else *pm = *im;
 }
 
-namespace {
 // OLFX_PREDELAY_KERNEL=1 runs v1 (A/B diagnostic)
-bool predelay_v1() {
+bool predelay_kernel_v1() {
     static const bool v = [] {
         const char *e = std::getenv("OLFX_PREDELAY_KERNEL");
         return e && std::atoi(e) == 1;
     }();
     return v;
 }
-}  // namespace
 
 hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
@@ -281,7 +280,7 @@ hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s) {
     if (a.pre_im) {
         // per-workgroup ring resources: 64 instances x 32 KB; inputs and the block by 32-bit offsets
         if ((uint64_t)a.n_frames * a.n * 4u >= (1ull << 32)) return hipErrorInvalidValue;
-        if (predelay_v1())
+        if (predelay_kernel_v1())
             hipLaunchKernelGGL(dattorro_predelay_v1, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
         else
             hipLaunchKernelGGL(dattorro_predelay_v2, dim3((a.n + 63) / 64), dim3(64), 0, s, a);

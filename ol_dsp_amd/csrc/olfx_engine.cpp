@@ -1737,7 +1737,10 @@ double olfx_algorithmic_read_bytes_per_frame(const olfx_engine *e) {
 const char *olfx_kernel_name(const olfx_engine *e) {
     if (!e) return "";
     switch (e->kind) {
-    case OLFX_KIND_DATTORRO: return "dattorro_block_v4";
+    case OLFX_KIND_DATTORRO:   // gather mode: the pre-delay pass ahead of the network, one launch pair per block
+        return e->dt_gather ? (predelay_kernel_v1() ? "dattorro_predelay_v1+dattorro_block_v4"
+                                                     : "dattorro_predelay_v2+dattorro_block_v4")
+                            : "dattorro_block_v4";
     case OLFX_KIND_CHORUS: return chorus_kernel_name(e->n, e->psize, e->csize, 0);
     case OLFX_KIND_PITCHSHIFT: return chorus_kernel_name(e->n, e->psize, e->csize, 1);
     case OLFX_KIND_VOICE: return "voice_block_v5";

@@ -90,6 +90,8 @@ struct DattorroArgs {
 // pre-delays, dattorro_block_v4's own tap) and instance-major (gather mode): the ring's content
 // is copied into the other layout (to_im: position-major -> instance-major)
 hipError_t launch_dattorro_pre_convert(const DattorroArgs &a, bool to_im, hipStream_t s);
+// gather mode's pre-delay pass: v2 unless OLFX_PREDELAY_KERNEL=1 (A/B diagnostic)
+bool predelay_kernel_v1();
 
 // ----------------------------------------------------------------------------------------------
 // Deterministic cos(2*pi*x): used by the chorus LFO (RNBO cycle~).  Branch-free (selects only, no

@@ -20,7 +20,7 @@ k=${PASS_BASE:-0}
 for p in "${passes[@]}"; do
   k=$((k+1))
   echo "== pass $k: $p"
-  timeout -k 10 300 rocprofv3 --kernel-trace --kernel-include-regex "_block_|voice_mix" --pmc $p -d "$out/p$k" -o run --output-format csv -- \
+  timeout -k 10 300 rocprofv3 --kernel-trace --kernel-include-regex "_block_|voice_mix|predelay" --pmc $p -d "$out/p$k" -o run --output-format csv -- \
       python3 bench.py --workload "$wl" --also "" --steps "$steps" --warmup 2 --cpu-seconds 0 "$@" > "$out/p$k.log" 2>&1
   rc=$?
   echo "   rc=$rc"
