@@ -948,7 +948,6 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, uin
         a.psize = e->psize;
         a.csize = e->csize;
         a.mode = mode;
-        a.cus = (uint32_t)e->cus;
         return a;
     };
     switch (e->kind) {
@@ -1741,8 +1740,8 @@ const char *olfx_kernel_name(const olfx_engine *e) {
         return e->dt_gather ? (predelay_kernel_v1() ? "dattorro_predelay_v1+dattorro_block_v4"
                                                      : "dattorro_predelay_v2+dattorro_block_v4")
                             : "dattorro_block_v4";
-    case OLFX_KIND_CHORUS: return chorus_kernel_name(e->n, e->psize, e->csize, 0);
-    case OLFX_KIND_PITCHSHIFT: return chorus_kernel_name(e->n, e->psize, e->csize, 1);
+    case OLFX_KIND_CHORUS:
+    case OLFX_KIND_PITCHSHIFT: return "chorus_block_v11";
     case OLFX_KIND_VOICE: return "voice_block_v5";
     case OLFX_KIND_VOICE_MOOG: return "voice_block_v4";
     case OLFX_KIND_CHAIN: return "chain_block_v5";

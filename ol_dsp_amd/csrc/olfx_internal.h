@@ -218,7 +218,6 @@ struct ChorusArgs {
     uint32_t t0;                // write position of the first frame (mod ring sizes)
     uint32_t psize, csize;      // ring sizes (powers of two)
     uint32_t mode;              // 0 = full chorus, 1 = pitch-shift stage only
-    uint32_t cus;               // compute units (chorus_block_v13's persistent grid)
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -342,7 +341,7 @@ hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s);
 hipError_t launch_chain(const ChainArgs &a, hipStream_t s);
 hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s);
 // the chorus kernel launch_chorus picks for n instances, ring sizes and cooperative I/O
-const char *chorus_kernel_name(uint32_t n, uint32_t psize, uint32_t csize, uint32_t mode);
+
 hipError_t launch_voice(const VoiceArgs &a, hipStream_t s);
 
 // ----------------------------------------------------------------------------------------------

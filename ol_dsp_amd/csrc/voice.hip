@@ -24,68 +24,43 @@ namespace {
 
 enum { SEG_IDLE = 0, SEG_ATTACK = 1, SEG_DECAY = 2, SEG_RELEASE = 3 };
 
+// Contraction.  The voice's continuous stages are contracted into FMAs where the firmware's
+// compiler would contract a * b + c (GCC's default -ffp-contract=fast in GNU C++): the polyBLEP
+// quadratics, Svf::SetFreq's sine polynomial and damping limit, the Svf's low/band updates, the
+// ladder's stages, feedback sum and SetAlpha polynomials.  Not the envelope updates, the
+// portamento or the phase accumulator (their segment ends and the phase wrap are discontinuous:
+// contracting them moved a segment end or a wrap by a sample, up to 2.8e-2 from the unfused
+// oracle) nor the Svf's notch (2.7e-5 on a default-parameter voice).  Measured on the CPU
+// restatement, the contracted stages together stay < 2e-6 from the unfused oracle; the voice's
+// parity tolerance is 1e-5 of max(|ref|, rms) (tests/test_gpu_parity.py).  MI355X: the Svf voice
+// 0.0358 -> 0.0333 ms, the Moog voice 0.1226 -> 0.0664 ms (32,768 voices, same box).
+
 // polyBLEP residual with one division: t/dt near the wrap start, (t-1)/dt near its end -- the
-// same quotients as the two-branch form
+// same quotients as the two-branch form; q + q - q q - 1 and q q + q + q + 1 as
+// fma(-q, q, 2q) - 1 and fma(q, q, 2q) + 1
 __device__ __forceinline__ float polyblep(float dt, float t) {
     const bool lo = t < dt, hi = !lo && t > 1.0f - dt;
     const float q = (lo ? t : t - 1.0f) * __builtin_amdgcn_rcpf(dt);   // v_rcp: ~1 ulp
-    float rlo = q + q - q * q - 1.0f;
-    float rhi = q * q + q + q + 1.0f;
+    const float q2 = q + q;
+    float rlo = __builtin_fmaf(-q, q, q2) - 1.0f;
+    float rhi = __builtin_fmaf(q, q, q2) + 1.0f;
     asm volatile("" : "+v"(rlo), "+v"(rhi));      // both computed: selects, not an exec-mask diamond
     return lo ? rlo : (hi ? rhi : 0.0f);
 }
 
-// the same residual with the quadratics contracted (voice_block_v5 under OLFX_VOICE_FMA)
-__device__ __forceinline__ float polyblep_fma(float dt, float t) {
-    const bool lo = t < dt, hi = !lo && t > 1.0f - dt;
-    const float q = (lo ? t : t - 1.0f) * __builtin_amdgcn_rcpf(dt);
-    const float q2 = q + q;
-    float rlo = __builtin_fmaf(-q, q, q2) - 1.0f;
-    float rhi = __builtin_fmaf(q, q, q2) + 1.0f;
-    asm volatile("" : "+v"(rlo), "+v"(rhi));
-    return lo ? rlo : (hi ? rhi : 0.0f);
-}
-
 // sin(x) for x in [0, pi/4] (Svf::SetFreq's argument pi * min(0.25, fc / 2sr)): odd Taylor
-// polynomial to x^9, truncation < 2e-9, i.e. within an ulp of sinf; branch-free.  The voice's
-// parity tolerance (1e-5 of max(|ref|, rms), tests/test_gpu_parity.py) covers ulp-level
-// differences from the host's sinf.
+// polynomial to x^9 in Horner form, truncation < 2e-9; branch-free.
 __device__ __forceinline__ float sin_quarter(float x) {
     const float x2 = x * x;
-    float p = 2.7557319e-6f;                 // 1/9!
-    p = p * x2 + -1.9841270e-4f;             // -1/7!
-    p = p * x2 + 8.3333333e-3f;              // 1/5!
-    p = p * x2 + -1.6666667e-1f;             // -1/3!
-    return x + (x * x2) * p;
-}
-__device__ __forceinline__ float sin_quarter_fma(float x) {
-    const float x2 = x * x;
-    float p = __builtin_fmaf(2.7557319e-6f, x2, -1.9841270e-4f);
-    p = __builtin_fmaf(p, x2, 8.3333333e-3f);
-    p = __builtin_fmaf(p, x2, -1.6666667e-1f);
+    float p = __builtin_fmaf(2.7557319e-6f, x2, -1.9841270e-4f);     // 1/9!, -1/7!
+    p = __builtin_fmaf(p, x2, 8.3333333e-3f);                        // 1/5!
+    p = __builtin_fmaf(p, x2, -1.6666667e-1f);                       // -1/3!
     return __builtin_fmaf(x * x2, p, x);
 }
 
 // packed FP32 (v_pk_mul_f32 / v_pk_add_f32: two IEEE operations per lane and instruction, the same
 // bits as two scalar ones)
 typedef float f2 __attribute__((ext_vector_type(2)));
-
-// daisysp::LadderFilter's tanh: Pade approximant, saturating beyond |x| > 3 (the exact division
-// keeps it bit-identical with the oracle)
-__device__ __forceinline__ float ladder_tanh(float x) {
-    const float x2 = x * x;
-    const float r = x * (27.0f + x2) / (27.0f + 9.0f * x2);
-    return x > 3.0f ? 1.0f : (x < -3.0f ? -1.0f : r);
-}
-
-// LadderFilter::LPF stage i: one zero at -0.3 (0.3/1.3 feed-forward of the previous input), one pole
-__device__ __forceinline__ float ladder_lpf(float s, float alpha, float &z0, float &z1) {
-    float ft = s * (1.0f / 1.3f) + (0.3f / 1.3f) * z0 - z1;
-    ft = ft * alpha + z1;
-    z1 = ft;
-    z0 = s;
-    return ft;
-}
 
 struct Ladder {
     float z0[4], z1[4], old;
@@ -213,9 +188,6 @@ struct Env {
 #define OLFX_VC_CHUNK 8
 #endif
 constexpr int kVcChunk = OLFX_VC_CHUNK;
-#ifndef OLFX_VOICE_FMA
-#define OLFX_VOICE_FMA 0
-#endif
 
 // Runs f(j) for the m samples of a chunk: unrolled when the chunk is full, so the off-recurrence
 // work of neighbouring samples interleaves (ILP for a wave that is alone on its SIMD).
@@ -299,11 +271,7 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
                         const float inc = port_z * inv_sr;
                         // Oscillator::Process, WAVE_POLYBLEP_SAW
                         float o = (2.0f * phase) - 1.0f;
-#if OLFX_VOICE_FMA
-                        o -= polyblep_fma(inc, phase);
-#else
                         o -= polyblep(inc, phase);
-#endif
                         o *= -1.0f;
                         phase += inc;
                         phase = phase > 1.0f ? phase - 1.0f : phase;
@@ -312,21 +280,12 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
                     }
                     if constexpr (CUT) {
                         const float fe = ef.step();
-#if OLFX_VOICE_FMA
                         const float fc_in = __builtin_fmaf(fe * 20000.0f, fenv_amt, cutoff);
                         const float wc = fc_in * 2.0f * 3.1415927410125732f * fc_max;
                         const float wc2 = wc * wc;
                         // the same polynomials in Horner form
                         cd.x = wc * __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(-0.0202f, wc, 0.1381f), wc, -0.4324f), wc, 0.9892f);
                         cd.y = __builtin_fmaf(__builtin_fmaf(-0.05f, wc2, -0.095f), wc2, __builtin_fmaf(0.0536f, wc, 1.006f));
-#else
-                        const float fc_in = cutoff + ((fe * 20000.0f) * fenv_amt);
-                        // LadderFilter::SetFreq (unclamped) -> SetAlpha
-                        const float wc = fc_in * 2.0f * 3.1415927410125732f * fc_max;
-                        const float wc2 = wc * wc;
-                        cd.x = 0.9892f * wc - 0.4324f * wc2 + 0.1381f * wc * wc2 - 0.0202f * wc2 * wc2;
-                        cd.y = 1.006f + 0.0536f * wc - 0.095f * wc2 - 0.05f * wc2 * wc2;
-#endif
                     }
                     if constexpr (AMP && CUT) {
                         qb[j * 64] = make_float4(ab.x, ab.y, cd.x, cd.y);
@@ -373,11 +332,10 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
                 for_chunk(m, [&](uint32_t j) {
                     const float4 v = qb[j * 64];
                     float y;
-#if OLFX_VOICE_FMA
                     {
-                        // contracted as the firmware's compiler contracts a * b + c; the Pade tanh
-                        // as r(med3(x, -3, 3)) (r(+-3) = +-1 exactly: the saturation, branch-free)
-                        // with a hardware reciprocal
+                        // contracted (see Contraction above); the Pade tanh as r(med3(x, -3, 3))
+                        // (r(+-3) = +-1 exactly: the saturation, branch-free) with a hardware
+                        // reciprocal
                         const float input = v.x, alpha = v.z, kq = k_or_unused * v.w;
                         const float fb0 = -0.5f * input;
                         float total = 0.0f;
@@ -402,27 +360,6 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
                         L.old = input;
                         y = total * v.y;
                     }
-#else
-                    {
-                        // LadderFilter::Process, LP24
-                        const float input = v.x, alpha = v.z, qadj = v.w;
-                        float total = 0.0f, interp = 0.0f;
-#pragma unroll
-                        for (int os = 0; os < 4; ++os) {
-                            float u = (interp * L.old + (1.0f - interp) * input) -
-                                      (L.z1[3] - 0.5f * input) * k_or_unused * qadj;
-                            u = ladder_tanh(u);
-                            const float s1 = ladder_lpf(u, alpha, L.z0[0], L.z1[0]);
-                            const float s2 = ladder_lpf(s1, alpha, L.z0[1], L.z1[1]);
-                            const float s3 = ladder_lpf(s2, alpha, L.z0[2], L.z1[2]);
-                            const float s4 = ladder_lpf(s3, alpha, L.z0[3], L.z1[3]);
-                            total += s4 * (1.0f / 4);
-                            interp += 1.0f / 4;
-                        }
-                        L.old = input;
-                        y = total * v.y;
-                    }
-#endif
                     out[(size_t)(f0 + j) * n] = y;
                 });
             }
@@ -537,11 +474,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                         ended = ended || xn.x > ea.hi || xn.x < ea.lo || xn.y > ef.hi || xn.y < ef.lo;
                         X = xn;
                         const f2 m = X * AMT;
-#if OLFX_VOICE_FMA
                         qo[j * 64] = make_float2(m.x, __builtin_fmaf(m.y, fenv_amt, cutoff));
-#else
-                        qo[j * 64] = make_float2(m.x, cutoff + m.y * fenv_amt);
-#endif
                     }
                     ea.x = X.x;
                     ef.x = X.y;
@@ -551,22 +484,14 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                         for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) {
                             const float amp = ea.step() * amp_amt;
                             const float fe = ef.step();
-#if OLFX_VOICE_FMA
                             qo[j * 64] = make_float2(amp, __builtin_fmaf(fe * 20000.0f, fenv_amt, cutoff));
-#else
-                            qo[j * 64] = make_float2(amp, cutoff + ((fe * 20000.0f) * fenv_amt));
-#endif
                         }
                     }
                 } else {
                     for_chunk(len(k), [&](uint32_t j) {
                         const float amp = ea.step() * amp_amt;
                         const float fe = ef.step();
-#if OLFX_VOICE_FMA
                         qo[j * 64] = make_float2(amp, __builtin_fmaf(fe * 20000.0f, fenv_amt, cutoff));
-#else
-                        qo[j * 64] = make_float2(amp, cutoff + ((fe * 20000.0f) * fenv_amt));
-#endif
                     });
                 }
             }
@@ -628,7 +553,6 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
 #pragma unroll
                     for (int q = 0; q < P; ++q)
                         qv[q] = num[q] * (f2){__builtin_amdgcn_rcpf(dt[q].x), __builtin_amdgcn_rcpf(dt[q].y)};
-#if OLFX_VOICE_FMA
                     // q + q - q q - 1 and q q + q + q + 1 as fma(-q, q, 2q) - 1 and fma(q, q, 2q) + 1
 #pragma unroll
                     for (int q = 0; q < P; ++q) qq[q] = qv[q] + qv[q];
@@ -646,23 +570,6 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                         for (int h = 0; h < 2; ++h) blep[h] = lo[q][h] ? rlo[q][h] : (hi[q][h] ? rhi[q][h] : 0.0f);
                         o[q] = o[q] - blep;
                     }
-#else
-#pragma unroll
-                    for (int q = 0; q < P; ++q) qq[q] = qv[q] * qv[q];
-#pragma unroll
-                    for (int q = 0; q < P; ++q) { rlo[q] = qv[q] + qv[q]; rhi[q] = qq[q] + qv[q]; }
-#pragma unroll
-                    for (int q = 0; q < P; ++q) { rlo[q] = rlo[q] - qq[q]; rhi[q] = rhi[q] + qv[q]; }
-#pragma unroll
-                    for (int q = 0; q < P; ++q) { rlo[q] = rlo[q] - 1.0f; rhi[q] = rhi[q] + 1.0f; o[q] = 2.0f * t[q]; }
-#pragma unroll
-                    for (int q = 0; q < P; ++q) {
-                        f2 blep;
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) blep[h] = lo[q][h] ? rlo[q][h] : (hi[q][h] ? rhi[q][h] : 0.0f);
-                        o[q] = (o[q] - 1.0f) - blep;
-                    }
-#endif
 #pragma unroll
                     for (int q = 0; q < P; ++q) {
                         // o *= -1; o * 0.5 (== o * -0.5 exactly)
@@ -678,11 +585,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                         phase += inc;
                         phase = phase > 1.0f ? phase - 1.0f : phase;
                         float o = (2.0f * t) - 1.0f;
-#if OLFX_VOICE_FMA
-                        o -= polyblep_fma(inc, t);
-#else
                         o -= polyblep(inc, t);
-#endif
                         o *= -1.0f;
                         qo[j * 64] = o * 0.5f;
                     }
@@ -709,21 +612,15 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     f2 x[P], x2[P], pp[P], fq[P];
 #pragma unroll
                     for (int q = 0; q < P; ++q) {
-#if OLFX_VOICE_FMA
                         // fminf(fmaxf(x, 1e-6), fc_max) for 1e-6 <= fc_max and a non-NaN cutoff sum
                         const float c0 = __builtin_amdgcn_fmed3f(qi[(2 * q) * 64].y, 1.0e-6f, fc_max);
                         const float c1 = __builtin_amdgcn_fmed3f(qi[(2 * q + 1) * 64].y, 1.0e-6f, fc_max);
-#else
-                        const float c0 = fminf(fmaxf(qi[(2 * q) * 64].y, 1.0e-6f), fc_max);
-                        const float c1 = fminf(fmaxf(qi[(2 * q + 1) * 64].y, 1.0e-6f), fc_max);
-#endif
                         const f2 fcn = (f2){c0, c1} * inv_2sr;
                         const f2 arg = {0.25f < fcn.x ? 0.25f : fcn.x, 0.25f < fcn.y ? 0.25f : fcn.y};
                         x[q] = 3.1415927410125732f * arg;
                     }
 #pragma unroll
                     for (int q = 0; q < P; ++q) x2[q] = x[q] * x[q];
-#if OLFX_VOICE_FMA
 #pragma unroll
                     for (int q = 0; q < P; ++q) pp[q] = __builtin_elementwise_fma((f2)2.7557319e-6f, x2[q], (f2)-1.9841270e-4f);
 #pragma unroll
@@ -742,49 +639,13 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                         qo[(2 * q) * 64] = make_float2(-(damp_res < d0 ? damp_res : d0), fq[q].x);
                         qo[(2 * q + 1) * 64] = make_float2(-(damp_res < d1 ? damp_res : d1), fq[q].y);
                     }
-#else
-#pragma unroll
-                    for (int q = 0; q < P; ++q) pp[q] = (f2)2.7557319e-6f * x2[q];
-#pragma unroll
-                    for (int q = 0; q < P; ++q) pp[q] = pp[q] + -1.9841270e-4f;
-#pragma unroll
-                    for (int q = 0; q < P; ++q) pp[q] = pp[q] * x2[q];
-#pragma unroll
-                    for (int q = 0; q < P; ++q) pp[q] = pp[q] + 8.3333333e-3f;
-#pragma unroll
-                    for (int q = 0; q < P; ++q) pp[q] = pp[q] * x2[q];
-#pragma unroll
-                    for (int q = 0; q < P; ++q) pp[q] = pp[q] + -1.6666667e-1f;
-#pragma unroll
-                    for (int q = 0; q < P; ++q) x2[q] = x[q] * x2[q];
-#pragma unroll
-                    for (int q = 0; q < P; ++q) pp[q] = x2[q] * pp[q];
-#pragma unroll
-                    for (int q = 0; q < P; ++q) fq[q] = 2.0f * (x[q] + pp[q]);   // 2 sin_quarter
-#pragma unroll
-                    for (int q = 0; q < P; ++q) {
-                        const f2 rq = {__builtin_amdgcn_rcpf(fq[q].x), __builtin_amdgcn_rcpf(fq[q].y)};
-                        const f2 lim = 2.0f * rq - fq[q] * 0.5f;
-                        const float d0 = 2.0f < lim.x ? 2.0f : lim.x, d1 = 2.0f < lim.y ? 2.0f : lim.y;
-                        qo[(2 * q) * 64] = make_float2(-(damp_res < d0 ? damp_res : d0), fq[q].x);
-                        qo[(2 * q + 1) * 64] = make_float2(-(damp_res < d1 ? damp_res : d1), fq[q].y);
-                    }
-#endif
                 } else {
                     for (uint32_t j = 0; j < len(k - 1); ++j) {
-#if OLFX_VOICE_FMA
                         const float fc = __builtin_amdgcn_fmed3f(qi[j * 64].y, 1.0e-6f, fc_max);
                         const float fcn = fc * inv_2sr;
                         const float arg = 0.25f < fcn ? 0.25f : fcn;
-                        const float fq = 2.0f * sin_quarter_fma(3.1415927410125732f * arg);
-                        const float lim = __builtin_fmaf(2.0f, __builtin_amdgcn_rcpf(fq), fq * -0.5f);
-#else
-                        const float fc = fminf(fmaxf(qi[j * 64].y, 1.0e-6f), fc_max);
-                        const float fcn = fc * inv_2sr;
-                        const float arg = 0.25f < fcn ? 0.25f : fcn;
                         const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
-                        const float lim = 2.0f * __builtin_amdgcn_rcpf(fq) - fq * 0.5f;
-#endif
+                        const float lim = __builtin_fmaf(2.0f, __builtin_amdgcn_rcpf(fq), fq * -0.5f);
                         const float dlim = 2.0f < lim ? 2.0f : lim;
                         qo[j * 64] = make_float2(-(damp_res < dlim ? damp_res : dlim), fq);
                     }
@@ -812,10 +673,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     // (packing this serial recurrence's paired products cost as many register
                     // moves as it saved operations: scalar)
                     const float src = sa.x, ndamp = fd.x, fq = fd.y;     // FREQ hands over -damp
-#if OLFX_VOICE_FMA
-                    // contracted as the firmware's compiler contracts a * b + c, except the notch
-                    // (contracting src - damp band moved a default-parameter voice 2.7e-5 from the
-                    // unfused oracle; the rest together < 2e-6, measured on the CPU restatement)
+                    // contracted except the notch (see Contraction above)
                     float notch = src + ndamp * band;
                     low = __builtin_fmaf(fq, band, low);
                     float high = notch - low;
@@ -826,18 +684,6 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     high = notch - low;
                     band = __builtin_fmaf(-((drive * band) * band), band, __builtin_fmaf(fq, high, band));
                     out_low = __builtin_fmaf(0.5f, low, out_low);
-#else
-                    float notch = src + ndamp * band;                    // == src - damp * band
-                    low = low + fq * band;
-                    float high = notch - low;
-                    band = fq * high + band - drive * band * band * band;
-                    float out_low = 0.5f * low;
-                    notch = src + ndamp * band;
-                    low = low + fq * band;
-                    high = notch - low;
-                    band = fq * high + band - drive * band * band * band;
-                    out_low += 0.5f * low;
-#endif
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(out_low * sa.y), ro, i * 4u, j * n * 4u, 0);
                 });
             }

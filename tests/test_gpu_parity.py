@@ -4,8 +4,6 @@ Bars: dattorro, chorus, pitch-shift and the chain are BIT-EXACT (integer-exact f
 -ffp-contract=off on both sides); the voice is within rel 1e-5 of max(|ref|, rms(ref)) because
 Svf::SetFreq calls sinf every sample (device ocml vs host glibc may differ by an ulp).
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -462,8 +460,7 @@ def test_chorus_long_run_many_wraps(cuda, kind, n):
     """100,000 frames at the fastest pitch phasors (every instance's two pitch taps wrap 12 times,
     each wrap a generic chunk with direct ring reads), ragged blocks with partial chunks:
     bit-exact against the oracle.  n = 70 runs chorus_block_v11's per-lane I/O (rows need
-    n % 4 == 0), n = 72 its row I/O, or under OLFX_CHORUS_KERNEL=13 / 14 the block-at-once kernels
-    (4.5 groups of 16, launches of at most 256 frames)."""
+    n % 4 == 0), n = 72 its row I/O."""
     frames = 100000
     rng = np.random.default_rng(93)
     p = chorus_params(rng, n)
@@ -489,12 +486,10 @@ def test_chorus_long_run_many_wraps(cuda, kind, n):
 @pytest.mark.parametrize("kind", ["chorus", "pitchshift"])
 @pytest.mark.parametrize("n", [4, 36, 1028])
 def test_chorus_block_kernel_edges(cuda, kind, n):
-    """The block-at-once kernels (OLFX_CHORUS_KERNEL=13 / 14, n % 4 == 0; v11 otherwise): a single
-    partial 16-instance group (4), a partial last group
-    (36, 1028: more groups than one per workgroup for none / some workgroups), calls of 252, 4, 8,
-    260 (two launches), 1000 and 2048 frames (blocks not a multiple of the 4-frame lores~ step
-    pairs, launches split at 256), extreme depth / rate corners (the chorus window bound):
-    bit-exact against the oracle; the engine reports the kernel it runs."""
+    """Row I/O (n % 4 == 0) at a single partial wave (4), a partial last wave (36, 1028), calls of
+    252, 4, 8, 260, 1000 and 2048 frames (partial 16-frame chunks), extreme depth / rate corners
+    (the chorus window bound): bit-exact against the oracle; the engine reports the kernel it
+    runs."""
     rng = np.random.default_rng(500 + n)
     p = chorus_params(rng, n)
     p[5, ::3] = 1.0                                        # depth max
@@ -513,9 +508,7 @@ def test_chorus_block_kernel_edges(cuda, kind, n):
         for i in range(n):
             ref.set(i, "pitch", float(p[0, i]))
             ref.set(i, "window", float(p[7, i]))
-    forced = os.environ.get("OLFX_CHORUS_KERNEL", "")           # the block-at-once kernels are opt-in
-    want = {"13": "chorus_block_v13", "14": "chorus_block_v14" if kind == "chorus" else "chorus_block_v13"}
-    assert e.kernel_name == want.get(forced, "chorus_block_v11")
+    assert e.kernel_name == "chorus_block_v11"
     y = run_gpu(e, x, blocks, cuda)
     yr = ref.process(x, threads=8)
     assert bits_equal(y, yr), first_mismatch(y, yr)
