@@ -581,7 +581,7 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
     if mix_ms is not None:
         nb = (n + 7) // 8
         mix_bytes = 4.0 * n * B + 8.0 * nb * B          # voice reads + bus read-modify-write
-        res["mix"] = {"kernel": "voice_mix_v2", "kernel_ms": mix_ms, "bound": "hbm",
+        res["mix"] = {"kernel": "voice_mix_v4", "kernel_ms": mix_ms, "bound": "hbm",
                       "achieved": mix_bytes / (mix_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                       "frac": mix_bytes / (mix_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                       "algorithmic_bytes_per_launch": mix_bytes, "bus_checksum_rank0": bus_sum}

@@ -64,35 +64,50 @@ __global__ __launch_bounds__(256) void voice_mix_v2(MixArgs a) {
     }
 }
 
-// voice_mix_v3: buses that are contiguous runs of voices in voice order (order[k] == k, the layout
-// Polyvoice groups get when voices are allotted in order -- the bench's buses of 8).  A block takes
-// 256 buses; per 4 frames it stages the voice run those buses cover, [off[b0], off[b0 + 256)), from
-// each frame row into LDS with coalesced loads (256 lanes x 4 B per instruction: one 1-KB run),
-// then every lane adds its bus's voices from LDS in list order -- the same adds as v2, bit for bit.
-// v2's lanes gathered 4 B each at the bus stride (32 B for buses of 8): 16 lines per load
-// instruction for 256 B used ("Voice buses").
-__global__ __launch_bounds__(256) void voice_mix_v3(MixArgs a, uint32_t span) {
-    extern __shared__ float stage[];                  // [kMixFr][span]
-    const uint32_t b0 = blockIdx.x * 256u, b = b0 + threadIdx.x;
-    const uint32_t bl = b0 + 256u < a.n_buses ? b0 + 256u : a.n_buses;
-    const uint32_t v0 = a.off[b0], len = a.off[bl] - v0;
-    const bool live = b < a.n_buses;
-    const uint32_t k0 = live ? a.off[b] - v0 : 0u, k1 = live ? a.off[b + 1] - v0 : 0u;
+// voice_mix_v4: buses that are contiguous runs of voices in voice order (order[k] == k, the layout
+// Polyvoice groups get when voices are allotted in order -- the bench's buses of 8) starting and
+// ending on multiples of 4 voices, with 16-B aligned frame rows.  A lane reads its bus's voices as
+// float4 runs (buses of 8: two 16-B loads per frame instead of v2's eight 4-B gathers at the bus
+// stride, 16 lines per instruction) and adds them in list order -- the same adds as v2, bit for bit.
+__global__ __launch_bounds__(256) void voice_mix_v4(MixArgs a) {
+    const uint32_t b = blockIdx.x * 256u + threadIdx.x;
+    if (b >= a.n_buses) return;
+    const uint32_t k0 = a.off[b], k1 = a.off[b + 1];
     for (uint32_t f0 = blockIdx.y * kMixFr; f0 < a.n_frames; f0 += gridDim.y * kMixFr) {
         const uint32_t nfr = a.n_frames - f0 < kMixFr ? a.n_frames - f0 : kMixFr;   // uniform per block
-        __syncthreads();                              // the previous rows' readers are done
-        for (uint32_t j = 0; j < nfr; ++j) {
-            const float *row = a.in + (size_t)(f0 + j) * a.n + v0;
-            for (uint32_t q = threadIdx.x; q < len; q += 256u) stage[j * span + q] = row[q];
-        }
-        __syncthreads();
-        if (!live) continue;
+        const float *row = a.in + (size_t)f0 * a.n;
         float *dst = a.out + (size_t)f0 * a.n_buses + b;
-        for (uint32_t j = 0; j < nfr; ++j) {
-            const float *v = stage + j * span;
-            float acc = dst[(size_t)j * a.n_buses];
-            for (uint32_t k = k0; k < k1; ++k) acc = acc + v[k];
-            dst[(size_t)j * a.n_buses] = acc;
+        if (nfr == kMixFr) {
+            float acc[kMixFr];
+#pragma unroll
+            for (uint32_t j = 0; j < kMixFr; ++j) acc[j] = dst[(size_t)j * a.n_buses];
+            uint32_t k = k0;
+            for (; k + 8 <= k1; k += 8) {                 // two runs of 4 per frame in flight
+                float4 v0[kMixFr], v1[kMixFr];
+#pragma unroll
+                for (uint32_t j = 0; j < kMixFr; ++j) {
+                    v0[j] = *(const float4 *)(row + (size_t)j * a.n + k);
+                    v1[j] = *(const float4 *)(row + (size_t)j * a.n + k + 4);
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < kMixFr; ++j)
+                    acc[j] = (((((((acc[j] + v0[j].x) + v0[j].y) + v0[j].z) + v0[j].w) + v1[j].x) + v1[j].y) + v1[j].z) + v1[j].w;
+            }
+            if (k < k1) {
+#pragma unroll
+                for (uint32_t j = 0; j < kMixFr; ++j) {
+                    const float4 v = *(const float4 *)(row + (size_t)j * a.n + k);
+                    acc[j] = (((acc[j] + v.x) + v.y) + v.z) + v.w;
+                }
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < kMixFr; ++j) dst[(size_t)j * a.n_buses] = acc[j];
+        } else {
+            for (uint32_t j = 0; j < nfr; ++j) {
+                float acc = dst[(size_t)j * a.n_buses];
+                for (uint32_t q = k0; q < k1; ++q) acc = acc + row[(size_t)j * a.n + q];
+                dst[(size_t)j * a.n_buses] = acc;
+            }
         }
     }
 }
@@ -101,9 +116,8 @@ hipError_t launch_mix(const MixArgs &a, hipStream_t s) {
     if (a.n_buses == 0 || a.n_frames == 0) return hipSuccess;
     const uint32_t rows = (a.n_frames + kMixFr - 1) / kMixFr;
     const dim3 grid((a.n_buses + 255) / 256, rows < kMixMaxRows ? rows : kMixMaxRows);
-    if (a.contig_span) {
-        hipLaunchKernelGGL(voice_mix_v3, grid, dim3(256), (size_t)kMixFr * a.contig_span * sizeof(float), s, a,
-                           a.contig_span);
+    if (a.quad && (a.n & 3u) == 0 && ((uintptr_t)a.in & 15u) == 0) {
+        hipLaunchKernelGGL(voice_mix_v4, grid, dim3(256), 0, s, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(voice_mix_v2, grid, dim3(256), 0, s, a);

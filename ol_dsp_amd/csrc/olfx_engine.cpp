@@ -455,7 +455,7 @@ struct olfx_engine {
     std::vector<olfx_voice_event> events;
     // voice buses (olfx_mix_config): [n_buses + 1] offsets, then the voice lists
     uint32_t *mix_dev = nullptr;
-    uint32_t mix_span = 0;                  // voice_mix_v3's LDS row (contiguous buses), else 0
+    uint32_t mix_quad = 0;                  // contiguous buses on multiples of 4 voices (voice_mix_v4)
     hipEvent_t mix_done = nullptr;          // recorded after every olfx_mix launch
     uint32_t n_buses = 0;
 
@@ -1629,19 +1629,15 @@ int olfx_mix_config(olfx_engine *e, uint32_t n_buses, const uint32_t *offsets, c
     }
     e->mix_dev = fresh;
     e->n_buses = n_buses;
-    // buses that are contiguous voice runs in voice order take voice_mix_v3 (staged, coalesced
-    // rows) when the run any 256 consecutive buses cover fits its LDS rows (4 x 4096 floats)
-    e->mix_span = 0;
+    // buses that are contiguous voice runs in voice order, on multiples of 4 voices, take
+    // voice_mix_v4 (float4 runs)
+    e->mix_quad = 0;
     if (n_buses) {
         const uint32_t len = offsets[n_buses];
-        bool ident = true;
-        for (uint32_t k = 0; k < len && ident; ++k) ident = order[k] == k;
-        uint32_t span = 0;
-        for (uint32_t b0 = 0; b0 < n_buses && ident; b0 += 256) {
-            const uint32_t b1 = std::min(b0 + 256u, n_buses);
-            span = std::max(span, offsets[b1] - offsets[b0]);
-        }
-        if (ident && span > 0 && span <= 4096) e->mix_span = span;
+        bool quad = true;
+        for (uint32_t k = 0; k < len && quad; ++k) quad = order[k] == k;
+        for (uint32_t b = 0; b <= n_buses && quad; ++b) quad = (offsets[b] & 3u) == 0;
+        e->mix_quad = quad ? 1u : 0u;
     }
     return OLFX_OK;
 }
@@ -1658,7 +1654,7 @@ int olfx_mix(olfx_engine *e, const float *voice_out, float *bus_out, uint32_t n_
     MixArgs a{};
     a.off = e->mix_dev;
     a.order = e->mix_dev + e->n_buses + 1;
-    a.contig_span = e->mix_span;
+    a.quad = e->mix_quad;
     a.n = e->n;
     a.n_buses = e->n_buses;
     a.n_frames = n_frames;

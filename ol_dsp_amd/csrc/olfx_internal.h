@@ -355,9 +355,9 @@ struct MixArgs {
     const uint32_t *off;        // [n_buses + 1]
     const uint32_t *order;      // [off[n_buses]] voice indices
     uint32_t n, n_buses, n_frames;
-    // buses are contiguous voice runs in voice order (order[k] == k): the widest run of voices any
-    // 256 consecutive buses cover (voice_mix_v3's LDS rows), else 0 (voice_mix_v2)
-    uint32_t contig_span;
+    // buses are contiguous voice runs in voice order (order[k] == k) on multiples of 4 voices
+    // (voice_mix_v4's float4 runs), else 0 (voice_mix_v2)
+    uint32_t quad;
 };
 hipError_t launch_mix(const MixArgs &a, hipStream_t s);
 

@@ -1085,12 +1085,13 @@ def test_mix_buses_bit_exact(cuda):
     assert bits_equal(e.mix(y), O.mix_ref(y, [back]))
 
 
-@pytest.mark.parametrize("n,sizes", [(300, [8]), (3000, [8]), (2100, [1, 7, 0, 12, 3])])
+@pytest.mark.parametrize("n,sizes", [(300, [8]), (3000, [8]), (2000, [4, 12, 0, 8, 20]), (2100, [1, 7, 0, 12, 3])])
 def test_mix_contiguous_buses_bit_exact(cuda, n, sizes):
-    """Buses that are contiguous voice runs in voice order (voice_mix_v3: staged coalesced rows):
-    buses of 8 (the bench's Polyvoice layout; 3000 voices -> 375 buses, more than one block of 256),
-    and ragged runs with empty buses; frame counts on and off the four-frame step: bit-identical to
-    Polyvoice's in-order adds into a non-zero bus buffer."""
+    """Buses that are contiguous voice runs in voice order: on multiples of 4 voices (voice_mix_v4:
+    float4 runs) -- buses of 8 (the bench's Polyvoice layout; 3000 voices -> 375 buses, more than
+    one block of 256), a last bus of 4 (300), ragged runs of 4..20 with empty buses -- and off them
+    (2100: voice_mix_v2); frame counts on and off the four-frame step: bit-identical to Polyvoice's
+    in-order adds into a non-zero bus buffer."""
     import torch
     rng = np.random.default_rng(n)
     cfg = voice_configs(rng, n)
