@@ -417,12 +417,10 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
     # Kernel timing: ONE event pair on the launch stream around the K timed steps: GPU time per
     # step = the kernel's average launch duration plus the gap between launches.  (A pair per step
     # adds two timestamp markers between consecutive kernels -- ~3-4 us each on the command
-    # processor, 10-20 % of a 35 us voice block, measured: tools/loop_probe.py.)  Only voice_poly,
-    # whose steps run two kernels, times each kernel with its own pair.
-    per_step = bus is not None
+    # processor, 10-20 % of a 35 us voice block, measured: tools/loop_probe.py.)  voice_poly's
+    # steps run two kernels: its mix is timed alone after the timed region (one pair around K mix
+    # launches), and the voice kernel's time is the step time less that.
     region = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)] if per_step else None
-    evm = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)] if per_step else None
 
     # The timed loop calls the C-ABI directly with prebuilt arguments (Engine.process's checks and
     # tensor handling cost ~20 us of Python per call, more than a voice block's kernel): the host
@@ -447,19 +445,11 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
             rc |= lib.olfx_note_events(*ev_args[k % 40])
         if cc_args:
             rc |= lib.olfx_set_param_list(*cc_args[k % 100])
-        if t is not None and per_step:
-            ev[t][0].record(stream)
         rc |= lib.olfx_process(*proc_args[k % pool_n])
-        if t is not None and per_step:
-            ev[t][1].record(stream)
         if rc:
             _lib.check(rc, h)
         if bus is not None:
-            if t is not None:
-                evm[t][0].record(stream)
             eng.mix(out, bus, stream=stream.cuda_stream)
-            if t is not None:
-                evm[t][1].record(stream)
 
     for k in range(W):
         step(k)
@@ -477,8 +467,8 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if per_step else region[0].elapsed_time(region[1]) / K
-    mix_ms = float(np.mean([a.elapsed_time(b) for a, b in evm])) if evm else None
+    kern_ms = region[0].elapsed_time(region[1]) / K
+    mix_ms = None
 
     # sum |y| over the finite outputs of the last block (a voice whose Svf diverges -- possible in
     # the reference DaisySP arithmetic at high cutoff, low resonance and high drive -- yields
@@ -487,6 +477,18 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
     nonfinite = int((~finite).sum().item())
     checksum = float(torch.where(finite, out.abs(), torch.zeros_like(out)).sum().item())
     bus_sum = float(bus.abs().sum().item()) if bus is not None else None
+    if bus is not None:            # the mix alone, K launches between one event pair (untimed for value)
+        scratch = torch.zeros_like(bus)
+        for _ in range(W):
+            eng.mix(out, scratch, stream=stream.cuda_stream)
+        mreg = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        mreg[0].record(stream)
+        for _ in range(K):
+            eng.mix(out, scratch, stream=stream.cuda_stream)
+        mreg[1].record(stream)
+        torch.cuda.synchronize(dev)
+        mix_ms = mreg[0].elapsed_time(mreg[1]) / K
+        kern_ms = max(kern_ms - mix_ms, 1e-6)
 
     # untimed parity material: the last timed block of sampled instances, the pool blocks they read
     # (read back from the device: exactly the timed inputs) and the leg's event / control schedule
@@ -554,7 +556,8 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
         if rd:
             measured.update({"traffic_read": rd, "hbm_read_gbs_measured": rd / (kern_ms * 1e-3) / 1e9,
                              "frac_read_measured": rd / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS})
-    timing = ("HIP event pair per step around olfx_process" if per_step else
+    timing = ("one HIP event pair around the K timed steps / K, less the mix's own time (one pair around K mix "
+              "launches after the timed region)" if bus is not None else
               "one HIP event pair on the launch stream around the K timed steps / K (launch duration + launch gap)")
     if voice:
         fps = VOICE_MOOG_FLOPS_PER_SAMPLE if kind == "voice_moog" else VOICE_FLOPS_PER_SAMPLE
