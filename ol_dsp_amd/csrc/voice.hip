@@ -430,6 +430,20 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     const uint32_t me = i - blockIdx.x * 64;
     const uint32_t nf = a.n_frames;
     const uint32_t nsteps = (nf + kVcChunk - 1) / kVcChunk + 2;
+#if OLFX_VC_STAMP
+    // diagnostic build: each role wave's total cycles and cycles at the step barriers go to output
+    // rows 2 role and 2 role + 1 of its voices (the outputs are garbage in this build)
+    const uint64_t st_start = __builtin_amdgcn_s_memtime();
+    uint64_t st_wait = 0;
+#define VC_SYNC()                                                  \
+    do {                                                           \
+        const uint64_t st_a = __builtin_amdgcn_s_memtime();        \
+        __syncthreads();                                           \
+        st_wait += __builtin_amdgcn_s_memtime() - st_a;            \
+    } while (0)
+#else
+#define VC_SYNC() __syncthreads()
+#endif
     const float *c = a.coef;
     float *s = a.state;
     auto len = [&](uint32_t k) {             // frames of chunk k (the last may be short)
@@ -495,7 +509,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     });
                 }
             }
-            __syncthreads();
+            VC_SYNC();
         }
         s[VCS_ENVA_X * n + i] = ea.x;
         s[VCS_ENVF_X * n + i] = ef.x;
@@ -591,7 +605,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     }
                 }
             }
-            __syncthreads();
+            VC_SYNC();
         }
         s[VCS_PHASE * n + i] = phase;
         s[VCS_PORT_Z * n + i] = port_z;
@@ -651,7 +665,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     }
                 }
             }
-            __syncthreads();
+            VC_SYNC();
         }
     } else {
         // ---- FILT: Svf::Process; Low() = the average of the two passes' low outputs; * amp ----
@@ -687,11 +701,17 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(out_low * sa.y), ro, i * 4u, j * n * 4u, 0);
                 });
             }
-            __syncthreads();
+            VC_SYNC();
         }
         s[VCS_LOW * n + i] = low;
         s[VCS_BAND * n + i] = band;
     }
+#if OLFX_VC_STAMP
+    __syncthreads();
+    a.out[(size_t)(2u * role) * n + i] = (float)(__builtin_amdgcn_s_memtime() - st_start);
+    a.out[(size_t)(2u * role + 1u) * n + i] = (float)st_wait;
+#endif
+#undef VC_SYNC
 }
 
 hipError_t launch_voice(const VoiceArgs &a, hipStream_t s) {

@@ -11,6 +11,7 @@
 #   ab:<workload>:<k>    A/B: the workload under the default and OLFX_CHORUS_KERNEL=<k>, twice each
 #   tl:<lib>:<k>         GPU tests matching <k> against an experimental build (OLFX_LIB=<lib>)
 #   te:<VAR=v>:<k>       GPU tests matching <k> with the environment variable VAR=v
+#   vstamp               voice role stamps (build/ab/vcstamp.so, tools/voice_stamps.py) at 32,768 and 16,384
 #   abl:<workload>:<lib> A/B of the main build against <lib> (tools/ab.sh)
 set -u
 out=gpurun_out
@@ -41,6 +42,11 @@ for m in "$@"; do
       r=${m#te:}; kv=${r%%:*}; k=${r#*:}
       step "pytest_env_$(echo "$kv$k" | tr -c 'a-zA-Z0-9_' '_')" 600 env "$kv" python -u -m pytest tests -m gpu -x -v \
           -p no:cacheprovider --timeout 120 --timeout-method thread -k "$k" ;;
+    vstamp)
+      step vstamp_32768 120 env OLFX_LIB=$PWD/build/ab/vcstamp.so python tools/voice_stamps.py 32768
+      cat "$out/vstamp_32768.log"
+      step vstamp_16384 120 env OLFX_LIB=$PWD/build/ab/vcstamp.so python tools/voice_stamps.py 16384
+      cat "$out/vstamp_16384.log" ;;
     abl:*)
       r=${m#abl:}; w=${r%%:*}; lib=${r#*:}
       step "abl_$w" 600 bash tools/ab.sh "$w" main "$lib"
