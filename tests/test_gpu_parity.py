@@ -111,7 +111,7 @@ def test_dattorro_per_instance_predelay(cuda):
 
 def test_dattorro_predelay_gather_mode_switches(cuda):
     """The standalone reverb switches its pre-delay ring between the position-major tap (one
-    pre-delay for every instance) and gather mode (per-instance pre-delays: dattorro_predelay_v1,
+    pre-delay for every instance) and gather mode (per-instance pre-delays: dattorro_predelay_v2,
     instance-major ring) whenever the pre-delays become equal or differ; the ring's content is
     carried across each switch.  Uniform -> per instance (edges 0..8, 255..257, 4800, past the max)
     -> uniform -> per instance, calls of 256, 4, 1028 (gather mode splits at 256) and 60 frames,
@@ -153,6 +153,30 @@ def test_dattorro_predelay_gather_mode_switches(cuda):
     x = fast_noise(n, 512, seed=99)
     y2, yr2 = run_gpu(e, x, [512], cuda), ref2.process(x)
     assert bits_equal(y2, yr2), first_mismatch(y2, yr2)
+
+
+def test_dattorro_gather_mode_long_run_wraps(cuda):
+    """Gather mode (per-instance pre-delays) over 70,000 frames: the uint16 wrap of t at 65536 and
+    calls that start off the pre-pass's 32-frame line grid (60, 3900, 504 frames: first and last
+    chunks partial); pre-delays on the line and chunk edges 0, 1, 31..33, 63..65, 96, 4800 and
+    8191; 70 instances (a partial 64-instance wave).  Bit-exact against the oracle."""
+    n = 70
+    rng = np.random.default_rng(85)
+    p = dt_params(rng, n, 0.0)
+    edge = np.array([0, 1, 31, 32, 33, 63, 64, 65, 96, 4800, 8191], np.float64) / 4800
+    p[0, :] = rng.uniform(0, 1, n).astype(np.float32)
+    p[0, :len(edge)] = edge.astype(np.float32)
+    x = fast_noise(n, 70000, seed=85)
+    e = engine("dattorro", n)
+    e.set_params(0, p)
+    y = run_gpu(e, x, [60] + [4096] * 16 + [3900, 504], cuda)
+    assert e.kernel_name.startswith("dattorro_predelay_v2")
+    ref = O.Dattorro(n)
+    for i in range(n):
+        for f in range(7):
+            ref.set(i, f, float(p[f, i]))
+    yr = ref.process(x, threads=8)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
 
 
 def test_dattorro_predelay_beyond_max(cuda):
