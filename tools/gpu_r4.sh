@@ -11,6 +11,7 @@
 #   ab:<workload>:<k>    A/B: the workload under the default and OLFX_CHORUS_KERNEL=<k>, twice each
 #   tl:<lib>:<k>         GPU tests matching <k> against an experimental build (OLFX_LIB=<lib>)
 #   te:<VAR=v>:<k>       GPU tests matching <k> with the environment variable VAR=v
+#   ts:<k>               GPU tests matching <k>, with their printed output (-s)
 #   vstamp               voice role stamps (build/ab/vcstamp.so, tools/voice_stamps.py) at 32,768 and 16,384
 #   abl:<workload>:<lib> A/B of the main build against <lib> (tools/ab.sh)
 set -u
@@ -42,6 +43,11 @@ for m in "$@"; do
       r=${m#te:}; kv=${r%%:*}; k=${r#*:}
       step "pytest_env_$(echo "$kv$k" | tr -c 'a-zA-Z0-9_' '_')" 600 env "$kv" python -u -m pytest tests -m gpu -x -v \
           -p no:cacheprovider --timeout 120 --timeout-method thread -k "$k" ;;
+    ts:*)
+      k=${m#ts:}
+      step "pytest_s_$(echo "$k" | tr -c 'a-zA-Z0-9_' '_')" 600 python -u -m pytest tests -m gpu -x -v -s -p no:cacheprovider \
+          --timeout 120 --timeout-method thread -k "$k"
+      grep -E "rel err|PASSED|FAILED" "$out/pytest_s_$(echo "$k" | tr -c 'a-zA-Z0-9_' '_').log" ;;
     vstamp)
       step vstamp_32768 120 env OLFX_LIB=$PWD/build/ab/vcstamp.so python tools/voice_stamps.py 32768
       cat "$out/vstamp_32768.log"
