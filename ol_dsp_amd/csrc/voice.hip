@@ -39,7 +39,7 @@ enum { SEG_IDLE = 0, SEG_ATTACK = 1, SEG_DECAY = 2, SEG_RELEASE = 3 };
 // same quotients as the two-branch form; q + q - q q - 1 and q q + q + q + 1 as
 // fma(-q, q, 2q) - 1 and fma(q, q, 2q) + 1
 __device__ __forceinline__ float polyblep(float dt, float t) {
-    const bool lo = t < dt, hi = !lo && t > 1.0f - dt;
+    const bool lo = t < dt, hi = t > 1.0f - dt;                          // (lo wins the select)
     const float q = (lo ? t : t - 1.0f) * __builtin_amdgcn_rcpf(dt);   // v_rcp: ~1 ulp
     const float q2 = q + q;
     float rlo = __builtin_fmaf(-q, q, q2) - 1.0f;
@@ -56,6 +56,12 @@ __device__ __forceinline__ float sin_quarter(float x) {
     p = __builtin_fmaf(p, x2, 8.3333333e-3f);                        // 1/5!
     p = __builtin_fmaf(p, x2, -1.6666667e-1f);                       // -1/3!
     return __builtin_fmaf(x * x2, p, x);
+}
+
+// Svf::SetFreq's damping, negated for FILT: -min(damp_res, min(2, lim)) = max(-damp_res, -2, -lim),
+// one v_max3 (the negations are operand modifiers); equal for every non-NaN lim
+__device__ __forceinline__ float neg_damp(float damp_res, float lim) {
+    return __builtin_fmaxf(__builtin_fmaxf(-damp_res, -2.0f), -lim);
 }
 
 // packed FP32 (v_pk_mul_f32 / v_pk_add_f32: two IEEE operations per lane and instruction, the same
@@ -484,12 +490,14 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     const f2 D0 = {ea.d0, ef.d0}, T = {ea.tgt, ef.tgt}, AMT = {amp_amt, 20000.0f};
 #pragma unroll
                     for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) {
-                        const f2 xn = X + D0 * (T - X);
-                        ended = ended || xn.x > ea.hi || xn.x < ea.lo || xn.y > ef.hi || xn.y < ef.lo;
-                        X = xn;
+                        X = X + D0 * (T - X);
                         const f2 m = X * AMT;
                         qo[j * 64] = make_float2(m.x, __builtin_fmaf(m.y, fenv_amt, cutoff));
                     }
+                    // inside a segment the envelope is monotone toward a target beyond its bound
+                    // (x += d0 (tgt - x) with tgt - x of one sign: each IEEE step keeps the
+                    // direction), so it crossed the bound inside the chunk iff it ends past it
+                    ended = X.x > ea.hi || X.x < ea.lo || X.y > ef.hi || X.y < ef.lo;
                     ea.x = X.x;
                     ef.x = X.y;
                     if (__builtin_amdgcn_ballot_w64(ended)) {
@@ -560,7 +568,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
 #pragma unroll
                         for (int h = 0; h < 2; ++h) {
                             lo[q][h] = t[q][h] < dt[q][h];
-                            hi[q][h] = !lo[q][h] && t[q][h] > one_m[h];
+                            hi[q][h] = t[q][h] > one_m[h];          // (lo wins the selects below)
                             num[q][h] = lo[q][h] ? t[q][h] : tm1[h];
                         }
                     }
@@ -630,7 +638,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                         const float c0 = __builtin_amdgcn_fmed3f(qi[(2 * q) * 64].y, 1.0e-6f, fc_max);
                         const float c1 = __builtin_amdgcn_fmed3f(qi[(2 * q + 1) * 64].y, 1.0e-6f, fc_max);
                         const f2 fcn = (f2){c0, c1} * inv_2sr;
-                        const f2 arg = {0.25f < fcn.x ? 0.25f : fcn.x, 0.25f < fcn.y ? 0.25f : fcn.y};
+                        const f2 arg = {__builtin_fminf(fcn.x, 0.25f), __builtin_fminf(fcn.y, 0.25f)};
                         x[q] = 3.1415927410125732f * arg;
                     }
 #pragma unroll
@@ -649,19 +657,17 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     for (int q = 0; q < P; ++q) {
                         const f2 rq = {__builtin_amdgcn_rcpf(fq[q].x), __builtin_amdgcn_rcpf(fq[q].y)};
                         const f2 lim = __builtin_elementwise_fma((f2)2.0f, rq, fq[q] * -0.5f);
-                        const float d0 = 2.0f < lim.x ? 2.0f : lim.x, d1 = 2.0f < lim.y ? 2.0f : lim.y;
-                        qo[(2 * q) * 64] = make_float2(-(damp_res < d0 ? damp_res : d0), fq[q].x);
-                        qo[(2 * q + 1) * 64] = make_float2(-(damp_res < d1 ? damp_res : d1), fq[q].y);
+                        qo[(2 * q) * 64] = make_float2(neg_damp(damp_res, lim.x), fq[q].x);
+                        qo[(2 * q + 1) * 64] = make_float2(neg_damp(damp_res, lim.y), fq[q].y);
                     }
                 } else {
                     for (uint32_t j = 0; j < len(k - 1); ++j) {
                         const float fc = __builtin_amdgcn_fmed3f(qi[j * 64].y, 1.0e-6f, fc_max);
                         const float fcn = fc * inv_2sr;
-                        const float arg = 0.25f < fcn ? 0.25f : fcn;
+                        const float arg = __builtin_fminf(fcn, 0.25f);
                         const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
                         const float lim = __builtin_fmaf(2.0f, __builtin_amdgcn_rcpf(fq), fq * -0.5f);
-                        const float dlim = 2.0f < lim ? 2.0f : lim;
-                        qo[j * 64] = make_float2(-(damp_res < dlim ? damp_res : dlim), fq);
+                        qo[j * 64] = make_float2(neg_damp(damp_res, lim), fq);
                     }
                 }
             }
