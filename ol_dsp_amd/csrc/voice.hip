@@ -348,7 +348,8 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
 #pragma unroll
                         for (int os = 0; os < 4; ++os) {
                             const float interp = 0.25f * (float)os;
-                            const float mixin = __builtin_fmaf(interp, L.old, (1.0f - interp) * input);
+                            // (os = 0: fma(0, old, 1 input) is input exactly for a finite old)
+                            const float mixin = os == 0 ? input : __builtin_fmaf(interp, L.old, (1.0f - interp) * input);
                             float x = __builtin_fmaf(-(L.z1[3] + fb0), kq, mixin);
                             x = __builtin_amdgcn_fmed3f(x, -3.0f, 3.0f);
                             const float x2 = x * x;
