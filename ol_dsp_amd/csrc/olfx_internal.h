@@ -166,8 +166,9 @@ enum {
 //     (exact integer arithmetic), clamped to [1, pmax]; the fraction rounded once to fp32;
 //   chorus: the LFO phase to 53 bits, cos(2 pi x) by a double Taylor polynomial (|err| < 4e-15),
 //     d = cos D + D in double (D double), clamped to [0, cmax]; the fraction rounded once to fp32.
+//     Spec v2.1 (round 4): the polynomial's Horner steps and cos D + D are fused multiply-adds.
 // Gains, interpolation, lores~ and the mix stay fp32.  Host and gfx950 evaluate these identically
-// (integer ops, IEEE double + and * in a fixed order, no contraction).
+// (integer ops, IEEE double +, * and fma in a fixed order, no other contraction).
 OLFX_HD void pitch_split(uint32_t ph, uint32_t wi, uint32_t wf, uint32_t pmax, uint32_t &di, float &fr) {
     const uint64_t d = (uint64_t)ph * wi + (((uint64_t)ph * wf) >> 32);     // p W, 32.32
     const uint64_t lo = 1ull << 32, hi = (uint64_t)pmax << 32;
@@ -183,21 +184,23 @@ OLFX_HD double cos2pi_d(double x) {
     const double th = b * 6.283185307179586;
     const double t2 = th * th;
     // cos(th) = sum (-1)^k th^2k / (2k)!, k <= 9 (th <= pi/2: truncation < 4e-15), Horner in th^2
-    double r = -1.5619206968586225e-16;            // -1 / 18!
-    r = r * t2 + 4.779477332387385e-14;            //  1 / 16!
-    r = r * t2 - 1.1470745597729725e-11;           // -1 / 14!
-    r = r * t2 + 2.08767569878681e-09;             //  1 / 12!
-    r = r * t2 - 2.755731922398589e-07;            // -1 / 10!
-    r = r * t2 + 2.48015873015873e-05;             //  1 / 8!
-    r = r * t2 - 0.001388888888888889;             // -1 / 6!
-    r = r * t2 + 0.041666666666666664;             //  1 / 4!
-    r = r * t2 - 0.5;
-    r = r * t2 + 1.0;
+    // with fused multiply-adds (IEEE fusedMultiplyAdd: C fma on the host, v_fma_f64 here -- the
+    // same bits; spec v2.1, round 4: half the double operations of the unfused Horner)
+    double r = -1.5619206968586225e-16;                        // -1 / 18!
+    r = __builtin_fma(r, t2, 4.779477332387385e-14);           //  1 / 16!
+    r = __builtin_fma(r, t2, -1.1470745597729725e-11);         // -1 / 14!
+    r = __builtin_fma(r, t2, 2.08767569878681e-09);            //  1 / 12!
+    r = __builtin_fma(r, t2, -2.755731922398589e-07);          // -1 / 10!
+    r = __builtin_fma(r, t2, 2.48015873015873e-05);            //  1 / 8!
+    r = __builtin_fma(r, t2, -0.001388888888888889);           // -1 / 6!
+    r = __builtin_fma(r, t2, 0.041666666666666664);            //  1 / 4!
+    r = __builtin_fma(r, t2, -0.5);
+    r = __builtin_fma(r, t2, 1.0);
     return hi ? -r : r;
 }
 OLFX_HD double chorus_delay(uint64_t phase, double D, double cmax) {
     const double x = (double)(phase >> 11) * 1.1102230246251565e-16;         // 53-bit phase (2^-53: exact)
-    const double d = cos2pi_d(x) * D + D;
+    const double d = __builtin_fma(cos2pi_d(x), D, D);
     return d < 0.0 ? 0.0 : (d > cmax ? cmax : d);
 }
 OLFX_HD void chorus_split(uint64_t phase, double D, double cmax, uint32_t &di, float &fr) {

@@ -219,7 +219,8 @@ static void pitch_split(uint32_t ph, uint64_t Wfix, uint32_t pmax, uint32_t *di,
 }
 
 /* cos(2 pi x) in double: exact reduction to b in [0, 1/4], Taylor series of cos to th^18 in th^2
-   (|err| < 4e-15), Horner, no contraction -- the same operations as the GPU */
+   (|err| < 4e-15), Horner in fused multiply-adds (C99 fma: correctly rounded, as v_fma_f64; spec
+   v2.1), no other contraction -- the same operations as the GPU */
 double oracle_cos2pi_d(double x)
 {
     const double u = x - rint(x);
@@ -229,15 +230,15 @@ double oracle_cos2pi_d(double x)
     const double th = b * 6.283185307179586;
     const double t2 = th * th;
     double r = -1.5619206968586225e-16;
-    r = r * t2 + 4.779477332387385e-14;
-    r = r * t2 - 1.1470745597729725e-11;
-    r = r * t2 + 2.08767569878681e-09;
-    r = r * t2 - 2.755731922398589e-07;
-    r = r * t2 + 2.48015873015873e-05;
-    r = r * t2 - 0.001388888888888889;
-    r = r * t2 + 0.041666666666666664;
-    r = r * t2 - 0.5;
-    r = r * t2 + 1.0;
+    r = fma(r, t2, 4.779477332387385e-14);
+    r = fma(r, t2, -1.1470745597729725e-11);
+    r = fma(r, t2, 2.08767569878681e-09);
+    r = fma(r, t2, -2.755731922398589e-07);
+    r = fma(r, t2, 2.48015873015873e-05);
+    r = fma(r, t2, -0.001388888888888889);
+    r = fma(r, t2, 0.041666666666666664);
+    r = fma(r, t2, -0.5);
+    r = fma(r, t2, 1.0);
     return hi ? -r : r;
 }
 
@@ -246,7 +247,7 @@ double oracle_cos2pi_d(double x)
 static void chorus_split(uint64_t phase, double D, double cmax, uint32_t *di, float *fr)
 {
     const double x = (double)(phase >> 11) * 1.1102230246251565e-16;
-    double d = oracle_cos2pi_d(x) * D + D;
+    double d = fma(oracle_cos2pi_d(x), D, D);
     d = d < 0.0 ? 0.0 : (d > cmax ? cmax : d);
     *di = (uint32_t)d;
     *fr = (float)(d - (double)*di);
