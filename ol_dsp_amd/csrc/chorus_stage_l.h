@@ -85,16 +85,19 @@ __device__ __forceinline__ PlanL plan_chunk_l(uint64_t lfo_acc, uint64_t lfo_inc
         p.sB = lo & ~3;
         p.okB = a1 >= a0 && hi - p.sB < kWin;
     }
-    // chorus tap: the endpoint delays are computed exactly as the frames compute theirs; in between
-    // the delay stays within [min, max] of them up to the curvature of the LFO over 16 frames
-    // (< 1e-3 for every legal depth and rate), so floor(min - .01) .. floor(max + .01) bounds every
-    // frame's floor delay, and those two differ by at most one (|d'| <= 0.038 frame/frame)
+    // chorus tap: the endpoint delays in fp32 (the 24-bit phase, cos2pi to 3e-7, D rounded: within
+    // 5e-4 sample of the frames' own double delays, spec v2); in between the delay stays within
+    // [min, max] of them up to the curvature of the LFO over 16 frames (< 1e-3 for every legal depth
+    // and rate), so floor(min - .01) .. floor(max + .01) bounds every frame's floor delay, and those
+    // two differ by at most one (|d'| <= 0.038 frame/frame).  (Round 4: the endpoints in double cost
+    // two of the ten double cosines per lane and chunk; only the window bound depends on them.)
     p.sC = 0; p.hiC = 0;
     if (full) {
-        const double e0 = chorus_delay(lfo_acc + lfo_off, D, cmaxd);
-        const double e1 = chorus_delay(lfo_acc + last * lfo_inc + lfo_off, D, cmaxd);
-        const int dhi = min((int)(fmax(e0, e1) + 0.01), (int)cmaxd);
-        const int dlo = (int)fmax(fmin(e0, e1) - 0.01, 0.0);
+        const float Df = (float)D, cm = (float)cmaxd;
+        const float e0 = fminf(fmaxf(cos2pi(unit24h(lfo_acc + lfo_off)) * Df + Df, 0.0f), cm);
+        const float e1 = fminf(fmaxf(cos2pi(unit24h(lfo_acc + last * lfo_inc + lfo_off)) * Df + Df, 0.0f), cm);
+        const int dhi = min((int)(fmaxf(e0, e1) + 0.01f), (int)cmaxd);
+        const int dlo = (int)fmaxf(fminf(e0, e1) - 0.01f, 0.0f);
         p.sC = (-dhi - 1) & ~3;
         p.hiC = (int)last - dlo;
     }
