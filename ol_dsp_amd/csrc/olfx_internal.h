@@ -171,10 +171,12 @@ enum {
 // (integer ops, IEEE double +, * and fma in a fixed order, no other contraction).
 OLFX_HD void pitch_split(uint32_t ph, uint32_t wi, uint32_t wf, uint32_t pmax, uint32_t &di, float &fr) {
     const uint64_t d = (uint64_t)ph * wi + (((uint64_t)ph * wf) >> 32);     // p W, 32.32
-    const uint64_t lo = 1ull << 32, hi = (uint64_t)pmax << 32;
-    const uint64_t c = d < lo ? lo : (d > hi ? hi : d);
-    di = (uint32_t)(c >> 32);
-    fr = (float)(uint32_t)c * 2.3283064365386963e-10f;                   // 2^-32: exact scaling
+    // clamp to [1, pmax] in 32.32 on the two words (the oracle clamps the 64-bit value; the same
+    // result): below 1 or at / above pmax the fraction is 0, the integer part the bound
+    const uint32_t dh = (uint32_t)(d >> 32);
+    const bool inside = dh >= 1u && dh < pmax;
+    di = dh < 1u ? 1u : (dh > pmax ? pmax : dh);
+    fr = inside ? (float)(uint32_t)d * 2.3283064365386963e-10f : 0.0f;      // 2^-32: exact scaling
 }
 OLFX_HD double cos2pi_d(double x) {
     const double u = x - rint(x);                  // exact, u in [-0.5, 0.5]
