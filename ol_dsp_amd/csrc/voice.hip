@@ -48,6 +48,11 @@ __device__ __forceinline__ float polyblep(float dt, float t) {
     return lo ? rlo : (hi ? rhi : 0.0f);
 }
 
+// Oscillator::Process's saw, WAVE_POLYBLEP_SAW with amp 0.5 (o = 2t - 1, o -= blep, o *= -1, o * amp):
+// -((2t - 1) - blep) / 2 = fma(1/2, blep, 1/2 - t) -- 2t - 1 = 2 (t - 1/2) and the halving are
+// exact scalings, so both forms round the same sum once (up to the sign of an exact zero)
+__device__ __forceinline__ float saw_out(float t, float blep) { return __builtin_fmaf(0.5f, blep, 0.5f - t); }
+
 // sin(x) for x in [0, pi/4] (Svf::SetFreq's argument pi * min(0.25, fc / 2sr)): odd Taylor
 // polynomial to x^9 in Horner form, truncation < 2e-9; branch-free.
 __device__ __forceinline__ float sin_quarter(float x) {
@@ -276,12 +281,9 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
                         port_z = freq + port_c * (port_z - freq);
                         const float inc = port_z * inv_sr;
                         // Oscillator::Process, WAVE_POLYBLEP_SAW
-                        float o = (2.0f * phase) - 1.0f;
-                        o -= polyblep(inc, phase);
-                        o *= -1.0f;
+                        const float src = saw_out(phase, polyblep(inc, phase));
                         phase += inc;
                         phase = phase > 1.0f ? phase - 1.0f : phase;
-                        const float src = o * 0.5f;
                         ab = make_float2(src * drive, amp);   // ladder: Process's input scaling
                     }
                     if constexpr (CUT) {
@@ -585,18 +587,15 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                         rhi[q] = __builtin_elementwise_fma(qv[q], qv[q], qq[q]);
                     }
 #pragma unroll
-                    for (int q = 0; q < P; ++q) { rlo[q] = rlo[q] - 1.0f; rhi[q] = rhi[q] + 1.0f; o[q] = __builtin_elementwise_fma((f2)2.0f, t[q], (f2)-1.0f); }
+                    for (int q = 0; q < P; ++q) { rlo[q] = rlo[q] - 1.0f; rhi[q] = rhi[q] + 1.0f; o[q] = 0.5f - t[q]; }
 #pragma unroll
                     for (int q = 0; q < P; ++q) {
                         f2 blep;
 #pragma unroll
                         for (int h = 0; h < 2; ++h) blep[h] = lo[q][h] ? rlo[q][h] : (hi[q][h] ? rhi[q][h] : 0.0f);
-                        o[q] = o[q] - blep;
-                    }
-#pragma unroll
-                    for (int q = 0; q < P; ++q) {
-                        // o *= -1; o * 0.5 (== o * -0.5 exactly)
-                        const f2 y = (-o[q]) * 0.5f;
+                        // -((2t - 1) - blep) / 2 as fma(1/2, blep, 1/2 - t): 2t - 1 = 2 (t - 1/2) and the
+                        // halving are exact, so both round the same sum once (saw_out below)
+                        const f2 y = __builtin_elementwise_fma((f2)0.5f, blep, o[q]);
                         qo[(2 * q) * 64] = y.x;
                         qo[(2 * q + 1) * 64] = y.y;
                     }
@@ -607,10 +606,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                         const float t = phase;
                         phase += inc;
                         phase = phase > 1.0f ? phase - 1.0f : phase;
-                        float o = (2.0f * t) - 1.0f;
-                        o -= polyblep(inc, t);
-                        o *= -1.0f;
-                        qo[j * 64] = o * 0.5f;
+                        qo[j * 64] = saw_out(t, polyblep(inc, t));
                     }
                 }
             }
