@@ -85,6 +85,44 @@ struct Tap {
     __device__ __forceinline__ void advance() {
         if (S) { cur = nxt; nxt = pre; } else { cur = pre; }
     }
+    // the ring's write, for a ring with this one tap (IN1)
+    __device__ __forceinline__ void write(const DattorroArgs &a, uint32_t gw, uint32_t i, float4 v) { *grpu<L>(a, gw, i) = v; }
+};
+
+// A fixed tap whose whole ring lives in LDS for the launch (the standalone reverb's IN1, 128
+// positions: 32 groups x 64 lanes x 16 B = 32 KB per wave): the kernel copies the ring in before the
+// first chunk and back after the last (lds_in / lds_out), and the chunks read and write LDS only.
+// The lane's groups sit at lds[(g & 31) * 64 + lane] (a wave's accesses: 1 KB contiguous).
+template <int L, uint32_t D>
+struct LdsTap {
+    static constexpr uint32_t S = (0u - D) & 3u;
+    static constexpr uint32_t kGroups = kDtSize[L] / 4u;
+    float4 *lds;                                      // this lane's column: lds[g * 64]
+    float4 cur, nxt, pre;
+    __device__ __forceinline__ static uint32_t g0(uint32_t t0) { return (t0 - D) >> 2; }
+    __device__ __forceinline__ float4 &at(uint32_t g) const { return lds[(g & (kGroups - 1u)) * 64u]; }
+    __device__ __forceinline__ void lds_in(const DattorroArgs &a, uint32_t i) {
+#pragma unroll
+        for (uint32_t g = 0; g < kGroups; ++g) at(g) = *grpu<L>(a, g, i);
+    }
+    __device__ __forceinline__ void lds_out(const DattorroArgs &a, uint32_t i) const {
+#pragma unroll
+        for (uint32_t g = 0; g < kGroups; ++g) *grpu<L>(a, g, i) = at(g);
+    }
+    __device__ __forceinline__ void prime(const DattorroArgs &, uint32_t t0, uint32_t) {
+        cur = at(g0(t0));
+        if (S) nxt = at(g0(t0) + 1u);
+    }
+    __device__ __forceinline__ void prefetch(const DattorroArgs &, uint32_t t0, uint32_t) {
+        pre = at(g0(t0) + (S ? 2u : 1u));
+    }
+    __device__ __forceinline__ float get(int k) const {
+        return (int)S + k < 4 ? el(cur, (int)S + k) : el(nxt, (int)S + k - 4);
+    }
+    __device__ __forceinline__ void advance() {
+        if (S) { cur = nxt; nxt = pre; } else { cur = pre; }
+    }
+    __device__ __forceinline__ void write(const DattorroArgs &, uint32_t gw, uint32_t, float4 v) { at(gw) = v; }
 };
 
 // A modulated tank all-pass tap (verb.cpp:262-270): delay D + ex(t), with ex wave-uniform and
@@ -294,7 +332,7 @@ __device__ __forceinline__ void step_body(
     const uint32_t gw = t0 >> 2;
     pre.write(a, gw, i, xin);
     *grpu<DT_IN0>(a, gw, i) = make_float4(w_in0[0], w_in0[1], w_in0[2], w_in0[3]);
-    *grpu<DT_IN1>(a, gw, i) = make_float4(w_in1[0], w_in1[1], w_in1[2], w_in1[3]);
+    in1.write(a, gw, i, make_float4(w_in1[0], w_in1[1], w_in1[2], w_in1[3]));
     *grpu<DT_IN2>(a, gw, i) = make_float4(w_in2[0], w_in2[1], w_in2[2], w_in2[3]);
     *grpu<DT_IN3>(a, gw, i) = make_float4(w_in3[0], w_in3[1], w_in3[2], w_in3[3]);
     *grpu<DT_AP1A>(a, gw, i) = make_float4(w_ap1a[0], w_ap1a[1], w_ap1a[2], w_ap1a[3]);
@@ -327,7 +365,9 @@ __device__ __forceinline__ void step_body(
 //   dt_finish()                                    writes the recursive scalars back
 #define DT_PRIME_OP(T) T.prime(dt_args, t0, dt_i);
 #define DT_STAGE(A, I) DT_STAGE_PRE(A, I, olfx::dt::PreTap)
-#define DT_STAGE_PRE(A, I, PRE_T)                                                                        \
+#define DT_STAGE_PRE(A, I, PRE_T) DT_STAGE_X(A, I, PRE_T, (olfx::dt::Tap<DT_IN1, 107, 0>))
+#define DT_UNPAREN(...) __VA_ARGS__
+#define DT_STAGE_X(A, I, PRE_T, IN1_T)                                                                   \
     const DattorroArgs &dt_args = (A);                                                                   \
     const uint32_t dt_n = dt_args.n, dt_i = (I);                                                         \
     const float g_pre = dt_args.coef[DTC_PREFILTER * dt_n + dt_i];                                       \
@@ -341,7 +381,7 @@ __device__ __forceinline__ void step_body(
     float lp_pre = dt_args.state[DTS_LP_PRE * dt_n + dt_i];                                              \
     float lp_a = dt_args.state[DTS_LP_DAMP_A * dt_n + dt_i];                                             \
     float lp_b = dt_args.state[DTS_LP_DAMP_B * dt_n + dt_i];                                             \
-    olfx::dt::Tap<DT_IN0, 142, 0> in0; olfx::dt::Tap<DT_IN1, 107, 0> in1;                               \
+    olfx::dt::Tap<DT_IN0, 142, 0> in0; DT_UNPAREN IN1_T in1;                                             \
     olfx::dt::Tap<DT_IN2, 379, 0> in2; olfx::dt::Tap<DT_IN3, 277, 0> in3;                               \
     olfx::dt::Tap<DT_DL2B, 3163, 0> fbA; olfx::dt::Tap<DT_DL2A, 3720, 0> fbB;                           \
     olfx::dt::Tap<DT_DL1A, 4453, 0> dl1a; olfx::dt::Tap<DT_DL1B, 4217, 0> dl1b;                         \
