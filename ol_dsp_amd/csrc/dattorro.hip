@@ -22,11 +22,13 @@
 
 namespace olfx {
 
-// IN1 (the second input diffuser, 128 positions, verb.cpp:180) is read and written in LDS for the
-// launch (LdsTap): its 8 B/frame of ring traffic become 512 B in and out per instance and launch.
+// Uniform mode: IN1 (the second input diffuser, 128 positions, verb.cpp:180) is read and written
+// in LDS for the launch (LdsTap): its 8 B/frame of ring traffic become 512 B in and out per
+// instance and launch (rocprof, same box: 571 -> 557 us).  Gather mode keeps IN1 in HBM: with the
+// LDS ring its network measured 527 -> 554 us.
 template <bool GATHER>
 __global__ __launch_bounds__(64, 1) void dattorro_block_v4(DattorroArgs a) {
-    __shared__ float4 in1_ring[kDtSize[DT_IN1] / 4u * 64u];      // 32 KB: [group][lane]
+    __shared__ float4 in1_ring[GATHER ? 1u : kDtSize[DT_IN1] / 4u * 64u];      // 32 KB: [group][lane]
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
     const uint32_t n = a.n;
@@ -34,9 +36,12 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v4(DattorroArgs a) {
     const bool stereo = a.in_ch == 2;
 
     using Pre = typename std::conditional<GATHER, olfx::dt::PreBlock, olfx::dt::PreTap>::type;
-    DT_STAGE_X(a, i, Pre, (olfx::dt::LdsTap<DT_IN1, 107>));
-    in1.lds = in1_ring + threadIdx.x;
-    in1.lds_in(a, i);
+    using In1 = typename std::conditional<GATHER, olfx::dt::Tap<DT_IN1, 107, 0>, olfx::dt::LdsTap<DT_IN1, 107>>::type;
+    DT_STAGE_X(a, i, Pre, (In1));
+    if constexpr (!GATHER) {
+        in1.lds = in1_ring + threadIdx.x;
+        in1.lds_in(a, i);
+    }
     dt_prime(a.t0);
 
     // raw input frames are prefetched one chunk ahead like the taps (gather mode: no input here)
@@ -75,7 +80,7 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v4(DattorroArgs a) {
         }
     }
     dt_finish();
-    in1.lds_out(a, i);
+    if constexpr (!GATHER) in1.lds_out(a, i);
 }
 
 // Gather mode's pre-pass: one lane per instance, chunk by chunk in stream order as
