@@ -178,6 +178,18 @@ OLFX_HD void pitch_split(uint32_t ph, uint32_t wi, uint32_t wf, uint32_t pmax, u
     di = dh < 1u ? 1u : (dh > pmax ? pmax : dh);
     fr = inside ? (float)(uint32_t)d * 2.3283064365386963e-10f : 0.0f;      // 2^-32: exact scaling
 }
+// r t2 + c as one v_fma_f64 with the constant in an SGPR pair: left to itself the compiler keeps the
+// constants in VGPR pairs and emits v_fmac_f64 (destination = addend), i.e. a v_mov_b64 of the
+// constant before each step -- 7 extra VALU per cosine, 8 cosines per lane and chunk in the chorus
+OLFX_HD double fma_dc(double r, double t2, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(r), "v"(t2), "s"(c));
+    return d;
+#else
+    return __builtin_fma(r, t2, c);
+#endif
+}
 OLFX_HD double cos2pi_d(double x) {
     const double u = x - rint(x);                  // exact, u in [-0.5, 0.5]
     const double a = u < 0.0 ? -u : u;
@@ -189,13 +201,13 @@ OLFX_HD double cos2pi_d(double x) {
     // with fused multiply-adds (IEEE fusedMultiplyAdd: C fma on the host, v_fma_f64 here -- the
     // same bits; spec v2.1, round 4: half the double operations of the unfused Horner)
     double r = -1.5619206968586225e-16;                        // -1 / 18!
-    r = __builtin_fma(r, t2, 4.779477332387385e-14);           //  1 / 16!
-    r = __builtin_fma(r, t2, -1.1470745597729725e-11);         // -1 / 14!
-    r = __builtin_fma(r, t2, 2.08767569878681e-09);            //  1 / 12!
-    r = __builtin_fma(r, t2, -2.755731922398589e-07);          // -1 / 10!
-    r = __builtin_fma(r, t2, 2.48015873015873e-05);            //  1 / 8!
-    r = __builtin_fma(r, t2, -0.001388888888888889);           // -1 / 6!
-    r = __builtin_fma(r, t2, 0.041666666666666664);            //  1 / 4!
+    r = fma_dc(r, t2, 4.779477332387385e-14);                  //  1 / 16!
+    r = fma_dc(r, t2, -1.1470745597729725e-11);                // -1 / 14!
+    r = fma_dc(r, t2, 2.08767569878681e-09);                   //  1 / 12!
+    r = fma_dc(r, t2, -2.755731922398589e-07);                 // -1 / 10!
+    r = fma_dc(r, t2, 2.48015873015873e-05);                   //  1 / 8!
+    r = fma_dc(r, t2, -0.001388888888888889);                  // -1 / 6!
+    r = fma_dc(r, t2, 0.041666666666666664);                   //  1 / 4!
     r = __builtin_fma(r, t2, -0.5);
     r = __builtin_fma(r, t2, 1.0);
     return hi ? -r : r;
