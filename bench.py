@@ -83,8 +83,9 @@ PARAM_SET = {"dattorro_rpd": "dattorro_rpd", "chain_rpd": "chain_rpd"}
 # the event-free workload a control leg is compared with (same kind and instances)
 EVENT_FREE = {"voice_events": "voice", "chain_cc": "chain"}
 # legs in print order; the north star's 65,536 chains last (the end of the line survives any tail cut)
-DEFAULT_ALSO = ("voice_poly,voice_events,chain_cc,dattorro_rpd,chain_rpd,voice_moog,fxrack,voice,chain,"
-                "dattorro,chain_65536")
+# (dattorro / dattorro_rpd and chain_rpd / chain_65536 adjacent: each pair on the same box state)
+DEFAULT_ALSO = ("voice_poly,voice_events,chain_cc,voice_moog,fxrack,voice,chain,dattorro,dattorro_rpd,"
+                "chain_rpd,chain_65536")
 
 
 def parse(argv=None):

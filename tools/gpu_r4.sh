@@ -64,9 +64,9 @@ for m in "$@"; do
       w=${m#b:}
       step "bench_$w" 300 python bench.py --workload "$w" --also "" --steps 20 --warmup 5 --cpu-seconds 0 --full-json "" ;;
     p:*)
-      w=${m#p:}
+      w=${m#p:}; wl=$w; [ "$w" = chain_16384 ] && wl=chain
       step "prof_$w" 300 rocprofv3 --kernel-trace --stats -d "$out/prof_$w" -o run --output-format csv -- \
-          python3 bench.py --workload "$w" --also "" --steps 20 --warmup 5 --cpu-seconds 0 --no-parity --full-json ""
+          python3 bench.py --workload "$wl" --also "" --steps 20 --warmup 5 --cpu-seconds 0 --no-parity --full-json ""
       find "$out/prof_$w" -name '*kernel_trace.csv' -delete ;;
     tr:*)
       w=${m#tr:}
