@@ -63,6 +63,11 @@ __device__ __forceinline__ float sin_quarter(float x) {
     return __builtin_fmaf(x * x2, p, x);
 }
 
+// the cutoff sum (SynthVoice.h:46-47) clamped as Svf::SetFreq clamps it, fclamp(f, 1e-6, sr / 3):
+// fminf(fmaxf(f, 1e-6), fc_max) for 1e-6 <= fc_max and a non-NaN sum (ENV hands it to FREQ clamped:
+// the ENV + FILT SIMDs had the spare issue slots)
+__device__ __forceinline__ float svf_fc(float f, float fc_max) { return __builtin_amdgcn_fmed3f(f, 1.0e-6f, fc_max); }
+
 // Svf::SetFreq's damping, negated for FILT: -min(damp_res, min(2, lim)) = max(-damp_res, -2, -lim),
 // one v_max3 (the negations are operand modifiers); equal for every non-NaN lim
 __device__ __forceinline__ float neg_damp(float damp_res, float lim) {
@@ -387,7 +392,7 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
 // ---------------------------------------------------------------------------------------------
 // voice_block_v5 (SvfFilter voices): v4's arithmetic, operation for operation, over
 // FOUR role waves per workgroup of 64 voices (two workgroups per CU, two waves per SIMD):
-//   ENV  : the amp and filter Adsr, the cutoff sum                            -> (amp, fc_in)
+//   ENV  : the amp and filter Adsr, the cutoff sum, its clamp                 -> (amp, fc)
 //   OSC  : Port, the oscillator's phase, the polyBLEP saw                     -> src
 //   FREQ : Svf::SetFreq(fc_in)                                                -> (-damp, fq)
 //   FILT : the two Svf passes, Low() * amp, the output store
@@ -470,7 +475,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
         apply_gate_events(ev, flags0, xa0, xf0);
         const bool gate = (flags0 >> 8) & 1u;
         bool gprev_a = (flags0 >> 6) & 1u, gprev_f = (flags0 >> 7) & 1u;
-        const float amp_amt = c[VCC_AMP_AMT * n + i];
+        const float amp_amt = c[VCC_AMP_AMT * n + i], fc_max = c[VCC_FC_MAX * n + i];
         const float cutoff = c[VCC_CUTOFF * n + i], fenv_amt = c[VCC_FENV_AMT * n + i];
         Env ea, ef;
         ea.begin(gate, gprev_a, flags0 & 7u, xa0, c[VCC_ATK_D0A * n + i],
@@ -495,7 +500,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) {
                         X = X + D0 * (T - X);
                         const f2 m = X * AMT;
-                        qo[j * 64] = make_float2(m.x, __builtin_fmaf(m.y, fenv_amt, cutoff));
+                        qo[j * 64] = make_float2(m.x, svf_fc(__builtin_fmaf(m.y, fenv_amt, cutoff), fc_max));
                     }
                     // inside a segment the envelope is monotone toward a target beyond its bound
                     // (x += d0 (tgt - x) with tgt - x of one sign: each IEEE step keeps the
@@ -509,14 +514,14 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                         for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) {
                             const float amp = ea.step() * amp_amt;
                             const float fe = ef.step();
-                            qo[j * 64] = make_float2(amp, __builtin_fmaf(fe * 20000.0f, fenv_amt, cutoff));
+                            qo[j * 64] = make_float2(amp, svf_fc(__builtin_fmaf(fe * 20000.0f, fenv_amt, cutoff), fc_max));
                         }
                     }
                 } else {
                     for_chunk(len(k), [&](uint32_t j) {
                         const float amp = ea.step() * amp_amt;
                         const float fe = ef.step();
-                        qo[j * 64] = make_float2(amp, __builtin_fmaf(fe * 20000.0f, fenv_amt, cutoff));
+                        qo[j * 64] = make_float2(amp, svf_fc(__builtin_fmaf(fe * 20000.0f, fenv_amt, cutoff), fc_max));
                     });
                 }
             }
@@ -616,7 +621,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
         s[VCS_PORT_Z * n + i] = port_z;
     } else if (role == 2) {
         // ---- FREQ: Svf::SetFreq (its divisions use the hardware reciprocal, as in v4) ----
-        const float damp_res = c[VCC_DAMP_RES * n + i], fc_max = c[VCC_FC_MAX * n + i];
+        const float damp_res = c[VCC_DAMP_RES * n + i];
         const float inv_2sr = 1.0f / (c[VCC_SR * n + i] * 2.0f);
         for (uint32_t k = 0; k < nsteps; ++k) {
             if (k >= 1 && k + 1 < nsteps) {
@@ -631,9 +636,8 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     f2 x[P], x2[P], pp[P], fq[P];
 #pragma unroll
                     for (int q = 0; q < P; ++q) {
-                        // fminf(fmaxf(x, 1e-6), fc_max) for 1e-6 <= fc_max and a non-NaN cutoff sum
-                        const float c0 = __builtin_amdgcn_fmed3f(qi[(2 * q) * 64].y, 1.0e-6f, fc_max);
-                        const float c1 = __builtin_amdgcn_fmed3f(qi[(2 * q + 1) * 64].y, 1.0e-6f, fc_max);
+                        const float c0 = qi[(2 * q) * 64].y;          // clamped by ENV (svf_fc)
+                        const float c1 = qi[(2 * q + 1) * 64].y;
                         const f2 fcn = (f2){c0, c1} * inv_2sr;
                         const f2 arg = {__builtin_fminf(fcn.x, 0.25f), __builtin_fminf(fcn.y, 0.25f)};
                         x[q] = 3.1415927410125732f * arg;
@@ -659,7 +663,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     }
                 } else {
                     for (uint32_t j = 0; j < len(k - 1); ++j) {
-                        const float fc = __builtin_amdgcn_fmed3f(qi[j * 64].y, 1.0e-6f, fc_max);
+                        const float fc = qi[j * 64].y;
                         const float fcn = fc * inv_2sr;
                         const float arg = __builtin_fminf(fcn, 0.25f);
                         const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
