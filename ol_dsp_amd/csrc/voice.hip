@@ -476,6 +476,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
         const bool gate = (flags0 >> 8) & 1u;
         bool gprev_a = (flags0 >> 6) & 1u, gprev_f = (flags0 >> 7) & 1u;
         const float amp_amt = c[VCC_AMP_AMT * n + i], fc_max = c[VCC_FC_MAX * n + i];
+        const float amp_half = 0.5f * amp_amt;       // FILT's Low() halving folded in (exact scaling)
         const float cutoff = c[VCC_CUTOFF * n + i], fenv_amt = c[VCC_FENV_AMT * n + i];
         Env ea, ef;
         ea.begin(gate, gprev_a, flags0 & 7u, xa0, c[VCC_ATK_D0A * n + i],
@@ -495,7 +496,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     // both envelopes' Env::step_spec in packed operations (the pair lives in a
                     // register pair for the chunk), then (x_a amp_amt, x_f 20000)
                     f2 X = {ea.x, ef.x};
-                    const f2 D0 = {ea.d0, ef.d0}, T = {ea.tgt, ef.tgt}, AMT = {amp_amt, 20000.0f};
+                    const f2 D0 = {ea.d0, ef.d0}, T = {ea.tgt, ef.tgt}, AMT = {amp_half, 20000.0f};
 #pragma unroll
                     for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) {
                         X = X + D0 * (T - X);
@@ -512,14 +513,14 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                         ea.x = xa0;
                         ef.x = xf0;
                         for (uint32_t j = 0; j < (uint32_t)kVcChunk; ++j) {
-                            const float amp = ea.step() * amp_amt;
+                            const float amp = ea.step() * amp_half;
                             const float fe = ef.step();
                             qo[j * 64] = make_float2(amp, svf_fc(__builtin_fmaf(fe * 20000.0f, fenv_amt, cutoff), fc_max));
                         }
                     }
                 } else {
                     for_chunk(len(k), [&](uint32_t j) {
-                        const float amp = ea.step() * amp_amt;
+                        const float amp = ea.step() * amp_half;
                         const float fe = ef.step();
                         qo[j * 64] = make_float2(amp, svf_fc(__builtin_fmaf(fe * 20000.0f, fenv_amt, cutoff), fc_max));
                     });
@@ -699,13 +700,13 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     low = __builtin_fmaf(fq, band, low);
                     float high = notch - low;
                     band = __builtin_fmaf(-((drive * band) * band), band, __builtin_fmaf(fq, high, band));
-                    float out_low = 0.5f * low;
+                    const float low1 = low;
                     notch = src + ndamp * band;
                     low = __builtin_fmaf(fq, band, low);
                     high = notch - low;
                     band = __builtin_fmaf(-((drive * band) * band), band, __builtin_fmaf(fq, high, band));
-                    out_low = __builtin_fmaf(0.5f, low, out_low);
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(out_low * sa.y), ro, i * 4u, j * n * 4u, 0);
+                    // Low() = 0.5 low1 + 0.5 low2, times amp: (low1 + low2) (amp / 2), the same rounding (halvings exact)
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((low1 + low) * sa.y), ro, i * 4u, j * n * 4u, 0);
                 });
             }
             VC_SYNC();
