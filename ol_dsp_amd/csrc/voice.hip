@@ -350,13 +350,14 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
                         // (r(+-3) = +-1 exactly: the saturation, branch-free) with a hardware
                         // reciprocal
                         const float input = v.x, alpha = v.z, kq = k_or_unused * v.w;
-                        const float fb0 = -0.5f * input;
+                        const float fb0 = -0.5f * input, dold = L.old - input;
                         float total = 0.0f;
 #pragma unroll
                         for (int os = 0; os < 4; ++os) {
                             const float interp = 0.25f * (float)os;
-                            // (os = 0: fma(0, old, 1 input) is input exactly for a finite old)
-                            const float mixin = os == 0 ? input : __builtin_fmaf(interp, L.old, (1.0f - interp) * input);
+                            // the linear interpolation interp old + (1 - interp) input as
+                            // input + interp (old - input): one fma per oversample (os = 0: input)
+                            const float mixin = os == 0 ? input : __builtin_fmaf(interp, dold, input);
                             float x = __builtin_fmaf(-(L.z1[3] + fb0), kq, mixin);
                             x = __builtin_amdgcn_fmed3f(x, -3.0f, 3.0f);
                             const float x2 = x * x;
