@@ -283,7 +283,10 @@ enum : uint32_t {
 // one host-link round trip without first reading where they are.  A workgroup with more than
 // kVevCap records puts them all in the overflow list and marks slot 0:
 // x = VEV_MORE << 8 | count << 16, y = first record in ev_more (a second round trip, for it only).
-constexpr uint32_t kVevCap = 4;
+#ifndef OLFX_VEV_CAP
+#define OLFX_VEV_CAP 4
+#endif
+constexpr uint32_t kVevCap = OLFX_VEV_CAP;
 
 struct VoiceArgs {
     float *state;               // [VCS_N][n], MoogFilter voices [VCS_N_MOOG][n]
