@@ -635,7 +635,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     // stage by stage (a packed result read by the next instruction costs a wait
                     // state; four independent pairs fill them)
                     constexpr int P = kVcChunk / 2;
-                    f2 x[P], x2[P], pp[P], fq[P];
+                    f2 x[P], x2[P], pp[P], fq[P], sq[P];
 #pragma unroll
                     for (int q = 0; q < P; ++q) {
                         const float c0 = qi[(2 * q) * 64].y;          // clamped by ENV (svf_fc)
@@ -655,11 +655,13 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
 #pragma unroll
                     for (int q = 0; q < P; ++q) x2[q] = x[q] * x2[q];
 #pragma unroll
-                    for (int q = 0; q < P; ++q) fq[q] = 2.0f * __builtin_elementwise_fma(x2[q], pp[q], x[q]);
+                    for (int q = 0; q < P; ++q) sq[q] = __builtin_elementwise_fma(x2[q], pp[q], x[q]);   // sin(x); fq = 2 sin
 #pragma unroll
                     for (int q = 0; q < P; ++q) {
-                        const f2 rq = {__builtin_amdgcn_rcpf(fq[q].x), __builtin_amdgcn_rcpf(fq[q].y)};
-                        const f2 lim = __builtin_elementwise_fma((f2)2.0f, rq, fq[q] * -0.5f);
+                        const f2 rq = {__builtin_amdgcn_rcpf(sq[q].x), __builtin_amdgcn_rcpf(sq[q].y)};
+                        // 2 / fq - fq / 2 = 1 / s - s: one subtraction (and the reciprocal of s, not of 2 s)
+                        const f2 lim = rq - sq[q];
+                        fq[q] = sq[q] + sq[q];
                         qo[(2 * q) * 64] = make_float2(neg_damp(damp_res, lim.x), fq[q].x);
                         qo[(2 * q + 1) * 64] = make_float2(neg_damp(damp_res, lim.y), fq[q].y);
                     }
@@ -668,8 +670,8 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                         const float fc = qi[j * 64].y;
                         const float fcn = fc * inv_2sr;
                         const float arg = __builtin_fminf(fcn, 0.25f);
-                        const float fq = 2.0f * sin_quarter(3.1415927410125732f * arg);
-                        const float lim = __builtin_fmaf(2.0f, __builtin_amdgcn_rcpf(fq), fq * -0.5f);
+                        const float s1 = sin_quarter(3.1415927410125732f * arg), fq = s1 + s1;
+                        const float lim = __builtin_amdgcn_rcpf(s1) - s1;
                         qo[j * 64] = make_float2(neg_damp(damp_res, lim), fq);
                     }
                 }
