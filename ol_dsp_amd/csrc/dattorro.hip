@@ -260,6 +260,107 @@ __global__ __launch_bounds__(64) void dattorro_predelay_v2(DattorroArgs a) {
     }
 }
 
+// dattorro_predelay_v3: the whole call's block (<= 256 frames) at once.  The pass has no serial
+// dependence inside a block: every pre-delayed sample x[t - d] is either this block's own input
+// (d <= f, from LDS) or a ring position written before the block (d > f), so v2's chunk-by-chunk
+// chain of line loads becomes three phases per 32-instance workgroup (4 waves, 66 KB of LDS: two
+// workgroups per CU):
+//   1. the block's input rows (32 instances = 128 B per row and channel, 16-B pieces, all 16 loads
+//      in flight at once), mono (l + r) / 2 transposed into `mono` [instance][frame];
+//   2. per instance (wave-uniform), lanes = 64 consecutive frames: the ring reads t - d of one
+//      instance are consecutive positions of its instance-major row (two or three 128-B lines per
+//      instruction); d <= f reads `mono` instead; results into `outv` [instance][frame];
+//   3. the pre-delayed block out of `outv` as [F/4][n][4] rows (512 B per frame group) and the
+//      block's mono input into the ring (1 KB per instance), after every read of phase 2: a
+//      pre-delay above 8192 - F reads a slot this block overwrites, and reads it first, as
+//      DelayBuffer_process does (verb.cpp:107-110).
+// Needs 16-B aligned input rows (n % 4 == 0, plane % 4 == 0, in 16-B aligned); v2 otherwise.
+namespace {
+constexpr uint32_t kPd3J = 32;                      // instances per workgroup
+constexpr uint32_t kPd3F = 256;                     // frames per launch (the engine splits at 256)
+constexpr uint32_t kPd3Row = kPd3F + 1;             // LDS floats per instance row (odd)
+}
+
+__global__ __launch_bounds__(256) void dattorro_predelay_v3(DattorroArgs a) {
+    __shared__ float mono[kPd3J * kPd3Row];
+    __shared__ float outv[kPd3J * kPd3Row];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t n = a.n, F = a.n_frames, t0 = a.t0;
+    const uint32_t i0 = blockIdx.x * kPd3J, nv = min(n - i0, kPd3J);
+    const bool stereo = a.in_ch == 2;
+    constexpr uint32_t kOob = 0xFFFFFFF0u;
+    {   // 1. input rows: piece pc (instances 4 pc .. 4 pc + 3) of rows r0 + 32 m
+        const ch::Rsrc rIn0 = ch::rsrc(a.in, (uint64_t)F * n * 4u);
+        const ch::Rsrc rIn1 = ch::rsrc(stereo ? a.in + a.plane : a.in, (uint64_t)F * n * 4u);
+        const uint32_t pc = tid & 7u, r0 = tid >> 3;
+        float4 l[8], r[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const uint32_t f = r0 + 32u * (uint32_t)m;
+            const uint32_t off = f < F && 4u * pc < nv ? (f * n + i0 + 4u * pc) * 4u : kOob;
+            l[m] = ch::ld4(rIn0, off);
+            r[m] = stereo ? ch::ld4(rIn1, off) : l[m];
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            float *dst = mono + 4u * pc * kPd3Row + r0 + 32u * (uint32_t)m;
+            dst[0] = stereo ? (l[m].x + r[m].x) / 2 : l[m].x;
+            dst[kPd3Row] = stereo ? (l[m].y + r[m].y) / 2 : l[m].y;
+            dst[2 * kPd3Row] = stereo ? (l[m].z + r[m].z) / 2 : l[m].z;
+            dst[3 * kPd3Row] = stereo ? (l[m].w + r[m].w) / 2 : l[m].w;
+        }
+    }
+    __syncthreads();
+    const ch::Rsrc rRing = ch::rsrc(a.pre_im + (size_t)i0 * kPreSize, (uint64_t)nv * kPreSize * 4u);
+    {   // 2. wave w: instances 8 w .. 8 w + 7, lane = frame within each 64-frame group
+        float rv[8][4];
+        uint32_t dj[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            const uint32_t j = 8u * w + (uint32_t)jj;
+            dj[jj] = (uint32_t)a.coef[DTC_PREDELAY * n + min(i0 + j, n - 1u)];   // exact integer 0..8191
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const uint32_t f = 64u * (uint32_t)g + lane;
+                const uint32_t off = j < nv && f < F && dj[jj] > f
+                                         ? (j * kPreSize + ((t0 + f - dj[jj]) & (kPreSize - 1u))) * 4u : kOob;
+                rv[jj][g] = ch::ld1(rRing, off, 0);
+            }
+        }
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            const uint32_t j = 8u * w + (uint32_t)jj;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const uint32_t f = 64u * (uint32_t)g + lane;
+                outv[j * kPd3Row + f] = dj[jj] <= f ? mono[j * kPd3Row + f - dj[jj]] : rv[jj][g];
+            }
+        }
+    }
+    __syncthreads();
+    {   // 3a. the pre-delayed block: frame groups gs + 8 m, instance j
+        const ch::Rsrc rBlk = ch::rsrc(a.pre_block, (uint64_t)F * n * 4u);
+        const uint32_t j = tid & 31u, gs = tid >> 5;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const uint32_t g = gs + 8u * (uint32_t)m;
+            const float *src = outv + j * kPd3Row + 4u * g;
+            ch::st4(rBlk, 4u * g < F && j < nv ? (g * n + i0 + j) * 16u : kOob,
+                    make_float4(src[0], src[1], src[2], src[3]));
+        }
+    }
+    {   // 3b. the block's mono input into the ring: wave w's instances, lane = 4-position piece
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            const uint32_t j = 8u * w + (uint32_t)jj;
+            const float *src = mono + j * kPd3Row + 4u * lane;
+            ch::st4(rRing, 4u * lane < F && j < nv ? (j * kPreSize + ((t0 + 4u * lane) & (kPreSize - 1u))) * 4u : kOob,
+                    make_float4(src[0], src[1], src[2], src[3]));
+        }
+    }
+}
+
 // the pre-delay ring between layouts: position-major groups [size/4][n][4] <-> instance-major
 // [n][size]; one thread per (group, instance), reads or writes coalesced on the position-major side
 __global__ __launch_bounds__(256) void dattorro_pre_convert(DattorroArgs a, int to_im) {
@@ -271,13 +372,14 @@ __global__ __launch_bounds__(256) void dattorro_pre_convert(DattorroArgs a, int 
     else *pm = *im;
 }
 
-// OLFX_PREDELAY_KERNEL=1 runs v1 (A/B diagnostic)
-bool predelay_kernel_v1() {
-    static const bool v = [] {
+// v3 when the rows allow it; OLFX_PREDELAY_KERNEL=1 / 2 runs v1 / v2 (A/B diagnostics)
+int predelay_kernel(uint32_t n, uint64_t plane, const float *in) {
+    static const int forced = [] {
         const char *e = std::getenv("OLFX_PREDELAY_KERNEL");
-        return e && std::atoi(e) == 1;
+        return e ? std::atoi(e) : 0;
     }();
-    return v;
+    if (forced == 1 || forced == 2) return forced;
+    return n % 4u == 0u && plane % 4u == 0u && ((uintptr_t)in & 15u) == 0u ? 3 : 2;
 }
 
 hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s) {
@@ -291,10 +393,14 @@ hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s) {
     if (a.pre_im) {
         // per-workgroup ring resources: 64 instances x 32 KB; inputs and the block by 32-bit offsets
         if ((uint64_t)a.n_frames * a.n * 4u >= (1ull << 32)) return hipErrorInvalidValue;
-        if (predelay_kernel_v1())
+        const int v = predelay_kernel(a.n, a.plane, a.in);
+        if (v == 3 && a.n_frames > kPd3F) return hipErrorInvalidValue;   // the engine splits at 256
+        if (v == 1)
             hipLaunchKernelGGL(dattorro_predelay_v1, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
-        else
+        else if (v == 2)
             hipLaunchKernelGGL(dattorro_predelay_v2, dim3((a.n + 63) / 64), dim3(64), 0, s, a);
+        else
+            hipLaunchKernelGGL(dattorro_predelay_v3, dim3((a.n + kPd3J - 1) / kPd3J), dim3(256), 0, s, a);
         hipLaunchKernelGGL(dattorro_block_v4<true>, dim3(blocks), dim3(threads), 0, s, a);
     } else {
         hipLaunchKernelGGL(dattorro_block_v4<false>, dim3(blocks), dim3(threads), 0, s, a);

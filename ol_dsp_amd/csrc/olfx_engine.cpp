@@ -439,6 +439,7 @@ struct olfx_engine {
     // pre-delay ring and the block's pre-delayed input, allocated on first need
     float *dt_pre_im = nullptr, *dt_pre_blk = nullptr;
     bool dt_gather = false;      // the pre-delay ring's content is instance-major (dt_pre_im)
+    int dt_pre_kernel = 3;       // gather mode's pre-delay pass at the last block (predelay_kernel)
     bool dt_pre_check = true;    // a pre-delay changed: re-decide the mode at the next block
     float *dt_state = nullptr;
     float *dt_coef = nullptr;
@@ -983,6 +984,7 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, uin
             ga.t0 = (t0 + f0) & 0xFFFFu;
             ga.pre_im = e->dt_pre_im;
             ga.pre_block = e->dt_pre_blk;
+            e->dt_pre_kernel = predelay_kernel(ga.n, ga.plane, ga.in);
             r = launch_dattorro(ga, s);
         }
         break;
@@ -1733,9 +1735,10 @@ const char *olfx_kernel_name(const olfx_engine *e) {
     if (!e) return "";
     switch (e->kind) {
     case OLFX_KIND_DATTORRO:   // gather mode: the pre-delay pass ahead of the network, one launch pair per block
-        return e->dt_gather ? (predelay_kernel_v1() ? "dattorro_predelay_v1+dattorro_block_v4"
-                                                     : "dattorro_predelay_v2+dattorro_block_v4")
-                            : "dattorro_block_v4";
+        return !e->dt_gather ? "dattorro_block_v4"
+               : e->dt_pre_kernel == 1 ? "dattorro_predelay_v1+dattorro_block_v4"
+               : e->dt_pre_kernel == 2 ? "dattorro_predelay_v2+dattorro_block_v4"
+                                       : "dattorro_predelay_v3+dattorro_block_v4";
     case OLFX_KIND_CHORUS:
     case OLFX_KIND_PITCHSHIFT: return "chorus_block_v11";
     case OLFX_KIND_VOICE: return "voice_block_v5";

@@ -82,7 +82,7 @@ struct DattorroArgs {
     uint32_t in_ch;             // 1 or 2
     // gather mode (standalone reverb with per-instance pre-delays, dattorro.hip): the pre-delay
     // ring instance-major ([n][8192]) and the block's pre-delayed input ([n_frames/4][n][4]),
-    // written by dattorro_predelay_v1 ahead of the block; nullptr otherwise
+    // written by the pre-delay pass (dattorro_predelay_v1/v2/v3) ahead of the block; nullptr otherwise
     float *pre_im;
     float *pre_block;
 };
@@ -90,8 +90,9 @@ struct DattorroArgs {
 // pre-delays, dattorro_block_v4's own tap) and instance-major (gather mode): the ring's content
 // is copied into the other layout (to_im: position-major -> instance-major)
 hipError_t launch_dattorro_pre_convert(const DattorroArgs &a, bool to_im, hipStream_t s);
-// gather mode's pre-delay pass: v2 unless OLFX_PREDELAY_KERNEL=1 (A/B diagnostic)
-bool predelay_kernel_v1();
+// gather mode's pre-delay pass for these rows: 3 (16-B aligned input rows), else 2;
+// OLFX_PREDELAY_KERNEL=1 / 2 forces v1 / v2 (A/B diagnostics)
+int predelay_kernel(uint32_t n, uint64_t plane, const float *in);
 
 // ----------------------------------------------------------------------------------------------
 // Deterministic cos(2*pi*x): used by the chorus LFO (RNBO cycle~).  Branch-free (selects only, no

@@ -13,6 +13,7 @@
 #   te:<VAR=v>:<k>       GPU tests matching <k> with the environment variable VAR=v
 #   ts:<k>               GPU tests matching <k>, with their printed output (-s)
 #   vstamp               voice role stamps (build/ab/vcstamp.so, tools/voice_stamps.py) at 32,768 and 16,384
+#   abe:<workload>:<VAR=v> A/B: the workload under the default and VAR=v, three times each
 #   abl:<workload>:<lib> A/B of the main build against <lib> (tools/ab.sh)
 set -u
 out=gpurun_out
@@ -77,6 +78,14 @@ for m in "$@"; do
         step "ab_${w}_default_$r" 300 python bench.py --workload "$w" --also "" --steps 50 --warmup 5 \
             --cpu-seconds 0 --no-parity --full-json ""
         step "ab_${w}_k${kv}_$r" 300 env OLFX_CHORUS_KERNEL=$kv python bench.py --workload "$w" --also "" --steps 50 --warmup 5 --cpu-seconds 0 \
+            --no-parity --full-json ""
+      done ;;
+    abe:*)
+      r=${m#abe:}; w=${r%%:*}; kv=${r#*:}
+      for r in 1 2 3; do
+        step "abe_${w}_default_$r" 300 python bench.py --workload "$w" --also "" --steps 50 --warmup 5 \
+            --cpu-seconds 0 --no-parity --full-json ""
+        step "abe_${w}_env_$r" 300 env "$kv" python bench.py --workload "$w" --also "" --steps 50 --warmup 5 --cpu-seconds 0 \
             --no-parity --full-json ""
       done ;;
     bench)
