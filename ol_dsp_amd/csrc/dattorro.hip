@@ -281,13 +281,9 @@ constexpr uint32_t kPd3F = 256;                     // frames per launch (the en
 constexpr uint32_t kPd3Row = kPd3F + 1;             // LDS floats per instance row (odd)
 }
 
-// ONE: a single 33-KB region (four workgroups per CU): phase 2's results wait in registers while
-// the ring store reads `mono`, then take its place
-template <bool ONE>
 __global__ __launch_bounds__(256) void dattorro_predelay_v3(DattorroArgs a) {
     __shared__ float mono[kPd3J * kPd3Row];
-    __shared__ float outv_[ONE ? 1 : kPd3J * kPd3Row];
-    float *outv = ONE ? mono : outv_;
+    __shared__ float outv[kPd3J * kPd3Row];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t n = a.n, F = a.n_frames, t0 = a.t0;
@@ -317,8 +313,8 @@ __global__ __launch_bounds__(256) void dattorro_predelay_v3(DattorroArgs a) {
     }
     __syncthreads();
     const ch::Rsrc rRing = ch::rsrc(a.pre_im + (size_t)i0 * kPreSize, (uint64_t)nv * kPreSize * 4u);
-    float rv[8][4];
     {   // 2. wave w: instances 8 w .. 8 w + 7, lane = frame within each 64-frame group
+        float rv[8][4];
         uint32_t dj[8];
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
@@ -338,31 +334,11 @@ __global__ __launch_bounds__(256) void dattorro_predelay_v3(DattorroArgs a) {
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const uint32_t f = 64u * (uint32_t)g + lane;
-                const float v = dj[jj] <= f ? mono[j * kPd3Row + f - dj[jj]] : rv[jj][g];
-                if (ONE) rv[jj][g] = v;
-                else outv[j * kPd3Row + f] = v;
+                outv[j * kPd3Row + f] = dj[jj] <= f ? mono[j * kPd3Row + f - dj[jj]] : rv[jj][g];
             }
         }
     }
     __syncthreads();
-    auto ring_store = [&] {   // 3b. the block's mono input into the ring: wave w's instances, lane = 4-position piece
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-            const uint32_t j = 8u * w + (uint32_t)jj;
-            const float *src = mono + j * kPd3Row + 4u * lane;
-            ch::st4(rRing, 4u * lane < F && j < nv ? (j * kPreSize + ((t0 + 4u * lane) & (kPreSize - 1u))) * 4u : kOob,
-                    make_float4(src[0], src[1], src[2], src[3]));
-        }
-    };
-    if (ONE) {
-        ring_store();
-        __syncthreads();
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) outv[(8u * w + (uint32_t)jj) * kPd3Row + 64u * (uint32_t)g + lane] = rv[jj][g];
-        __syncthreads();
-    }
     {   // 3a. the pre-delayed block: frame groups gs + 8 m, instance j
         const ch::Rsrc rBlk = ch::rsrc(a.pre_block, (uint64_t)F * n * 4u);
         const uint32_t j = tid & 31u, gs = tid >> 5;
@@ -374,7 +350,15 @@ __global__ __launch_bounds__(256) void dattorro_predelay_v3(DattorroArgs a) {
                     make_float4(src[0], src[1], src[2], src[3]));
         }
     }
-    if (!ONE) ring_store();
+    {   // 3b. the block's mono input into the ring: wave w's instances, lane = 4-position piece
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            const uint32_t j = 8u * w + (uint32_t)jj;
+            const float *src = mono + j * kPd3Row + 4u * lane;
+            ch::st4(rRing, 4u * lane < F && j < nv ? (j * kPreSize + ((t0 + 4u * lane) & (kPreSize - 1u))) * 4u : kOob,
+                    make_float4(src[0], src[1], src[2], src[3]));
+        }
+    }
 }
 
 // the pre-delay ring between layouts: position-major groups [size/4][n][4] <-> instance-major
@@ -388,15 +372,14 @@ __global__ __launch_bounds__(256) void dattorro_pre_convert(DattorroArgs a, int 
     else *pm = *im;
 }
 
-// v3 when the rows allow it; OLFX_PREDELAY_KERNEL=1 / 2 / 4 runs v1 / v2 / v3<ONE> (A/B diagnostics)
+// v3 when the rows allow it; OLFX_PREDELAY_KERNEL=1 / 2 runs v1 / v2 (A/B diagnostics)
 int predelay_kernel(uint32_t n, uint64_t plane, const float *in) {
     static const int forced = [] {
         const char *e = std::getenv("OLFX_PREDELAY_KERNEL");
         return e ? std::atoi(e) : 0;
     }();
     if (forced == 1 || forced == 2) return forced;
-    const bool rows16 = n % 4u == 0u && plane % 4u == 0u && ((uintptr_t)in & 15u) == 0u;
-    return !rows16 ? 2 : forced == 4 ? 4 : 3;
+    return n % 4u == 0u && plane % 4u == 0u && ((uintptr_t)in & 15u) == 0u ? 3 : 2;
 }
 
 hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s) {
@@ -411,15 +394,13 @@ hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s) {
         // per-workgroup ring resources: 64 instances x 32 KB; inputs and the block by 32-bit offsets
         if ((uint64_t)a.n_frames * a.n * 4u >= (1ull << 32)) return hipErrorInvalidValue;
         const int v = predelay_kernel(a.n, a.plane, a.in);
-        if (v >= 3 && a.n_frames > kPd3F) return hipErrorInvalidValue;   // the engine splits at 256
+        if (v == 3 && a.n_frames > kPd3F) return hipErrorInvalidValue;   // the engine splits at 256
         if (v == 1)
             hipLaunchKernelGGL(dattorro_predelay_v1, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
         else if (v == 2)
             hipLaunchKernelGGL(dattorro_predelay_v2, dim3((a.n + 63) / 64), dim3(64), 0, s, a);
-        else if (v == 3)
-            hipLaunchKernelGGL(dattorro_predelay_v3<false>, dim3((a.n + kPd3J - 1) / kPd3J), dim3(256), 0, s, a);
         else
-            hipLaunchKernelGGL(dattorro_predelay_v3<true>, dim3((a.n + kPd3J - 1) / kPd3J), dim3(256), 0, s, a);
+            hipLaunchKernelGGL(dattorro_predelay_v3, dim3((a.n + kPd3J - 1) / kPd3J), dim3(256), 0, s, a);
         hipLaunchKernelGGL(dattorro_block_v4<true>, dim3(blocks), dim3(threads), 0, s, a);
     } else {
         hipLaunchKernelGGL(dattorro_block_v4<false>, dim3(blocks), dim3(threads), 0, s, a);
