@@ -15,13 +15,15 @@ from collections import defaultdict
 
 
 def load(d, kernel_sub):
-    """{kernel: {counter: [per-dispatch values]}} for kernels whose name contains kernel_sub."""
+    """{kernel: {counter: [per-dispatch values]}} for kernels whose name contains kernel_sub
+    (or one of its "|"-separated alternatives)."""
+    subs = kernel_sub.split("|")
     vals = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = row.get("Kernel_Name", "")
-                if kernel_sub not in k:
+                if not any(x in k for x in subs):
                     continue
                 vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return vals
