@@ -79,7 +79,7 @@ __device__ __forceinline__ float neg_damp(float damp_res, float lim) {
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 struct Ladder {
-    float z0[4], z1[4];
+    float z0[4], z1[4], old;
 };
 
 // The block's folded note events (VoiceArgs::ev, VEV_*) of this lane's voice: the wave reads its
@@ -221,18 +221,13 @@ __device__ __forceinline__ void for_chunk(uint32_t m, F &&f) {
 // waves that hand each sample's values on through an LDS double buffer (one barrier per 8-sample
 // chunk):
 //   feed wave   : amp envelope, portamento, oscillator, filter envelope, cutoff,
-//                 LadderFilter::SetFreq -> SetAlpha, and the ladder's per-sample inputs that do not
-//                 depend on its state: the oversampled input mix (input, and input + interp (old -
-//                 input) for interp = 1/4, 1/2, 3/4), the feedback offset -input/2, K * Qadjust
-//                 -> (input, mix1, mix2, mix3), (-input/2, amp, alpha, K Qadjust)
-//   filter wave : LadderFilter::Process's recurrence, output store
-// The ladder's serial recurrence dominates the voice (the filter wave issues ~2.4x the feed's VALU
-// per sample), so the feed roles share one wave and take every operation off the filter's that
-// does not need its state (the same operations on the same operands: bit-identical).  (The Svf
+//                 LadderFilter::SetFreq -> SetAlpha          -> (src * drive, amp, alpha, Qadjust)
+//   filter wave : LadderFilter::Process, output store
+// The ladder's serial recurrence dominates the voice, so the feed roles share one wave.  (The Svf
 // voice runs voice_block_v5 below, over four role waves.)
 __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
     constexpr uint32_t kRoles = 2u;
-    __shared__ float4 q[2][kVcChunk][2][64];
+    __shared__ float4 q[2][kVcChunk][64];
     __shared__ uint32_t fflags[64];
     __shared__ uint2 evslot[64];
     const uint32_t n = a.n;
@@ -252,7 +247,6 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
     // ---------------- amp and/or cutoff roles (compile-time role flags: straight-line chunks) ----------------
     auto feed = [&](auto amp_c, auto cut_c) {
         constexpr bool AMP = decltype(amp_c)::value, CUT = decltype(cut_c)::value;
-        static_assert(AMP && CUT, "v4 runs one feed wave");
         // the block's note events first (one feed wave per workgroup applies them); the state loads
         // are issued before the event read, so their latency hides under its host-link round trip
         uint32_t flags0 = __float_as_uint(s[VCS_FLAGS * n + i]);
@@ -268,8 +262,6 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
         // ladder: drive_scaled (VCC_DRIVE), 1/(4 sr) (VCC_FC_MAX)
         const float drive = c[VCC_DRIVE * n + i];
         const float fc_max = c[VCC_FC_MAX * n + i];
-        const float ladder_k = c[VCC_LADDER_K * n + i];
-        float old = s[VCS_LOLD * n + i];                     // the ladder's previous input
         float phase = s[VCS_PHASE * n + i];
         float port_z = s[VCS_PORT_Z * n + i];
         bool gprev_a = (flags0 >> 6) & 1u, gprev_f = (flags0 >> 7) & 1u;
@@ -285,7 +277,7 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
             if (k < nchunks) {
                 const uint32_t f0 = k * kVcChunk;
                 const uint32_t m = nf - f0 < (uint32_t)kVcChunk ? nf - f0 : (uint32_t)kVcChunk;
-                float4 *qb = &q[k & 1][0][0][lane];
+                float4 *qb = &q[k & 1][0][lane];
                 for_chunk(m, [&](uint32_t j) {
                     float2 ab, cd;
                     if constexpr (AMP) {
@@ -308,13 +300,13 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
                         cd.x = wc * __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(-0.0202f, wc, 0.1381f), wc, -0.4324f), wc, 0.9892f);
                         cd.y = __builtin_fmaf(__builtin_fmaf(-0.05f, wc2, -0.095f), wc2, __builtin_fmaf(0.0536f, wc, 1.006f));
                     }
-                    // the oversampled input mix as input + interp (old - input): one fma per
-                    // oversample (contracted, see Contraction above)
-                    const float input = ab.x, dold = old - input;
-                    qb[j * 128] = make_float4(input, __builtin_fmaf(0.25f, dold, input),
-                                              __builtin_fmaf(0.5f, dold, input), __builtin_fmaf(0.75f, dold, input));
-                    qb[j * 128 + 64] = make_float4(-0.5f * input, ab.y, cd.x, ladder_k * cd.y);
-                    old = input;
+                    if constexpr (AMP && CUT) {
+                        qb[j * 64] = make_float4(ab.x, ab.y, cd.x, cd.y);
+                    } else if constexpr (AMP) {
+                        reinterpret_cast<float2 *>(&qb[j * 64])[0] = ab;
+                    } else {
+                        reinterpret_cast<float2 *>(&qb[j * 64])[1] = cd;
+                    }
                 });
             }
             __syncthreads();
@@ -328,7 +320,6 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
             s[VCS_PORT_Z * n + i] = port_z;
             s[VCS_ENVA_X * n + i] = ea.x;
             s[VCS_FLAGS * n + i] = __uint_as_float(ea.mode | fbits | (uint32_t)gprev_a << 6 | (uint32_t)gate << 8);
-            s[VCS_LOLD * n + i] = old;
             if (ev.op & VEV_FREQ) s[VCS_FREQ * n + i] = freq;
         }
         if constexpr (CUT) s[VCS_ENVF_X * n + i] = ef.x;
@@ -337,31 +328,36 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
         feed(std::true_type{}, std::true_type{});
     } else {
         // ---------------- filter role: LadderFilter::Process ----------------
+        const float k_or_unused = c[VCC_DAMP_RES * n + i];     // ladder: K (VCC_LADDER_K)
         Ladder L;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             L.z0[k] = s[(VCS_LZ0 + k) * n + i];
             L.z1[k] = s[(VCS_LZ1 + k) * n + i];
         }
+        L.old = s[VCS_LOLD * n + i];
         float *out = a.out + i;
         for (uint32_t k = 0; k <= nchunks; ++k) {
             if (k > 0) {
                 const uint32_t f0 = (k - 1) * kVcChunk;
                 const uint32_t m = nf - f0 < (uint32_t)kVcChunk ? nf - f0 : (uint32_t)kVcChunk;
-                const float4 *qb = &q[(k - 1) & 1][0][0][lane];
+                const float4 *qb = &q[(k - 1) & 1][0][lane];
                 for_chunk(m, [&](uint32_t j) {
-                    const float4 mix = qb[j * 128], v = qb[j * 128 + 64];
+                    const float4 v = qb[j * 64];
                     float y;
                     {
                         // contracted (see Contraction above); the Pade tanh as r(med3(x, -3, 3))
                         // (r(+-3) = +-1 exactly: the saturation, branch-free) with a hardware
-                        // reciprocal.  The input mix, -input/2 and K * Qadjust come from the feed.
-                        const float fb0 = v.x, alpha = v.z, kq = v.w;
-                        const float mixes[4] = {mix.x, mix.y, mix.z, mix.w};
+                        // reciprocal
+                        const float input = v.x, alpha = v.z, kq = k_or_unused * v.w;
+                        const float fb0 = -0.5f * input, dold = L.old - input;
                         float total = 0.0f;
 #pragma unroll
                         for (int os = 0; os < 4; ++os) {
-                            const float mixin = mixes[os];
+                            const float interp = 0.25f * (float)os;
+                            // the linear interpolation interp old + (1 - interp) input as
+                            // input + interp (old - input): one fma per oversample (os = 0: input)
+                            const float mixin = os == 0 ? input : __builtin_fmaf(interp, dold, input);
                             float x = __builtin_fmaf(-(L.z1[3] + fb0), kq, mixin);
                             x = __builtin_amdgcn_fmed3f(x, -3.0f, 3.0f);
                             const float x2 = x * x;
@@ -376,6 +372,7 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
                             }
                             total = __builtin_fmaf(u, 0.25f, total);
                         }
+                        L.old = input;
                         y = total * v.y;
                     }
                     out[(size_t)(f0 + j) * n] = y;
@@ -389,6 +386,7 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
             s[(VCS_LZ0 + k) * n + i] = L.z0[k];
             s[(VCS_LZ1 + k) * n + i] = L.z1[k];
         }
+        s[VCS_LOLD * n + i] = L.old;
     }
 }
 
