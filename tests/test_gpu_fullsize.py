@@ -119,6 +119,31 @@ def test_full_size_stream_kinds(cuda, kind, n):
     e.close()
 
 
+@pytest.mark.parametrize("pset,kind", [("dattorro_rpd", "dattorro"), ("chain_rpd", "chain")])
+def test_full_size_random_predelay(cuda, pset, kind):
+    """The bench's dattorro_rpd / chain_rpd legs at 65,536: a random pre-delay per instance
+    (verb.cpp:137-139), so the standalone reverb runs gather mode (dattorro_predelay_v3 ahead of
+    the network) and the chain its per-lane pre-delay gather.  Two blocks; clones bit-identical,
+    sampled instances (workgroup edges included) bit-exact against the oracle."""
+    import torch
+    n = 65536
+    p = _params(pset, 0, n, clone=True)
+    xs = _inputs(0, n, 2, cuda, clone=True)
+    e = _engine(kind, n)
+    e.set_params(0, p)
+    y = _run(e, xs)
+    if kind == "dattorro":
+        assert e.kernel_name.startswith("dattorro_predelay_v3")
+    assert torch.isfinite(y).all()
+    _check_clones(y, n)
+    idx = np.union1d(_sample_idx(n), np.array([30, 32, 34, 96, 65502, 65534], np.int64))
+    x = torch.cat(xs, 1)[:, :, idx].cpu().numpy()
+    yr = _oracle(kind, p, idx, np.ascontiguousarray(x))
+    yg = y[:, :, idx].cpu().numpy()
+    assert bits_equal(yg, yr), first_mismatch(yg, yr)
+    e.close()
+
+
 def test_chain_persistent_groups_ragged(cuda):
     """chain_block_v5 runs one workgroup per CU over 64-instance groups back to back, its queues and
     counters running on across groups.  n = CUs x 64 x 2 + 37 instances: every workgroup runs two
