@@ -37,6 +37,10 @@ __device__ __forceinline__ Rsrc rsrc(const void *p, uint64_t bytes) {
 }
 // cache policy of the streamed accesses (block input/output, ring stores): 0 = default,
 // 2 = nt (gfx950 aux bit 1).  A/B knob; the shipped value is measured.
+// s_setprio around the line-carry stage's line loads (A/B knob, 0 = off)
+#ifndef OLFX_CH_PRIO
+#define OLFX_CH_PRIO 0
+#endif
 #ifndef OLFX_STREAM_AUX
 #define OLFX_STREAM_AUX 0
 #endif

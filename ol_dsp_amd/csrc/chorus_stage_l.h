@@ -229,6 +229,9 @@ struct ChStageL {
     template <int HI>
     __device__ __forceinline__ void load_lines(const PlanL &p, uint32_t w, bool first) {
         constexpr int LO = HI ^ 1;
+#if OLFX_CH_PRIO
+        __builtin_amdgcn_s_setprio(OLFX_CH_PRIO);   // A/B knob: the line loads ahead of the other wave's arithmetic
+#endif
         const int s[3] = {p.sA, p.sB, p.sC};
         uint32_t s15n = 0;
         int pk[3];
@@ -267,6 +270,9 @@ struct ChStageL {
             strag_slot = need ? top - ((w + (uint32_t)p.sC)) : (uint32_t)kWin;
             if (need) strag = ld1(rC, own_cb() + (top & cmask) * 8u, 0);
         }
+#if OLFX_CH_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
     }
 
     // lines of tap t -> the chunk's LDS window ([tap][slot][lane], slot = position - window start)
