@@ -41,6 +41,9 @@ __device__ __forceinline__ Rsrc rsrc(const void *p, uint64_t bytes) {
 #ifndef OLFX_CH_PRIO
 #define OLFX_CH_PRIO 0
 #endif
+#ifndef OLFX_CH_PRIO_IN
+#define OLFX_CH_PRIO_IN 0
+#endif
 #ifndef OLFX_STREAM_AUX
 #define OLFX_STREAM_AUX 0
 #endif

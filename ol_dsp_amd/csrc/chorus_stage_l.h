@@ -495,7 +495,13 @@ struct ChStageL {
             }
         }
         started = true;
+#if OLFX_CH_PRIO_IN
+        __builtin_amdgcn_s_setprio(OLFX_CH_PRIO_IN);   // A/B knob: the next chunk's input loads too
+#endif
         prefetch();
+#if OLFX_CH_PRIO_IN
+        __builtin_amdgcn_s_setprio(0);
+#endif
 
         const bool fast = C == kChunk && __all(cur.okA && cur.okB);
         if (fast) {
