@@ -14,6 +14,7 @@
 #   ts:<k>               GPU tests matching <k>, with their printed output (-s)
 #   vstamp               voice role stamps (build/ab/vcstamp.so, tools/voice_stamps.py) at 32,768 and 16,384
 #   abe:<workload>:<VAR=v> A/B: the workload under the default and VAR=v, three times each
+#   abm:<w1,w2>:<lib1,lib2> A/B of the main build against several libs over several workloads
 #   abl:<workload>:<lib> A/B of the main build against <lib> (tools/ab.sh)
 set -u
 out=gpurun_out
@@ -58,6 +59,10 @@ for m in "$@"; do
       r=${m#abl:}; w=${r%%:*}; lib=${r#*:}
       step "abl_$w" 600 bash tools/ab.sh "$w" main "$lib"
       cat "$out/abl_$w.log" ;;
+    abm:*)
+      r=${m#abm:}; w=${r%%:*}; libs=${r#*:}
+      step "abm_$(echo "$w" | tr -c 'a-zA-Z0-9_' '_')" 900 bash tools/ab.sh "${w//,/ }" main ${libs//,/ }
+      cat "$out/abm_$(echo "$w" | tr -c 'a-zA-Z0-9_' '_').log" ;;
     tests)
       step pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
       step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
