@@ -405,6 +405,12 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
 // of a full chunk run speculatively (Env::step_spec, no per-sample lane vote and branch) and the
 // chunk is redone exactly when a lane's segment ended in it.  Roles are assigned by SIMD (below).
 // ---------------------------------------------------------------------------------------------
+#ifndef OLFX_VC_PRIO
+#define OLFX_VC_PRIO 0
+#endif
+#ifndef OLFX_VC_PRIO_OSC
+#define OLFX_VC_PRIO_OSC 0
+#endif
 __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     __shared__ float2 eq[3][kVcChunk][64];      // ENV -> OSC, FREQ (fc_in), FILT (amp): three chunks live
     __shared__ float sq[2][kVcChunk][64];       // OSC -> FILT: src
@@ -439,6 +445,11 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
         if (m == 15u) role = hw_simd[4] ? 3u - sm : sm;
         role = __builtin_amdgcn_readfirstlane(role);
     }
+#endif
+#if OLFX_VC_PRIO
+    // A/B knob: the roles with a per-sample recurrence (FILT, and OSC with OLFX_VC_PRIO_OSC) ahead
+    // of their SIMD partner at issue
+    if (role == 3u || (OLFX_VC_PRIO_OSC && role == 1u)) __builtin_amdgcn_s_setprio(OLFX_VC_PRIO);
 #endif
     const uint32_t i0 = blockIdx.x * 64 + lane;
     const uint32_t i = i0 < n ? i0 : n - 1;      // dead lanes mirror voice n-1, as in v4
