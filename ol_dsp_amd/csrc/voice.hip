@@ -405,8 +405,10 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
 // of a full chunk run speculatively (Env::step_spec, no per-sample lane vote and branch) and the
 // chunk is redone exactly when a lane's segment ended in it.  Roles are assigned by SIMD (below).
 // ---------------------------------------------------------------------------------------------
+// FILT (the Svf recurrence, the critical chain of the ENV + FILT pair) issues ahead of ENV on
+// their SIMD: ~2 % same-box; OSC too was slower.  0 = off.
 #ifndef OLFX_VC_PRIO
-#define OLFX_VC_PRIO 0
+#define OLFX_VC_PRIO 2
 #endif
 #ifndef OLFX_VC_PRIO_OSC
 #define OLFX_VC_PRIO_OSC 0
@@ -447,7 +449,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     }
 #endif
 #if OLFX_VC_PRIO
-    // A/B knob: the roles with a per-sample recurrence (FILT, and OSC with OLFX_VC_PRIO_OSC) ahead
+    // the roles with a per-sample recurrence (FILT; OSC with the A/B knob OLFX_VC_PRIO_OSC) ahead
     // of their SIMD partner at issue
     if (role == 3u || (OLFX_VC_PRIO_OSC && role == 1u)) __builtin_amdgcn_s_setprio(OLFX_VC_PRIO);
 #endif
