@@ -1085,9 +1085,7 @@ int run_frames(olfx_engine *e, const float *in, float *out, uint32_t n_frames, h
     const uint32_t ich = in_channels(e->kind), och = out_channels(e->kind);
     const uint32_t F = (uint32_t)std::max<uint64_t>(4, std::min<uint64_t>(n_frames, ((1ull << 26) / (2 * n)) & ~3ull));
     if (e->tile_floats < (size_t)2 * F * n) {
-        if (e->dt_pre_im) (void)hipFree(e->dt_pre_im);
-    if (e->dt_pre_blk) (void)hipFree(e->dt_pre_blk);
-    if (e->tile_in) (void)hipFree(e->tile_in);
+        if (e->tile_in) (void)hipFree(e->tile_in);
         if (e->tile_out) (void)hipFree(e->tile_out);
         e->tile_in = e->tile_out = nullptr;
         e->tile_floats = 0;
@@ -1486,10 +1484,16 @@ int olfx_set_member(olfx_engine *e, uint32_t inst, uint32_t field, float value) 
     if (!is_voice_kind(e->kind)) return olfx_set_params(e, inst, 1, field, 1, &value);
     if (inst >= e->n || field >= e->n_params) return e->fail(OLFX_E_ARG, "olfx_set_member: out of range");
     if (const char *why = bad_value(e, field, value)) return e->fail(OLFX_E_ARG, "olfx_set_member: %s", why);
-    // after the first Update() the derived components follow the members (set_params); a member
-    // written then would take effect at the next block as if Update() had run, which SynthVoice
-    // does not do (SynthVoice.h:66-98): refused instead of silently diverging
-    if (e->configured[inst])
+    // SynthVoice::Process reads filter_cutoff, filter_env_amount and amp_env_amount itself every
+    // sample (SynthVoice.h:42-52): writing them takes effect at once, Update()d or not.  Re-deriving
+    // at the next block changes nothing else, since every other member still holds the value the
+    // last Update() saw (they change only through olfx_set_params, i.e. with an Update()).
+    const bool process_reads = field == OLFX_VC_FILTER_CUTOFF || field == OLFX_VC_FILTER_ENV_AMOUNT ||
+                               field == OLFX_VC_AMP_ENV_AMOUNT;
+    // the other members feed the components only through Update() (SynthVoice.h:66-98); written
+    // after the first Update() they would take effect at the next block as if Update() had run,
+    // which SynthVoice does not do: refused instead of silently diverging
+    if (e->configured[inst] && !process_reads)
         return e->fail(OLFX_E_STATE, "olfx_set_member: instance %u is already Update()d (use olfx_set_params)", inst);
     store_param(e, field, inst, value);                 // no Update(): `configured` unchanged
     mark_dirty(e, inst, 1);

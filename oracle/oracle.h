@@ -85,6 +85,12 @@ int oracle_voice_note(oracle_voice *o, int inst, int on, int note);
 /* 0 NoteOff, 1 NoteOn, 2 GateOn, 3 GateOff, 4 SetFrequency(value Hz) (Voice.h:33-57) */
 int oracle_voice_event(oracle_voice *o, int inst, int type, int note, float value);
 int oracle_voice_process(oracle_voice *o, float *out, int n_frames, int n_threads);
+/* arith 1: the GPU kernels' arithmetic (contractions, sine polynomial, v_rcp model; voice_ref.c),
+   0: the unfused restatement (default) */
+int oracle_voice_set_arith(oracle_voice *o, int kernel);
+/* v_rcp_f32's 2^23 results over the mantissas of [1, 2) (copied); NULL: correctly rounded 1/x */
+int oracle_rcp_table_set(const uint32_t *tab);
+float oracle_rcp_model(float x);
 
 /* ---- fxlib effect rack ol::fx::FxRack<2> (spec oracle for the DaisySP parts, parity unpinned) ---- */
 enum {

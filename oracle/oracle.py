@@ -82,6 +82,10 @@ def lib(o0: bool = False) -> ctypes.CDLL:
         L.oracle_voice_note.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.oracle_voice_event.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _F]
         L.oracle_voice_process.argtypes = [ctypes.c_void_p, _PF, ctypes.c_int, ctypes.c_int]
+        L.oracle_voice_set_arith.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.oracle_rcp_table_set.argtypes = [ctypes.c_void_p]
+        L.oracle_rcp_model.restype = _F
+        L.oracle_rcp_model.argtypes = [_F]
         L.oracle_fxrack_defaults.argtypes = [_PF]
         L.oracle_fxrack_create.restype = ctypes.c_void_p
         L.oracle_fxrack_create.argtypes = [ctypes.c_int, _F]
@@ -239,11 +243,14 @@ class Voice(_Bank):
     """SynthVoice bank.  moog=False: SvfFilter voice (SynthVoice default); moog=True: MoogFilter
     voice (daisysp::LadderFilter, the Daisy synth firmware's voice, main.cpp:49-52)."""
 
-    def __init__(self, n: int, sample_rate: float = 48000.0, moog: bool = False, o0: bool = False):
+    def __init__(self, n: int, sample_rate: float = 48000.0, moog: bool = False, o0: bool = False,
+                 kernel_arith: bool = False):
         self.n = n
         self.L = lib(o0)
         self.h = self.L.oracle_voice_create_model(n, sample_rate, int(bool(moog)))
         assert self.h
+        if kernel_arith:
+            assert self.L.oracle_voice_set_arith(self.h, 1) == 0
 
     def close(self):
         if getattr(self, "h", None):
@@ -272,6 +279,19 @@ class Voice(_Bank):
         out = np.empty((1, frames, self.n), dtype=np.float32)
         assert self.L.oracle_voice_process(self.h, _pf(out), frames, threads) == 0
         return out
+
+
+def set_rcp_table(tab) -> None:
+    """The v_rcp_f32 model of the voice's kernel arithmetic (voice_ref.c): `tab` = the instruction's
+    2^23 results (uint32 bits) over the mantissas of [1, 2), as read from the device; None = the
+    correctly rounded reciprocal."""
+    L = lib()
+    if tab is None:
+        assert L.oracle_rcp_table_set(None) == 0
+        return
+    t = np.ascontiguousarray(tab, dtype=np.uint32)
+    assert t.shape == (1 << 23,)
+    assert L.oracle_rcp_table_set(t.ctypes.data) == 0
 
 
 def chorus_c1(params, n_frames: int, block: int = 256, sample_rate: float = 48000.0, o0: bool = False):

@@ -54,6 +54,7 @@ typedef struct {
 struct oracle_voice {
     int n;
     float sr;
+    int arith;        /* 0: the restatement (unfused, glibc sinf); 1: the kernels' arithmetic (below) */
     voice_t *v;
     float *params;    /* [n][OVC_NPARAMS] SynthVoice members (Config order) */
 };
@@ -262,6 +263,155 @@ static float voice_tick(voice_t *v)
     return out_low * amp;
 }
 
+/* ---------------------------------------------------------------------------------------------
+ * The kernels' arithmetic (arith = 1).  The GPU voices (ol_dsp_amd/csrc/voice.hip) compute the same
+ * composition with three documented departures from the restatement above, restated here operation
+ * for operation so that the GPU output can be checked BIT-EXACTLY (tests/test_gpu_parity.py
+ * test_voice_bit_exact_kernel_arith); the restatement above stays the tolerance-based check:
+ *   1. contraction into fused multiply-adds (C99 fmaf, correctly rounded like v_fma_f32) at the
+ *      sites voice.hip lists under "Contraction": the polyBLEP quadratics and the saw's output, the
+ *      sine polynomial and the cutoff sum, the Svf's low/band updates, the ladder's stages, its
+ *      oversampling interpolation, feedback sum and SetAlpha polynomials;
+ *   2. Svf::SetFreq's sinf as the odd Taylor polynomial to x^9 (voice.hip sin_quarter), its
+ *      2/fq - fq/2 as 1/s - s (s = fq/2) and fc / (2 sr) as fc * (1 / (2 sr));
+ *   3. divisions by the hardware reciprocal v_rcp_f32 (the polyBLEP's t/dt, 1/s, the Pade tanh's
+ *      denominator).  v_rcp_f32 is not correctly rounded: measured on gfx950 over every mantissa of
+ *      [1, 2) (tools/rcp_probe.hip), it differs from RN(1/x) on 10.70 % of them, always by one ulp
+ *      (the exact quotient within 0.1..0.85 ulp of the floor: an approximation of < 0.4 ulp error,
+ *      rounded), and rcp(m 2^e) = rcp(m) 2^-e exactly for every normal result.  Its model here is
+ *      that table: oracle_rcp_table_set() takes the 2^23 results (the GPU tests read them from the
+ *      device, tests/gpu_probe/rcp_probe.hip), scaled by the exponent.  Without a table the model is
+ *      the correctly rounded 1/x.  Inputs whose result is not normal (0, denormals, inf: the voices
+ *      never divide by them where the quotient is used) fall back to 1/x.
+ * Everything else (envelopes, portamento, phase, notch, the Low() sum) is unfused in both. */
+static uint32_t *g_rcp_tab;
+
+int oracle_rcp_table_set(const uint32_t *tab)
+{
+    free(g_rcp_tab);
+    g_rcp_tab = NULL;
+    if (!tab) return 0;
+    g_rcp_tab = (uint32_t *)malloc(sizeof(uint32_t) << 23);
+    if (!g_rcp_tab) return -1;
+    memcpy(g_rcp_tab, tab, sizeof(uint32_t) << 23);
+    return 0;
+}
+
+float oracle_rcp_model(float x)
+{
+    uint32_t b;
+    memcpy(&b, &x, 4);
+    const int e = (int)((b >> 23) & 0xffu);
+    if (!g_rcp_tab || e == 0 || e == 255) return 1.0f / x;
+    const uint32_t r = g_rcp_tab[b & 0x7fffffu];
+    const int re = (int)((r >> 23) & 0xffu) - (e - 127);
+    if (re <= 0 || re >= 255) return 1.0f / x;
+    const uint32_t o = (b & 0x80000000u) | ((uint32_t)re << 23) | (r & 0x7fffffu);
+    float y;
+    memcpy(&y, &o, 4);
+    return y;
+}
+
+/* voice.hip polyblep + saw_out: q = (lo ? t : t - 1) rcp(dt); fma(-q, q, 2q) - 1 / fma(q, q, 2q) + 1 */
+static float k_saw(float t, float dt)
+{
+    const int lo = t < dt, hi = t > 1.0f - dt;
+    const float q = (lo ? t : t - 1.0f) * oracle_rcp_model(dt);
+    const float q2 = q + q;
+    const float rlo = fmaf(-q, q, q2) - 1.0f;
+    const float rhi = fmaf(q, q, q2) + 1.0f;
+    const float blep = lo ? rlo : (hi ? rhi : 0.0f);
+    return fmaf(0.5f, blep, 0.5f - t);
+}
+
+/* voice.hip sin_quarter */
+static float k_sin_quarter(float x)
+{
+    const float x2 = x * x;
+    float p = fmaf(2.7557319e-6f, x2, -1.9841270e-4f);
+    p = fmaf(p, x2, 8.3333333e-3f);
+    p = fmaf(p, x2, -1.6666667e-1f);
+    return fmaf(x * x2, p, x);
+}
+
+/* voice.hip voice_block_v4 (MOOG) filter wave: LadderFilter::Process contracted, the Pade tanh as
+   r(med3(x, -3, 3)) with v_rcp */
+static float k_ladder(voice_t *v, float alpha, float qadj, float input)
+{
+    const float kq = v->l_k * qadj;
+    const float fb0 = -0.5f * input, dold = v->l_old - input;
+    float total = 0.0f;
+    for (int os = 0; os < LADDER_OS; os++) {
+        const float interp = 0.25f * (float)os;
+        const float mixin = os == 0 ? input : fmaf(interp, dold, input);
+        float x = fmaf(-(v->lz1[3] + fb0), kq, mixin);
+        x = fminf(fmaxf(x, -3.0f), 3.0f);
+        const float x2 = x * x;
+        float u = (x * (27.0f + x2)) * oracle_rcp_model(fmaf(9.0f, x2, 27.0f));
+        for (int st = 0; st < 4; st++) {
+            float ft = fmaf(u, 1.0f / 1.3f, fmaf(0.3f / 1.3f, v->lz0[st], -v->lz1[st]));
+            ft = fmaf(ft, alpha, v->lz1[st]);
+            v->lz1[st] = ft;
+            v->lz0[st] = u;
+            u = ft;
+        }
+        total = fmaf(u, 0.25f, total);
+    }
+    v->l_old = input;
+    return total;
+}
+
+static float voice_tick_k(voice_t *v)
+{
+    const int moog = v->model == 1;
+    /* ENV: the segment machine is adsr_process's (voice.hip Env: identical updates and clamps);
+       the Svf voice hands FILT amp * (amp_env_amount / 2) (Low()'s halving folded in, exact) */
+    const float env_a = adsr_process(&v->amp_env, v->gate);
+    const float amp = env_a * (moog ? v->amp_env_amount : 0.5f * v->amp_env_amount);
+    /* OSC */
+    v->port_z = v->freq + v->port_coef * (v->port_z - v->freq);
+    const float inc = v->port_z * v->sr_recip;
+    const float t = v->phase;
+    v->phase += inc;
+    if (v->phase > 1.0f) v->phase -= 1.0f;
+    const float src = k_saw(t, inc);
+    const float fe = adsr_process(&v->filt_env, v->gate);
+    const float fc_in = fmaf(fe * 20000.0f, v->filter_env_amount, v->filter_cutoff);
+    if (moog) {
+        const float wc = fc_in * 2.0f * 3.1415927410125732f * v->l_sr_int_recip;
+        const float wc2 = wc * wc;
+        const float alpha = wc * fmaf(fmaf(fmaf(-0.0202f, wc, 0.1381f), wc, -0.4324f), wc, 0.9892f);
+        const float qadj = fmaf(fmaf(-0.05f, wc2, -0.095f), wc2, fmaf(0.0536f, wc, 1.006f));
+        return k_ladder(v, alpha, qadj, src * v->l_drive_scaled) * amp;
+    }
+    /* FREQ: Svf::SetFreq */
+    const float fc = fminf(fmaxf(fc_in, 1.0e-6f), v->fc_max);
+    const float inv_2sr = 1.0f / (v->sr * 2.0f);
+    const float s = k_sin_quarter(3.1415927410125732f * fminf(fc * inv_2sr, 0.25f));
+    const float fq = s + s;
+    const float lim = oracle_rcp_model(s) - s;
+    const float damp_res = 2.0f * (1.0f - powf(v->res, 0.25f));
+    const float ndamp = fmaxf(fmaxf(-damp_res, -2.0f), -lim);
+    /* FILT: Svf::Process, the notch unfused */
+    float notch = src + ndamp * v->band;
+    v->low = fmaf(fq, v->band, v->low);
+    float high = notch - v->low;
+    v->band = fmaf(-((v->drive * v->band) * v->band), v->band, fmaf(fq, high, v->band));
+    const float low1 = v->low;
+    notch = src + ndamp * v->band;
+    v->low = fmaf(fq, v->band, v->low);
+    high = notch - v->low;
+    v->band = fmaf(-((v->drive * v->band) * v->band), v->band, fmaf(fq, high, v->band));
+    return (low1 + v->low) * amp;
+}
+
+int oracle_voice_set_arith(oracle_voice *o, int kernel)
+{
+    if (!o || kernel < 0 || kernel > 1) return -1;
+    o->arith = kernel;
+    return 0;
+}
+
 oracle_voice *oracle_voice_create(int n_inst, float sample_rate)
 {
     return oracle_voice_create_model(n_inst, sample_rate, 0);
@@ -348,11 +498,13 @@ int oracle_voice_process(oracle_voice *o, float *out, int n_frames, int n_thread
 {
     if (!o || n_frames < 0) return -1;
     const long n = o->n;
+    const int k = o->arith;
     (void)n_threads;
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static) num_threads(n_threads > 0 ? n_threads : 1)
 #endif
     for (long i = 0; i < n; i++)
-        for (int f = 0; f < n_frames; f++) out[(long)f * n + i] = voice_tick(&o->v[i]);
+        for (int f = 0; f < n_frames; f++)
+            out[(long)f * n + i] = k ? voice_tick_k(&o->v[i]) : voice_tick(&o->v[i]);
     return 0;
 }

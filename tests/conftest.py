@@ -38,3 +38,30 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.fail("GPU test requested but no GPU is visible")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="session")
+def rcp_table(cuda):
+    """gfx950's v_rcp_f32 over every mantissa of [1, 2), read from the device by the test helper
+    tests/gpu_probe/librcp_probe.so, checked against the documented error model (within one ulp of
+    the correctly rounded 1/x, never further) and installed as the voice oracle's v_rcp model
+    (oracle/voice_ref.c "kernels' arithmetic").  Yields the table; the model is removed after."""
+    import ctypes
+
+    import numpy as np
+
+    import oracle as O
+    path = os.path.join(ROOT, "tests", "gpu_probe", "librcp_probe.so")
+    if not os.path.exists(path):
+        pytest.fail(f"{path} not built (make -C tests/gpu_probe)")
+    L = ctypes.CDLL(path)
+    L.probe_rcp_table.argtypes = [ctypes.c_void_p]
+    tab = np.empty(1 << 23, np.uint32)
+    assert L.probe_rcp_table(tab.ctypes.data) == 0
+    x = ((np.uint32(127) << np.uint32(23)) | np.arange(1 << 23, dtype=np.uint32)).view(np.float32)
+    cr = (np.float32(1.0) / x).view(np.uint32)            # numpy float32 division: correctly rounded
+    d = tab.astype(np.int64) - cr.astype(np.int64)
+    assert np.abs(d).max() <= 1, "v_rcp_f32 outside one ulp of 1/x"
+    O.set_rcp_table(tab)
+    yield tab
+    O.set_rcp_table(None)

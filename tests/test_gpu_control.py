@@ -374,13 +374,21 @@ def test_reset_waits_for_the_engines_own_stream(cuda):
 
 def test_set_member_after_update_is_refused(cuda):
     """olfx_set_member is the member write BEFORE Init/Update (the firmware's setup order); once a
-    voice has been Update()d, its components follow set_params, so a bare member write is refused
-    (OLFX_E_STATE) instead of acting like an Update() the reference would not run."""
+    voice has been Update()d, members that feed the components only through Update() (resonance,
+    drive, envelope times, portamento) are refused (OLFX_E_STATE) instead of acting like an Update()
+    the reference would not run; the members SynthVoice::Process reads itself every sample
+    (filter_cutoff, filter_env_amount, amp_env_amount, SynthVoice.h:42-52) are accepted at any time
+    and take effect at the next block (test_voice_bit_exact_kernel_arith checks the audio)."""
     from ol_dsp_amd import _lib
     e = engine("voice", 4)
     lib, h = e.lib, e.handle
-    assert lib.olfx_set_member(h, 1, 0, 500.0) == 0               # before Update: accepted
+    assert lib.olfx_set_member(h, 1, 1, 0.5) == 0                 # before Update: accepted
     e.update(1, 1)
-    assert lib.olfx_set_member(h, 1, 0, 900.0) == _lib.OLFX_E_STATE    # after: refused, unchanged
-    assert e.get_param(1, "filter_cutoff") == np.float32(500.0)
-    assert lib.olfx_set_member(h, 2, 0, 900.0) == 0               # other voices untouched
+    assert lib.olfx_set_member(h, 1, 1, 0.9) == _lib.OLFX_E_STATE    # after: refused, unchanged
+    assert e.get_param(1, "filter_resonance") == np.float32(0.5)
+    for f in ("filter_attack", "portamento", "amp_sustain"):
+        assert lib.olfx_set_member(h, 1, e.field(f), 0.3) == _lib.OLFX_E_STATE
+    assert lib.olfx_set_member(h, 2, 1, 0.9) == 0                 # other voices untouched
+    for f, v in (("filter_cutoff", 900.0), ("filter_env_amount", 0.25), ("amp_env_amount", 0.5)):
+        assert lib.olfx_set_member(h, 1, e.field(f), v) == 0      # Process reads these: accepted
+        assert e.get_param(1, f) == np.float32(v)

@@ -168,9 +168,10 @@ def test_chain_persistent_groups_ragged(cuda):
 
 
 @pytest.mark.parametrize("kind", ["voice", "voice_moog"])
-def test_full_size_voices(cuda, kind):
+def test_full_size_voices(cuda, rcp_table, kind):
     """configs[3]'s per-GPU shard: 32,768 voices, NoteOn at block 0 and NoteOff at block 2 of 4 (SURVEY
-    8d): clones bit-identical; sampled voices within the voice tolerance of the oracle."""
+    8d): clones bit-identical; sampled voices within the voice tolerance of the oracle, and
+    bit-exact against its kernel-arithmetic mode (oracle/voice_ref.c)."""
     import torch
 
     from ol_dsp_amd.workload import voice_notes
@@ -190,16 +191,23 @@ def test_full_size_voices(cuda, kind):
         out[:, 256 * b:256 * (b + 1)] = ob
     torch.cuda.synchronize()
     _check_clones(out, n)
-    idx = _sample_idx(n)
-    ref = O.Voice(len(idx), moog=kind == "voice_moog")
-    for k, i in enumerate(idx):
-        ref.config(k, p[:, i])
-        ref.note(k, True, int(notes[i]))
-    yr = ref.process(512)
-    for k, i in enumerate(idx):
-        ref.note(k, False, int(notes[i]))
-    yr = np.concatenate([yr, ref.process(512)], 1)
+    idx = np.union1d(_sample_idx(n), np.array([64 * 97, 64 * 97 + 62, 64 * 311 + 30, 20000], np.int64))
     yg = out[:, :, idx].cpu().numpy()
+
+    def oracle_run(kernel_arith):
+        ref = O.Voice(len(idx), moog=kind == "voice_moog", kernel_arith=kernel_arith)
+        for k, i in enumerate(idx):
+            ref.config(k, p[:, i])
+            ref.note(k, True, int(notes[i]))
+        yr = ref.process(512)
+        for k, i in enumerate(idx):
+            ref.note(k, False, int(notes[i]))
+        return np.concatenate([yr, ref.process(512)], 1)
+
+    yk = oracle_run(True)
+    fin = np.isfinite(yk)
+    assert np.array_equal(fin, np.isfinite(yg)) and np.array_equal(yg[fin].view(np.uint32), yk[fin].view(np.uint32))
+    yr = oracle_run(False)
     fin = np.isfinite(yr)
     assert np.array_equal(fin, np.isfinite(yg)), "non-finite pattern differs from the oracle"
     keep = fin.all(axis=(0, 1))

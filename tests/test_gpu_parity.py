@@ -634,6 +634,71 @@ def test_voice_vs_oracle(cuda, kind):
     # 2.3e-6, max 4.5e-4, 59.0 % bit-identical; Moog p99 2.1e-6, max 5.1e-4, 44.4 % bit-identical;
     # max |d| / peak 4.2e-7 / 5.8e-7
     assert np.quantile(pw, 0.99) <= 1e-5
+    # explicit pointwise bound: p99 and max of |d| / |ref| where |ref| is above
+    # 1e-3 of the voice's rms, at the values DESIGN.md section 2 states (with margin: 2.3e-6 / 4.5e-4
+    # for the Svf voice, 2.1e-6 / 5.1e-4 for the Moog voice)
+    assert np.quantile(pw, 0.99) <= 5e-6 and pw.max() <= 1e-3
+
+
+def voice_bits_equal(y, yr):
+    """Bit-exact where the oracle is finite, the same non-finite pattern elsewhere (a diverging Svf
+    produces inf/NaN in the reference arithmetic too; NaN payloads are not compared)."""
+    fin = np.isfinite(yr)
+    if not np.array_equal(fin, np.isfinite(y)):
+        return False
+    return np.array_equal(y[fin].view(np.uint32), yr[fin].view(np.uint32))
+
+
+@pytest.mark.parametrize("kind", ["voice", "voice_moog"])
+def test_voice_bit_exact_kernel_arith(cuda, rcp_table, kind):
+    """the GPU voices BIT-EXACT against the oracle's kernel-arithmetic mode
+    (oracle/voice_ref.c: the same contractions, sine polynomial and v_rcp model), so that an
+    indexing or event-timing bug of any size shows.  Half the voices configured, half at Init's
+    defaults; NoteOn / NoteOff / GateOn / GateOff / SetFrequency storms at block boundaries; ragged
+    blocks (4..300 frames: partial chunks); a config change and Process-read member writes
+    (olfx_set_member of filter_cutoff, filter_env_amount, amp_env_amount after Update()) mid-run."""
+    from ol_dsp_amd import _lib
+    n = 200
+    rng = np.random.default_rng(2024)
+    e = engine(kind, n)
+    ref = O.Voice(n, moog=kind == "voice_moog", kernel_arith=True)
+    cfg = voice_configs(rng, n)
+    conf = np.arange(n) % 2 == 0
+    for i in np.flatnonzero(conf):
+        e.set_params(0, cfg[:, i:i + 1], first=int(i))
+        ref.config(int(i), cfg[:, i])
+    ys, yrs, total, b = [], [], 0, 0
+    while total < 6000:
+        if b == 9:                                   # a new config for a third of the voices
+            who = np.flatnonzero(rng.random(n) < 1 / 3)
+            new = voice_configs(rng, n)
+            for i in who:
+                e.set_params(0, new[:, i:i + 1], first=int(i))
+                ref.config(int(i), new[:, i])
+                cfg[:, i] = new[:, i]
+                conf[i] = True
+        if b == 14:                                  # members Process reads, written after Update()
+            for i in np.flatnonzero(conf)[:40]:
+                for f, lo, hi in ((0, 100.0, 8000.0), (3, 0.0, 1.0), (9, 0.2, 1.0)):
+                    v = np.float32(rng.uniform(lo, hi))
+                    assert e.lib.olfx_set_member(e.handle, int(i), f, float(v)) == 0
+                    cfg[f, i] = v
+                ref.config(int(i), cfg[:, i])        # the same members, the rest unchanged
+        evs = []
+        for i in np.flatnonzero(rng.random(n) < (1.0 if b == 0 else 0.3)):
+            t = 1 if b == 0 else int(rng.integers(0, 5))
+            evs.append((int(i), t, int(rng.integers(30, 100)), float(rng.uniform(30.0, 3000.0))))
+        e.voice_events(evs)
+        for i, t, note, hz in evs:
+            ref.event(i, t, note, hz if t == _lib.EV_SET_FREQUENCY else 0.0)
+        fr = int(rng.choice([256, 256, 4, 12, 100, 300, 37 * 4]))
+        ys.append(_voice_run(e, fr, cuda))
+        yrs.append(ref.process(fr))
+        total += fr
+        b += 1
+    y, yr = np.concatenate(ys, 1), np.concatenate(yrs, 1)
+    assert np.isfinite(yr).mean() > 0.9
+    assert voice_bits_equal(y, yr), first_mismatch(y, yr)
 
 
 @pytest.mark.parametrize("kind", ["voice", "voice_moog"])

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from helpers import bits_equal, first_mismatch, fxrack_params, noise_block
+from helpers import bits_equal, first_mismatch, fxrack_params, noise_block, rel_err
 
 
 # ---------------------------------------------------------------- dattorro, vs golden fixtures
@@ -315,6 +315,54 @@ def test_voice_reference_pins_synth_test():
 def test_voice_silent_until_note():
     vo = O.Voice(2)
     assert np.all(vo.process(512) == 0)
+
+
+@pytest.mark.parametrize("moog", [False, True])
+def test_voice_kernel_arith_mode_tracks_the_restatement(golden, moog):
+    """The oracle's kernel-arithmetic mode (voice_ref.c: the GPU kernels' contractions, sine
+    polynomial and reciprocal; here with the correctly rounded reciprocal, no device table) stays
+    within the voice tolerance of the unfused restatement on the golden voices, keeps the
+    synth_test.cpp:102-148 first-sample pins, and is not the restatement itself."""
+    g = golden["voice_moog" if moog else "voice"]
+    p = np.asarray(g["params"], np.float32)
+    outs = []
+    for karith in (False, True):
+        vo = O.Voice(g["n"], moog=moog, kernel_arith=karith)
+        for i in range(g["n"]):
+            vo.config(i, p[:, i])
+            vo.note(i, True, g["notes"][i])
+        ya = vo.process(g["note_off_at"])
+        for i in range(g["n"]):
+            vo.note(i, False, g["notes"][i])
+        outs.append(np.concatenate([ya, vo.process(g["frames"] - g["note_off_at"])], axis=1))
+    assert rel_err(outs[1][0].T, outs[0][0].T) <= 1e-5
+    assert not bits_equal(outs[0], outs[1])
+    vo = O.Voice(1, moog=moog, kernel_arith=True)
+    vo.note(0, True, 60)
+    vo.note(0, False, 60)
+    assert vo.process(1)[0, 0, 0] == 0
+
+
+def test_rcp_model_scales_the_mantissa_table():
+    """The v_rcp model (voice_ref.c oracle_rcp_model): no table = correctly rounded 1/x; with a table
+    of the 2^23 mantissa results, rcp(m 2^e) = table[m] 2^-e with the sign kept, and 1/x for inputs
+    whose result is not normal."""
+    xs = np.array([1.0, 1.5, 3.0, 0.007, -27.5, 108.0, 1e-30, 3e37], np.float32)
+    O.set_rcp_table(None)
+    L = O.lib()
+    assert [L.oracle_rcp_model(float(x)) for x in xs] == [float(np.float32(1) / x) for x in xs]
+    x = ((np.uint32(127) << np.uint32(23)) | np.arange(1 << 23, dtype=np.uint32)).view(np.float32)
+    tab = (np.float32(1.0) / x).view(np.uint32).copy()
+    tab[1:] += 1                                       # every result but 1/1 one ulp up
+    try:
+        O.set_rcp_table(tab)
+        got = np.array([L.oracle_rcp_model(float(v)) for v in xs], np.float32)
+        want = (np.float32(1) / xs)
+        w = want.view(np.uint32).copy()
+        w[(xs.view(np.uint32) & 0x7FFFFF) != 0] += 1      # all but the exact powers of two
+        assert np.array_equal(got.view(np.uint32), w), (got, w.view(np.float32))
+    finally:
+        O.set_rcp_table(None)
 
 
 # ------------------------------------------- MoogFilter voice (daisysp::LadderFilter, unpinned)
