@@ -317,9 +317,25 @@ def parity_check(job: dict, sr: float) -> dict:
 # ------------------------------------------------------------------------------------------------
 # GPU workloads
 # ------------------------------------------------------------------------------------------------
+_LIB_SHA = []
+
+
+def _lib_sha256() -> str:
+    """sha256 of the libolfx.so this process runs (the traffic files' build stamp)."""
+    if not _LIB_SHA:
+        import hashlib
+
+        from ol_dsp_amd import _lib
+        with open(_lib.LIB_PATH, "rb") as f:
+            _LIB_SHA.append(hashlib.sha256(f.read()).hexdigest())
+    return _LIB_SHA[0]
+
+
 def _traffic(name: str, n: int, B: int, override: str = "", kernel: str = ""):
     """The PMC traffic summary of this workload's kernel (tools/pmc_traffic.py), if one was recorded
-    for the same instance count, block and kernel (a summary of another kernel is never used)."""
+    for the same instance count, block and kernel AND with the same build: the file's
+    `libolfx_sha256` must be the hash of the library this process runs (counters
+    of an older build are never attached to the current kernel)."""
     for tj in ([override] if override else []) + [os.path.join(ROOT, "profiles", f"traffic_{name}_{n}.json"),
                                                   os.path.join(ROOT, "profiles", f"traffic_{name}.json")]:
         if tj and os.path.exists(tj):
@@ -329,7 +345,8 @@ def _traffic(name: str, n: int, B: int, override: str = "", kernel: str = ""):
                 kernels = tr.get("counters_per_kernel") or {}
                 # a launch sequence ("a+b") needs a summary of every kernel in it
                 same_kernel = not kernel or all(any(part in k for k in kernels) for part in kernel.split("+"))
-                if tr.get("instances") == n and tr.get("block") == B and same_kernel:
+                if (tr.get("instances") == n and tr.get("block") == B and same_kernel
+                        and tr.get("libolfx_sha256") == _lib_sha256()):
                     return tr
             except Exception:
                 pass
@@ -455,7 +472,7 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
     for k in range(W):
         step(k)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -464,7 +481,7 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
         step(W + k, k)
     region[1].record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
@@ -550,7 +567,7 @@ def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, wi
     traffic = tr.get("hbm_bytes_per_launch") if tr else None
     # the PMC-measured HBM bytes of the same kernel (profiles/traffic_<workload>.json, separate
     # --pmc passes) over this run's kernel time: what HBM actually moved, against the peak
-    measured = {}
+    measured = {"traffic_build": (tr or {}).get("libolfx_sha256", "none recorded for this libolfx.so")[:16]}
     if tr and traffic:
         measured["hbm_gbs_measured"] = traffic / (kern_ms * 1e-3) / 1e9
         rd = tr.get("read_bytes_by_request_size")
@@ -675,12 +692,15 @@ def main():
     import torch.distributed as dist
 
     rank, world, local = env_ranks()
+    # under a launcher (WORLD_SIZE set, 1 included) the ranks form a process group: RCCL over xGMI
+    # ("nccl") on the GPUs, gloo for the CPU stub
+    grouped = world > 1 or "WORLD_SIZE" in os.environ
     if args.stub:
-        if world > 1:
+        if grouped:
             dist.init_process_group("gloo", rank=rank, world_size=world)
         dev = torch.device("cpu")
     else:
-        if world > 1:
+        if grouped:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         dev = torch.device("cuda", local)
@@ -785,7 +805,7 @@ def main():
             except OSError:
                 pass
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

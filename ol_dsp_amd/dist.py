@@ -47,10 +47,12 @@ def shard(n_total: int, world: int, rank: int) -> Tuple[int, int]:
 
 
 def reduce_stats(stats: RunStats, device=None) -> RunStats:
-    """One all-reduce of the run counters (no-op when torch.distributed is not initialised)."""
+    """One all-reduce of the run counters (no-op when torch.distributed is not initialised).  A
+    process group of world size 1 (a launcher's single rank) runs the collective too, so the RCCL
+    path is exercised on a one-GPU box exactly as at N > 1 (tests/test_gpu_rccl.py)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return stats
     t_max = torch.tensor([stats.elapsed_s, stats.kernel_ms], dtype=torch.float64, device=device)
     t_sum = torch.tensor([stats.frames, stats.checksum, stats.ranks], dtype=torch.float64, device=device)

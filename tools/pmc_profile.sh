@@ -7,6 +7,9 @@ wl=${1:-chorus}; steps=${2:-20}; shift 2 || true
 out=gpurun_out/pmc_$wl
 mkdir -p "$out"
 export TMPDIR=/tmp
+# the build these counters belong to: tools/pmc_traffic.py stamps its JSON with this hash and
+# bench.py attaches a traffic file only to the libolfx.so it was recorded with
+sha256sum ol_dsp_amd/libolfx.so | cut -d' ' -f1 > "$out/libolfx.sha256"
 passes=(
   "FETCH_SIZE"
   "WRITE_SIZE"

@@ -55,6 +55,13 @@ def main():
         print(f"{k:28s} {agg[k]:.6g}")
     res = {"workload": wl, "instances": n, "block": block, "counters_per_launch": agg,
            "counters_per_kernel": res_k}
+    # the build the counters were taken with (tools/pmc_profile.sh): bench.py refuses a traffic file
+    # whose libolfx.so hash differs from the library it runs
+    stamp = os.path.join(base, "libolfx.sha256")
+    if not os.path.exists(stamp):
+        sys.exit(f"{stamp} missing: re-run tools/pmc_profile.sh (it records the library's hash)")
+    with open(stamp) as f:
+        res["libolfx_sha256"] = f.read().split()[0]
     if "FETCH_SIZE" in agg and "WRITE_SIZE" in agg:
         fetch = agg["FETCH_SIZE"] * 1024 * fscale
         write = agg["WRITE_SIZE"] * 1024
