@@ -22,11 +22,15 @@
  * the generation runs one olfx_process over the whole block for all of them.  Consequences,
  * stated as the interface contract:
  *   - Latency: getLeft/getRight after the k-th process call return the reference's output for
- *     sample k - block (0 for k < block).  Bit-exact otherwise (the engine is, verb.cpp order).
- *   - Lockstep: within a block, every live instance of a generation is processed once per sample
- *     before any instance starts the next block -- the per-frame callback shape of every
- *     reference caller (ReverbFx_process per frame; workout_buddy / Daisy callbacks).  An
- *     instance that runs a whole block ahead of the others is an error.
+ *     sample k - D * block (0 before; D = the pool depth, 1 by default).  Bit-exact otherwise (the
+ *     engine is, verb.cpp order).
+ *   - Call order: any interleaving in which no instance runs more than the pool depth D (default
+ *     1) blocks ahead of the slowest live one: the per-frame callback shape of every reference
+ *     caller (ReverbFx_process per frame; workout_buddy / Daisy callbacks), and hosts that run
+ *     each reverb over its whole buffer in turn with D = buffer / block, or ceil(buffer / block) + 1
+ *     for a buffer that is not a multiple of the block (olfx_dattorro_pool_config_depth; the latency
+ *     is then D blocks).  An instance that runs D
+ *     blocks ahead of the others is an error.
  *   - Setters take effect at the next block boundary (olfx_set_params), not the next sample.
  * Errors: the reference functions return void (create returns NULL on allocation failure,
  * verb.cpp:227).  Any other failure -- no GPU, a HIP error, a lockstep violation -- prints the
@@ -63,7 +67,11 @@ t_sample DattorroVerb_getRight(struct sDattorroVerb *v);
    generations created after this call -- the setting of olfx_sample_pool_config, shared with the
    other per-sample operators.  Defaults: device 0, block 256.  Returns OLFX_OK (0) or OLFX_E_ARG. */
 int olfx_dattorro_pool_config(int device, uint32_t block);
-/* The latency in samples of instance v (its generation's block). */
+/* The same with the pool depth D (1..8; olfx_sample_pool_config_depth): instances may run up to D
+   blocks ahead of each other (e.g. each reverb over a whole host buffer of D blocks in turn); the
+   latency is D * block. */
+int olfx_dattorro_pool_config_depth(int device, uint32_t block, uint32_t depth);
+/* The latency in samples of instance v (its generation's depth x block). */
 uint32_t olfx_dattorro_latency(const struct sDattorroVerb *v);
 /* Generation facts: instances in v's generation and v's index in it (the engine instance). */
 uint32_t olfx_dattorro_generation_size(const struct sDattorroVerb *v);

@@ -129,6 +129,7 @@ SIGNATURES = {
     "olfx_num_buses": (_U32, [_P]),
     # include/olfx_sample.h: per-instance, per-sample operators (one block of latency)
     "olfx_sample_pool_config": (ctypes.c_int, [ctypes.c_int, _U32]),
+    "olfx_sample_pool_config_depth": (ctypes.c_int, [ctypes.c_int, _U32, _U32]),
     "olfx_sample_create": (ctypes.c_int, [ctypes.c_int, _F, ctypes.POINTER(_P)]),
     "olfx_sample_destroy": (ctypes.c_int, [_P]),
     "olfx_sample_set_param": (ctypes.c_int, [_P, _U32, _F]),
@@ -143,6 +144,7 @@ SIGNATURES = {
     "olfx_sample_index": (_U32, [_P]),
     # include/olfx_dattorro.h: pool control of the verb.h-compatible names
     "olfx_dattorro_pool_config": (ctypes.c_int, [ctypes.c_int, _U32]),
+    "olfx_dattorro_pool_config_depth": (ctypes.c_int, [ctypes.c_int, _U32, _U32]),
     "olfx_dattorro_latency": (_U32, [_P]),
     "olfx_dattorro_generation_size": (_U32, [_P]),
     "olfx_dattorro_index": (_U32, [_P]),

@@ -79,6 +79,9 @@ t_sample DattorroVerb_getLeft(struct sDattorroVerb *v) { return olfx_dv::get(v, 
 t_sample DattorroVerb_getRight(struct sDattorroVerb *v) { return olfx_dv::get(v, 1); }
 
 int olfx_dattorro_pool_config(int device, uint32_t block) { return olfx_sample_pool_config(device, block); }
+int olfx_dattorro_pool_config_depth(int device, uint32_t block, uint32_t depth) {
+    return olfx_sample_pool_config_depth(device, block, depth);
+}
 uint32_t olfx_dattorro_latency(const struct sDattorroVerb *v) { return v ? olfx_sample_latency(v->s) : 0; }
 uint32_t olfx_dattorro_generation_size(const struct sDattorroVerb *v) { return v ? olfx_sample_generation_size(v->s) : 0; }
 uint32_t olfx_dattorro_index(const struct sDattorroVerb *v) { return v ? olfx_sample_index(v->s) : 0; }

@@ -3,18 +3,25 @@
 // include/olfx_ref.hpp: the reference's names on top).
 //
 // A generation = the instances of one (kind, sample rate) created before the pool first ran them
-// = one engine of that many instances.  Per-frame calls fill a host block [in_ch][block][n]; the
-// last instance to complete a block runs the whole generation once.  Outputs are double-buffered
-// by block parity: while an instance feeds block b it reads block b-1's outputs, so the run that
-// writes block b's never races a reader.  Parameter / note / control calls made before the
-// engine exists or while a block is being filled are queued and applied, in order, when it is
-// created or right after that block's run: a call never reaches frames given before it.
+// = one engine of that many instances.  Per-frame calls fill a host ring of `depth` input blocks
+// [depth][in_ch][block][n]: an instance may run up to `depth` blocks ahead of the engine, in any
+// order relative to the other instances (frame-major callbacks, or instance-major hosts that run
+// each object over its whole buffer in turn, modules/juce/host/host.cpp:682).  Block b runs once
+// every live instance has given all its frames, blocks in order; the instance whose frame
+// completes the last missing block runs it (and any later blocks that are complete too).  An
+// instance's frame p returns the engine's output frame p - depth * block, from a ring of depth + 1
+// output blocks: an instance giving input block b reads output block b - depth, whose slot only the
+// run of block b + 1 rewrites, and that run waits for this instance's input block b + 1.  Calls
+// take effect at the instance's next block boundary at or after its position (never on frames it
+// gave before the call): applied at once when that boundary is the engine's next block, else
+// queued with that block as target and applied, in call order, right before it runs.
 //
-// Locking.  The per-frame call (olfx_sample_process) takes no lock: it touches only its own
-// instance's column of the block and the generation's atomic counters; the instance that
-// completes a block takes the generation's mutex to run it.  Parameter / note / control calls
-// take the generation's mutex.  Only create / destroy / the first run (freeze) take the pool's
-// mutex (the list of open generations).  Different generations never share a lock.
+// Locking.  The per-frame call (olfx_sample_process) takes no lock except once per block (its
+// frame that completes a block takes the generation's mutex to count it and run what is
+// complete): it touches only its own instance's column of the rings and atomics.  Parameter /
+// note / control calls take the generation's mutex.  Only create / destroy / the first run
+// (freeze) take the pool's mutex (the list of open generations).  Different generations never
+// share a lock.
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -36,36 +43,43 @@ struct Generation;
 struct olfx_sample {
     Generation *g;
     uint32_t idx;                   // engine instance
-    std::atomic<uint32_t> pos;      // frames of the current block given so far
+    std::atomic<uint64_t> given;    // frames given so far (its position in the generation's stream)
 };
 
 namespace {
 
-struct PendingOp {      // a call waiting for the next block boundary
+struct PendingOp {      // a call waiting for a block boundary
     enum { PARAM, MEMBER, EVENT, CONTROL, UPDATE } type;
     uint32_t inst, field;
     float value;
     uint8_t a, b, c;
+    uint64_t target;    // applied right before block `target` runs
 };
+
+constexpr uint32_t kMaxDepth = 8;
 
 struct Generation {
     int kind, device;
     float sr;
-    uint32_t block, ich, och;
-    std::mutex mu;                        // pending, engine calls, run_block, members' slots
+    uint32_t block, depth, ich, och;
+    std::mutex mu;                        // pending, engine calls, run_complete, members' slots, complete[]
     std::atomic<olfx_engine *> e{nullptr};  // created when the generation first runs
     std::vector<olfx_sample *> members;   // fixed once frozen (destroyed slots become null)
     std::vector<PendingOp> pending;
-    std::vector<float> in;                // [ich][block][n]
-    std::vector<float> out[2];            // [och][block][n], by block parity
-    std::atomic<uint32_t> live{0}, complete{0};
-    std::atomic<bool> filling{false};     // some instance has given a frame of the block being filled
+    std::vector<float> in;                // [depth][ich][block][n]: input block b in slot b % depth
+    std::vector<float> out;               // [depth + 1][och][block][n]: output block b in slot b % (depth + 1)
+    std::atomic<uint32_t> live{0};
+    uint32_t complete[kMaxDepth] = {};    // live instances that gave all of block b (slot b % depth)
     std::atomic<uint64_t> blocks{0};      // blocks run so far
+
+    size_t n() const { return members.size(); }
+    float *in_block(uint64_t b) { return in.data() + (size_t)(b % depth) * (ich ? ich : 1) * block * n(); }
+    float *out_block(uint64_t b) { return out.data() + (size_t)(b % (depth + 1)) * och * block * n(); }
 };
 
 std::mutex g_mu;                          // g_open, the pool config, generation membership
 int g_device = 0;
-uint32_t g_block = 256;
+uint32_t g_block = 256, g_depth = 1;
 std::vector<Generation *> g_open;         // generations accepting members, one per (kind, sr)
 
 int fail(int code, const char *what) {
@@ -99,15 +113,23 @@ int apply(Generation *g, const PendingOp &op) {
     return OLFX_E_ARG;
 }
 
-// calls made while a block was being filled take effect at the next block boundary: after the
-// run of that block (rounding the boundary up, so no call reaches frames given before it).
-// Caller holds g->mu.
-int apply_pending(Generation *g) {
-    for (const PendingOp &op : g->pending) {
+// the queued calls whose boundary is block `upto` or earlier, in call order (an instance's
+// targets never decrease, and calls of different instances commute).  Caller holds g->mu.
+int apply_pending(Generation *g, uint64_t upto) {
+    size_t keep = 0;
+    for (size_t k = 0; k < g->pending.size(); ++k) {
+        const PendingOp &op = g->pending[k];
+        if (op.target > upto) {
+            g->pending[keep++] = op;
+            continue;
+        }
         const int rc = apply(g, op);
-        if (rc) return engine_fail(g, rc, "applying a queued call");
+        if (rc) {
+            g->pending.erase(g->pending.begin() + (ptrdiff_t)keep, g->pending.begin() + (ptrdiff_t)k + 1);
+            return engine_fail(g, rc, "applying a queued call");
+        }
     }
-    g->pending.clear();
+    g->pending.resize(keep);
     return OLFX_OK;
 }
 
@@ -125,37 +147,43 @@ int freeze(Generation *g) {
         return fail(rc, buf);
     }
     try {
-        g->in.assign((size_t)(g->ich ? g->ich : 1) * g->block * n, 0.f);
-        g->out[0].assign((size_t)g->och * g->block * n, 0.f);
-        g->out[1].assign((size_t)g->och * g->block * n, 0.f);
+        g->in.assign((size_t)g->depth * (g->ich ? g->ich : 1) * g->block * n, 0.f);
+        g->out.assign((size_t)(g->depth + 1) * g->och * g->block * n, 0.f);
     } catch (const std::bad_alloc &) {
         olfx_destroy(e);
-        return fail(OLFX_E_NOMEM, "olfx_sample: out of host memory for the generation's block");
+        return fail(OLFX_E_NOMEM, "olfx_sample: out of host memory for the generation's blocks");
     }
     g->e.store(e, std::memory_order_release);
-    return apply_pending(g);
+    return apply_pending(g, ~0ull);
 }
 
-// Caller holds g->mu; every live instance has given the whole block.
-int run_block(Generation *g) {
-    const uint64_t b = g->blocks.load(std::memory_order_relaxed);
-    std::vector<float> &o = g->out[b & 1];
-    const int rc = olfx_process(g->e.load(), g->ich ? g->in.data() : nullptr, o.data(), g->block, OLFX_IO_HOST, nullptr);
-    if (rc) return engine_fail(g, rc, "olfx_process");
-    g->complete.store(0, std::memory_order_relaxed);
-    g->filling.store(false, std::memory_order_relaxed);
-    // publish the new block count first, then each member's pos = 0 with release: a member that
-    // reads its pos 0 (acquire) also sees the new count and this run's outputs
-    g->blocks.store(b + 1, std::memory_order_release);
-    for (olfx_sample *m : g->members)
-        if (m) m->pos.store(0, std::memory_order_release);
-    return apply_pending(g);
+// Run every block that is complete, in order: block R = blocks needs each live instance's whole
+// input block R (complete[R % depth] == live).  Caller holds g->mu.
+int run_complete(Generation *g) {
+    for (;;) {
+        const uint64_t b = g->blocks.load(std::memory_order_relaxed);
+        const uint32_t live = g->live.load();
+        if (live == 0 || g->complete[b % g->depth] != live) return OLFX_OK;
+        int rc = apply_pending(g, b);
+        if (rc) return rc;
+        rc = olfx_process(g->e.load(), g->ich ? g->in_block(b) : nullptr, g->out_block(b), g->block, OLFX_IO_HOST,
+                          nullptr);
+        if (rc) return engine_fail(g, rc, "olfx_process");
+        g->complete[b % g->depth] = 0;          // the slot now counts block b + depth
+        // release: an instance that reads the new count (acquire) sees this run's outputs, and may
+        // refill input slot b % depth
+        g->blocks.store(b + 1, std::memory_order_release);
+    }
 }
 
-int queue_or_apply(olfx_sample *s, const PendingOp &op) {
+// a call lands at the instance's next block boundary at or after its position
+int queue_or_apply(olfx_sample *s, PendingOp op) {
     Generation *g = s->g;
     std::lock_guard<std::mutex> lk(g->mu);
-    if (!g->e.load() || g->filling.load()) {   // before the engine exists, or mid-block: at the next boundary
+    const uint64_t at = s->given.load(std::memory_order_relaxed);
+    op.target = (at + g->block - 1) / g->block;
+    // before the engine exists, or a boundary past the engine's next block: queued
+    if (!g->e.load() || op.target > g->blocks.load(std::memory_order_relaxed)) {
         g->pending.push_back(op);
         return OLFX_OK;
     }
@@ -167,13 +195,17 @@ int queue_or_apply(olfx_sample *s, const PendingOp &op) {
 
 extern "C" {
 
-int olfx_sample_pool_config(int device, uint32_t block) {
-    if (device < 0 || block == 0 || (block & 3u)) return fail(OLFX_E_ARG, "olfx_sample_pool_config: bad argument");
+int olfx_sample_pool_config_depth(int device, uint32_t block, uint32_t depth) {
+    if (device < 0 || block == 0 || (block & 3u) || depth == 0 || depth > kMaxDepth)
+        return fail(OLFX_E_ARG, "olfx_sample_pool_config: bad argument");
     std::lock_guard<std::mutex> lk(g_mu);
     g_device = device;
     g_block = block;
+    g_depth = depth;
     return OLFX_OK;
 }
+
+int olfx_sample_pool_config(int device, uint32_t block) { return olfx_sample_pool_config_depth(device, block, 1); }
 
 int olfx_sample_create(int kind, float sample_rate, olfx_sample **out) {
     if (!out) return fail(OLFX_E_ARG, "olfx_sample_create: null out");
@@ -188,17 +220,19 @@ int olfx_sample_create(int kind, float sample_rate, olfx_sample **out) {
     try {
         Generation *g = nullptr;
         for (Generation *c : g_open)
-            if (c->kind == kind && c->sr == sample_rate && c->device == g_device && c->block == g_block) g = c;
+            if (c->kind == kind && c->sr == sample_rate && c->device == g_device && c->block == g_block &&
+                c->depth == g_depth)
+                g = c;
         if (!g) {
             g = new Generation;
-            g->kind = kind; g->device = g_device; g->sr = sample_rate; g->block = g_block;
+            g->kind = kind; g->device = g_device; g->sr = sample_rate; g->block = g_block; g->depth = g_depth;
             g->ich = info.in_channels; g->och = info.out_channels;
             g_open.push_back(g);
         }
         std::lock_guard<std::mutex> gl(g->mu);
         s->g = g;
         s->idx = (uint32_t)g->members.size();
-        s->pos.store(0);
+        s->given.store(0);
         g->members.push_back(s);
         g->live.fetch_add(1);
     } catch (const std::bad_alloc &) {
@@ -218,15 +252,19 @@ int olfx_sample_destroy(olfx_sample *s) {
     {
         std::lock_guard<std::mutex> gl(g->mu);
         g->members[s->idx] = nullptr;
-        if (s->pos.load() == g->block) g->complete.fetch_sub(1);
+        // un-count the blocks it completed that have not run
+        const uint64_t R = g->blocks.load(), given = s->given.load();
+        for (uint64_t b = R; b < R + g->depth && (b + 1) * g->block <= given; ++b) --g->complete[b % g->depth];
         const uint32_t live = g->live.fetch_sub(1) - 1;
         if (g->e.load() && g->ich) {   // the slot keeps running on silence, unobserved
             const size_t n = g->members.size();
-            for (uint32_t c = 0; c < g->ich; ++c)
-                for (uint32_t f = 0; f < g->block; ++f) g->in[((size_t)c * g->block + f) * n + s->idx] = 0.f;
+            for (uint32_t q = 0; q < g->depth; ++q)
+                for (uint32_t c = 0; c < g->ich; ++c)
+                    for (uint32_t f = 0; f < g->block; ++f)
+                        g->in[(((size_t)q * g->ich + c) * g->block + f) * n + s->idx] = 0.f;
         }
         if (live == 0) last = true;
-        else if (g->e.load() && g->complete.load() == live) rc = run_block(g);   // the rest only waited for this one
+        else if (g->e.load()) rc = run_complete(g);   // the rest may have waited only for this one
     }
     delete s;
     if (last) {
@@ -285,40 +323,41 @@ int olfx_sample_process(olfx_sample *s, const float *in, float *out) {
             if (rc) return rc;
         }
     }
-    // pos first (acquire, pairs with run_block's release of pos = 0), then the block count: a reset
-    // pos is never seen with the previous count (the output buffer of the wrong parity)
-    const uint32_t pos = s->pos.load(std::memory_order_acquire);
-    const uint64_t blocks = g->blocks.load(std::memory_order_acquire);
-    if (pos == g->block) {
-        char buf[256];
+    const uint64_t p = s->given.load(std::memory_order_relaxed);     // written by this instance only
+    const uint64_t R = g->blocks.load(std::memory_order_acquire);    // pairs with run_complete's release
+    const uint64_t B = g->block, b = p / B;
+    if (b >= R + g->depth) {
+        char buf[320];
         std::snprintf(buf, sizeof buf,
                       "olfx_sample_process: instance %u started block %llu before the other %u live instances of "
-                      "its generation finished block %llu (calls must be frame-major, olfx_sample.h)",
-                      s->idx, (unsigned long long)(blocks + 1), g->live.load() - 1, (unsigned long long)blocks);
+                      "its generation finished block %llu (an instance may run at most %u block(s) ahead: "
+                      "olfx_sample_pool_config_depth, olfx_sample.h)",
+                      s->idx, (unsigned long long)b, g->live.load() - 1, (unsigned long long)R, g->depth);
         return fail(OLFX_E_STATE, buf);
     }
     const size_t n = g->members.size();
-    const size_t at = (size_t)pos * n + s->idx;
-    const size_t plane = (size_t)g->block * n;
-    for (uint32_t c = 0; c < g->ich; ++c) g->in[c * plane + at] = in[c];
-    // this frame's output: frame pos of the previous block (zeros before the first block ran)
-    if (blocks == 0) {
+    const size_t at = (size_t)(p % B) * n + s->idx;
+    const size_t plane = (size_t)B * n;
+    float *ib = g->in_block(b);
+    for (uint32_t c = 0; c < g->ich; ++c) ib[c * plane + at] = in[c];
+    // this frame's output: the engine's frame p - depth * block (zeros before it exists); that
+    // block has run (b - depth < R) and its slot is not rewritten before this instance gives block b + 1
+    if (b < g->depth) {
         for (uint32_t c = 0; c < g->och; ++c) out[c] = 0.f;
     } else {
-        const float *o = g->out[(blocks - 1) & 1].data();
+        const float *o = g->out_block(b - g->depth);
         for (uint32_t c = 0; c < g->och; ++c) out[c] = o[c * plane + at];
     }
-    if (pos == 0) g->filling.store(true, std::memory_order_relaxed);   // once per instance per block
-    s->pos.store(pos + 1, std::memory_order_relaxed);
-    if (pos + 1 == g->block && g->complete.fetch_add(1, std::memory_order_acq_rel) + 1 == g->live.load()) {
+    s->given.store(p + 1, std::memory_order_relaxed);
+    if (p % B == B - 1) {            // its last frame of block b: count it, run what is complete
         std::lock_guard<std::mutex> gl(g->mu);
-        // re-checked under the lock: a concurrent destroy may have run the block already
-        if (g->complete.load() == g->live.load() && g->blocks.load() == blocks) return run_block(g);
+        ++g->complete[b % g->depth];
+        return run_complete(g);
     }
     return OLFX_OK;
 }
 
-uint32_t olfx_sample_latency(const olfx_sample *s) { return s ? s->g->block : 0; }
+uint32_t olfx_sample_latency(const olfx_sample *s) { return s ? s->g->block * s->g->depth : 0; }
 uint32_t olfx_sample_generation_size(const olfx_sample *s) { return s ? (uint32_t)s->g->members.size() : 0; }
 uint32_t olfx_sample_index(const olfx_sample *s) { return s ? s->idx : 0; }
 

@@ -240,6 +240,49 @@ def test_late_instances_form_a_second_generation(cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("depth,buf", [(2, 512), (1, 256), (4, 600)])
+def test_instance_major_host_buffers(cuda, depth, buf):
+    """a host that runs each reverb over its whole buffer in turn (instance-major,
+    the per-plugin processBlock shape, modules/juce/host/host.cpp:682) -- 3 instances, `buf` frames
+    each per cycle, 5 cycles -- with the pool depth D = ceil(buf / block): equals the oracle delayed
+    by the documented latency D * block, bit for bit, with a setter landing at the instance's next
+    block boundary.  (buf = 600 is not a multiple of the block: the lead reaches ceil(600 / 256) + 1 = 4.)"""
+    lib = ofx.load()
+    F = _fns(lib, False)
+    B, n, cycles = 256, 3, 5
+    assert lib.olfx_dattorro_pool_config_depth(0, B, depth) == 0
+    rng = np.random.default_rng(40 + depth)
+    p = _draw_params(n, rng)
+    vs = [F["create"]() for _ in range(n)]
+    assert lib.olfx_dattorro_latency(vs[0]) == depth * B
+    for i, v in enumerate(vs):
+        for f, s in enumerate(SETTERS):
+            F[s](v, float(p[f, i]))
+    T = buf * cycles
+    x = (rng.random((T, n), dtype=np.float32) - 0.5).astype(np.float32)
+    y = np.zeros((2, T, n), np.float32)
+    t_set = 2 * buf                              # instance 1's setter before its third buffer
+    for c in range(cycles):
+        for i, v in enumerate(vs):
+            if i == 1 and c * buf == t_set:
+                F["setDecay"](v, 0.35)
+            for t in range(c * buf, (c + 1) * buf):
+                F["process"](v, float(x[t, i]))
+                y[0, t, i] = F["getLeft"](v)
+                y[1, t, i] = F["getRight"](v)
+    for v in vs:
+        F["delete"](v)
+    assert lib.olfx_dattorro_pool_config(0, B) == 0
+    L = depth * B
+    land = -(-t_set // B) * B                    # the instance's next block boundary at or after it
+    ref = _oracle(n, p, x, changes=[(land, 1, 5, 0.35)])
+    assert not np.any(y[:, :L])
+    got, want = y[:, L:], ref[:, :T - L]
+    assert bits_equal(got, want), first_mismatch(got, want)
+    assert np.any(want != 0)
+
+
+@pytest.mark.gpu
 def test_instance_running_a_block_ahead_aborts(cuda):
     r = _run_child("""
         import ol_dsp_amd as ofx
@@ -252,3 +295,17 @@ def test_instance_running_a_block_ahead_aborts(cuda):
     """)
     assert r.returncode != 0 and "unreachable" not in r.stdout
     assert "started block 1 before the other 1 live instances" in r.stderr
+    # depth 2: two blocks of run-ahead are taken, the third aborts
+    r = _run_child("""
+        import ol_dsp_amd as ofx
+        lib = ofx.load()
+        assert lib.olfx_dattorro_pool_config_depth(0, 8, 2) == 0
+        a, b = lib.DattorroVerb_create(), lib.DattorroVerb_create()
+        for t in range(16):
+            lib.DattorroVerb_process(a, 0.5)
+        print("sixteen taken", flush=True)
+        lib.DattorroVerb_process(a, 0.5)
+        print("unreachable")
+    """)
+    assert r.returncode != 0 and "sixteen taken" in r.stdout and "unreachable" not in r.stdout
+    assert "started block 2 before the other 1 live instances" in r.stderr
