@@ -18,8 +18,6 @@
 #include "dattorro_stage.h"
 #include "chorus_stage.h"
 
-#include <cstdlib>
-
 namespace olfx {
 
 // Uniform mode: IN1 (the second input diffuser, 128 positions, verb.cpp:180) is read and written
@@ -83,49 +81,11 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v4(DattorroArgs a) {
     if constexpr (!GATHER) in1.lds_out(a, i);
 }
 
-// Gather mode's pre-pass: one lane per instance, chunk by chunk in stream order as
-// DelayBuffer_process (verb.cpp:107-110: write position t, then read t - d): the chunk's
-// pre-delayed samples are read first -- the positions before the chunk from the instance's own
-// ring (two aligned 16-B pieces: consecutive chunks hit the same line back to back, one fetch per
-// line), those inside it (d < 4) from the chunk's input -- then the chunk's mono input (l + r) / 2
-// is written (a lane's pieces of one line leave back to back: the L2 merges them into whole lines).
-// The pre-delayed block goes out as [F/4][n][4] (coalesced) for the network.
 constexpr uint32_t kPreSize = kDtSize[DT_PRE];
-__global__ __launch_bounds__(256) void dattorro_predelay_v1(DattorroArgs a) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
-    const uint32_t n = a.n;
-    const size_t plane = a.plane;
-    const bool stereo = a.in_ch == 2;
-    const uint32_t d = (uint32_t)a.coef[DTC_PREDELAY * n + i];         // exact integer 0..8191
-    const float *ring_r = a.pre_im + (size_t)i * kPreSize;
-    float *ring = a.pre_im + (size_t)i * kPreSize;
-    float4 *blk = (float4 *)a.pre_block;
-    for (uint32_t f0 = 0; f0 < a.n_frames; f0 += 4) {
-        float x[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float l = a.in[(size_t)(f0 + k) * n + i];
-            x[k] = stereo ? (l + a.in[plane + (size_t)(f0 + k) * n + i]) / 2 : l;
-        }
-        const uint32_t t = a.t0 + f0, q = t - d, g = q & ~3u;
-        const float4 pa = *(const float4 *)(ring_r + (g & (kPreSize - 1u)));
-        const float4 pb = *(const float4 *)(ring_r + ((g + 4u) & (kPreSize - 1u)));
-        float v[4];
-        olfx::dt::shift4(q & 3u, pa, pb, v);
-        // positions inside this chunk (d <= k): x[k - d], by selects (no indexed register access)
-        v[0] = d == 0u ? x[0] : v[0];
-        v[1] = d == 0u ? x[1] : (d == 1u ? x[0] : v[1]);
-        v[2] = d == 0u ? x[2] : (d == 1u ? x[1] : (d == 2u ? x[0] : v[2]));
-        v[3] = d == 0u ? x[3] : (d == 1u ? x[2] : (d == 2u ? x[1] : (d == 3u ? x[0] : v[3])));
-        blk[(size_t)(f0 >> 2) * n + i] = make_float4(v[0], v[1], v[2], v[3]);
-        *(float4 *)(ring + (t & (kPreSize - 1u))) = make_float4(x[0], x[1], x[2], x[3]);
-    }
-}
 
-// dattorro_predelay_v2: v1's pass with whole 128-B lines.  v1 moved 16-B pieces, one per lane and
-// 4-frame chunk, each in its own line (64 lines per instruction; a line touched by 8 chunks):
-// 0.78 ms for the gather-mode reverb against 0.54 uniform.  One wave per workgroup = 64 instances,
+// dattorro_predelay_v2: gather mode's pre-pass in whole 128-B lines (round 4's first form, one lane
+// per instance in 4-frame chunks moving 16-B pieces -- 64 lines per instruction, each line touched
+// by 8 chunks -- made the mode 0.78 ms against 0.54 uniform and is gone).  One wave per workgroup = 64 instances,
 // 32-frame chunks aligned to the ring's lines (chunk positions [T, T + 32), T % 32 == 0):
 //   - a chunk's ring write is exactly one line per instance, stored cooperatively (8 lanes x 16 B
 //     per line, 8 lines per instruction) from the LDS history `hist`;
@@ -138,7 +98,7 @@ __global__ __launch_bounds__(256) void dattorro_predelay_v1(DattorroArgs a) {
 //     own line [T, T + 32) -- when it is that line, hist's copy replaces it.
 // Frames outside [t0, t0 + n_frames) in the first and last chunks are neither stored nor output;
 // the first chunk's history positions [T, t0) and [T - 32, T) are loaded into `hist` from the ring.
-// The pre-delayed block goes out as [F/4][n][4] (coalesced), as v1's.
+// The pre-delayed block goes out as [F/4][n][4] (coalesced).
 namespace {
 constexpr uint32_t kPdLine = 32;                   // positions per 128-B line
 constexpr uint32_t kPdLines = kPreSize / kPdLine;   // 256
@@ -372,13 +332,8 @@ __global__ __launch_bounds__(256) void dattorro_pre_convert(DattorroArgs a, int 
     else *pm = *im;
 }
 
-// v3 when the rows allow it; OLFX_PREDELAY_KERNEL=1 / 2 runs v1 / v2 (A/B diagnostics)
+// v3 when the rows allow it (16-B aligned input rows), else v2
 int predelay_kernel(uint32_t n, uint64_t plane, const float *in) {
-    static const int forced = [] {
-        const char *e = std::getenv("OLFX_PREDELAY_KERNEL");
-        return e ? std::atoi(e) : 0;
-    }();
-    if (forced == 1 || forced == 2) return forced;
     return n % 4u == 0u && plane % 4u == 0u && ((uintptr_t)in & 15u) == 0u ? 3 : 2;
 }
 
@@ -395,9 +350,7 @@ hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s) {
         if ((uint64_t)a.n_frames * a.n * 4u >= (1ull << 32)) return hipErrorInvalidValue;
         const int v = predelay_kernel(a.n, a.plane, a.in);
         if (v == 3 && a.n_frames > kPd3F) return hipErrorInvalidValue;   // the engine splits at 256
-        if (v == 1)
-            hipLaunchKernelGGL(dattorro_predelay_v1, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
-        else if (v == 2)
+        if (v == 2)
             hipLaunchKernelGGL(dattorro_predelay_v2, dim3((a.n + 63) / 64), dim3(64), 0, s, a);
         else
             hipLaunchKernelGGL(dattorro_predelay_v3, dim3((a.n + kPd3J - 1) / kPd3J), dim3(256), 0, s, a);

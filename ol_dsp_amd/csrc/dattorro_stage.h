@@ -228,7 +228,7 @@ struct PreTap {
     }
 };
 
-// Gather mode (per-instance pre-delays, verb.cpp:137-139): dattorro_predelay_v1 has already written
+// Gather mode (per-instance pre-delays, verb.cpp:137-139): dattorro_predelay_v3 (or v2) has already written
 // the block's pre-delayed input, group by group, to a.pre_block ([n_frames/4][n][4]: 16 B per lane
 // and chunk, coalesced) and kept the ring itself, instance-major.  The network reads that stream:
 // no gather across lines here, and no ring write.

@@ -38,11 +38,6 @@
 
 namespace olfx {
 
-// A/B knob: 1 = per-lane audio I/O (16 + 16 single floats per lane and chunk) everywhere
-#ifndef OLFX_FXRACK_PERLANE
-#define OLFX_FXRACK_PERLANE 0
-#endif
-
 namespace {
 
 constexpr int kFrThreads = 256;
@@ -421,7 +416,7 @@ hipError_t launch_fxrack(const FxRackArgs &a, hipStream_t s) {
     const uint32_t waves = (a.n + 31) / 32;
     const uint32_t blocks = (waves + kFrThreads / 64 - 1) / (kFrThreads / 64);
     const size_t lds = (size_t)(kFrThreads / 64) * kFrRegion * sizeof(float);
-    const bool coop = !OLFX_FXRACK_PERLANE && (a.n & 3u) == 0 && (a.plane & 3u) == 0 &&
+    const bool coop = (a.n & 3u) == 0 && (a.plane & 3u) == 0 &&
                       (((uintptr_t)a.in | (uintptr_t)a.out) & 15u) == 0;
     if (a.components) {
         if (coop) hipLaunchKernelGGL((fxrack_block_v3<true, true>), dim3(blocks), dim3(kFrThreads), lds, s, a);

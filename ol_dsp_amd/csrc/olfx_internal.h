@@ -90,8 +90,7 @@ struct DattorroArgs {
 // pre-delays, dattorro_block_v4's own tap) and instance-major (gather mode): the ring's content
 // is copied into the other layout (to_im: position-major -> instance-major)
 hipError_t launch_dattorro_pre_convert(const DattorroArgs &a, bool to_im, hipStream_t s);
-// gather mode's pre-delay pass for these rows: 3 (16-B aligned input rows), else 2;
-// OLFX_PREDELAY_KERNEL=1 / 2 forces v1 / v2 (A/B diagnostics)
+// gather mode's pre-delay pass for these rows: 3 (16-B aligned input rows), else 2
 int predelay_kernel(uint32_t n, uint64_t plane, const float *in);
 
 // ----------------------------------------------------------------------------------------------
@@ -213,10 +212,37 @@ OLFX_HD double cos2pi_d(double x) {
     r = __builtin_fma(r, t2, 1.0);
     return hi ? -r : r;
 }
+// cos(2 pi x) for the 53-bit phase x = (phase >> 11) 2^-53, exactly cos2pi_d(x) with its reduction
+// done in integers: u = x - rint(x) is the phase's high word read as SIGNED (u in [-1/2, 1/2); at
+// x = 1/2, u = -1/2 where rint gives +1/2: the same |u|), and u = hi 2^-32 + (lo >> 11) 2^-53 is one
+// exact fma (53 significant bits).  Round 5: 5 VALU instead of 8 for the conversion and reduction.
+OLFX_HD double cos2pi_phase(uint64_t phase) {
+    const int32_t sh = (int32_t)(uint32_t)(phase >> 32);
+    const uint32_t lo = (uint32_t)phase >> 11;
+    const double u = __builtin_fma((double)sh, 2.3283064365386963e-10, (double)lo * 1.1102230246251565e-16);
+    const double a = __builtin_fabs(u);
+    const bool hi = a > 0.25;
+    const double b = hi ? 0.5 - a : a;             // exact
+    const double th = b * 6.283185307179586;
+    const double t2 = th * th;
+    double r = -1.5619206968586225e-16;                        // the Horner steps of cos2pi_d
+    r = fma_dc(r, t2, 4.779477332387385e-14);
+    r = fma_dc(r, t2, -1.1470745597729725e-11);
+    r = fma_dc(r, t2, 2.08767569878681e-09);
+    r = fma_dc(r, t2, -2.755731922398589e-07);
+    r = fma_dc(r, t2, 2.48015873015873e-05);
+    r = fma_dc(r, t2, -0.001388888888888889);
+    r = fma_dc(r, t2, 0.041666666666666664);
+    r = __builtin_fma(r, t2, -0.5);
+    r = __builtin_fma(r, t2, 1.0);
+    return hi ? -r : r;
+}
 OLFX_HD double chorus_delay(uint64_t phase, double D, double cmax) {
-    const double x = (double)(phase >> 11) * 1.1102230246251565e-16;         // 53-bit phase (2^-53: exact)
-    const double d = __builtin_fma(cos2pi_d(x), D, D);
-    return d < 0.0 ? 0.0 : (d > cmax ? cmax : d);
+    const double d = __builtin_fma(cos2pi_phase(phase), D, D);
+    // clamp to [0, cmax] as min / max (one v_max_f64 + one v_min_f64; the compare-select form cost
+    // two compares, four selects and their hazard waits): equal for every non-NaN d, and d is never
+    // -0 (cos = -1 gives D - D = +0)
+    return __builtin_fmin(__builtin_fmax(d, 0.0), cmax);
 }
 OLFX_HD void chorus_split(uint64_t phase, double D, double cmax, uint32_t &di, float &fr) {
     const double d = chorus_delay(phase, D, cmax);
@@ -284,10 +310,7 @@ enum : uint32_t {
 // one host-link round trip without first reading where they are.  A workgroup with more than
 // kVevCap records puts them all in the overflow list and marks slot 0:
 // x = VEV_MORE << 8 | count << 16, y = first record in ev_more (a second round trip, for it only).
-#ifndef OLFX_VEV_CAP
-#define OLFX_VEV_CAP 4
-#endif
-constexpr uint32_t kVevCap = OLFX_VEV_CAP;
+constexpr uint32_t kVevCap = 4;
 
 struct VoiceArgs {
     float *state;               // [VCS_N][n], MoogFilter voices [VCS_N_MOOG][n]

@@ -200,10 +200,7 @@ struct Env {
 // samples per hand-off between the roles: 8 (34 barrier steps per 256-frame block, pipeline fill
 // 2 of them) measured 2 % faster than 16 (18 steps) for the Svf voice and equal for the Moog
 // voice; 32 halves the workgroups per CU (96 KB of LDS each) and is 1.7x slower
-#ifndef OLFX_VC_CHUNK
-#define OLFX_VC_CHUNK 8
-#endif
-constexpr int kVcChunk = OLFX_VC_CHUNK;
+constexpr int kVcChunk = 8;
 
 // Runs f(j) for the m samples of a chunk: unrolled when the chunk is full, so the off-recurrence
 // work of neighbouring samples interleaves (ILP for a wave that is alone on its SIMD).
@@ -406,13 +403,7 @@ __global__ __launch_bounds__(128) void voice_block_v4(VoiceArgs a) {
 // chunk is redone exactly when a lane's segment ended in it.  Roles are assigned by SIMD (below).
 // ---------------------------------------------------------------------------------------------
 // FILT (the Svf recurrence, the critical chain of the ENV + FILT pair) issues ahead of ENV on
-// their SIMD: ~2 % same-box; OSC too was slower.  0 = off.
-#ifndef OLFX_VC_PRIO
-#define OLFX_VC_PRIO 2
-#endif
-#ifndef OLFX_VC_PRIO_OSC
-#define OLFX_VC_PRIO_OSC 0
-#endif
+// their SIMD at wave priority 2: ~2 % same-box; OSC raised too was slower.
 __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     __shared__ float2 eq[3][kVcChunk][64];      // ENV -> OSC, FREQ (fc_in), FILT (amp): three chunks live
     __shared__ float sq[2][kVcChunk][64];       // OSC -> FILT: src
@@ -422,9 +413,6 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
     const uint32_t n = a.n;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if OLFX_VOICE_ROLE_WAVE
-    const uint32_t role = wave;
-#else
     // Roles by SIMD.  The roles' VALU loads differ (per 8-sample chunk FILT ~218, OSC ~190, FREQ
     // ~159, ENV ~111 instructions) and the two co-resident workgroups of a CU put wave w on the
     // same SIMD, so role = wave stacks two FILTs on one SIMD.  Each wave reads its SIMD (HW_ID
@@ -447,31 +435,13 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
         if (m == 15u) role = hw_simd[4] ? 3u - sm : sm;
         role = __builtin_amdgcn_readfirstlane(role);
     }
-#endif
-#if OLFX_VC_PRIO
-    // the roles with a per-sample recurrence (FILT; OSC with the A/B knob OLFX_VC_PRIO_OSC) ahead
-    // of their SIMD partner at issue
-    if (role == 3u || (OLFX_VC_PRIO_OSC && role == 1u)) __builtin_amdgcn_s_setprio(OLFX_VC_PRIO);
-#endif
+    // the role with the per-sample recurrence (FILT) ahead of its SIMD partner at issue
+    if (role == 3u) __builtin_amdgcn_s_setprio(2);
     const uint32_t i0 = blockIdx.x * 64 + lane;
     const uint32_t i = i0 < n ? i0 : n - 1;      // dead lanes mirror voice n-1, as in v4
     const uint32_t me = i - blockIdx.x * 64;
     const uint32_t nf = a.n_frames;
     const uint32_t nsteps = (nf + kVcChunk - 1) / kVcChunk + 2;
-#if OLFX_VC_STAMP
-    // diagnostic build: each role wave's total cycles and cycles at the step barriers go to output
-    // rows 2 role and 2 role + 1 of its voices (the outputs are garbage in this build)
-    const uint64_t st_start = __builtin_amdgcn_s_memtime();
-    uint64_t st_wait = 0;
-#define VC_SYNC()                                                  \
-    do {                                                           \
-        const uint64_t st_a = __builtin_amdgcn_s_memtime();        \
-        __syncthreads();                                           \
-        st_wait += __builtin_amdgcn_s_memtime() - st_a;            \
-    } while (0)
-#else
-#define VC_SYNC() __syncthreads()
-#endif
     const float *c = a.coef;
     float *s = a.state;
     auto len = [&](uint32_t k) {             // frames of chunk k (the last may be short)
@@ -540,7 +510,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     });
                 }
             }
-            VC_SYNC();
+            __syncthreads();
         }
         s[VCS_ENVA_X * n + i] = ea.x;
         s[VCS_ENVF_X * n + i] = ef.x;
@@ -630,7 +600,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     }
                 }
             }
-            VC_SYNC();
+            __syncthreads();
         }
         s[VCS_PHASE * n + i] = phase;
         s[VCS_PORT_Z * n + i] = port_z;
@@ -689,7 +659,7 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     }
                 }
             }
-            VC_SYNC();
+            __syncthreads();
         }
     } else {
         // ---- FILT: Svf::Process; Low() = the average of the two passes' low outputs; * amp ----
@@ -725,17 +695,11 @@ __global__ __launch_bounds__(256) void voice_block_v5(VoiceArgs a) {
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((low1 + low) * sa.y), ro, i * 4u, j * n * 4u, 0);
                 });
             }
-            VC_SYNC();
+            __syncthreads();
         }
         s[VCS_LOW * n + i] = low;
         s[VCS_BAND * n + i] = band;
     }
-#if OLFX_VC_STAMP
-    __syncthreads();
-    a.out[(size_t)(2u * role) * n + i] = (float)(__builtin_amdgcn_s_memtime() - st_start);
-    a.out[(size_t)(2u * role + 1u) * n + i] = (float)st_wait;
-#endif
-#undef VC_SYNC
 }
 
 hipError_t launch_voice(const VoiceArgs &a, hipStream_t s) {

@@ -1,6 +1,8 @@
 """Diagnostic (round 4): per-role total and barrier-wait cycles of voice_block_v5, from a build with
 -DOLFX_VC_STAMP (each role wave writes [total cycles, cycles at the step barriers] into output
-rows 2 role, 2 role + 1; the outputs are garbage in that build).  Usage (GPU box):
+rows 2 role, 2 role + 1; the outputs are garbage in that build).  The stamp code left the kernel in
+round 5: build it from the round-4 source, `bash tools/build_variant.sh vcstamp 5fe6fd8 -DOLFX_VC_STAMP=1`.
+Usage (GPU box):
   OLFX_LIB=build/ab/vcstamp.so python tools/voice_stamps.py [voices]"""
 import sys
 
