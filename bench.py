@@ -153,8 +153,22 @@ def _oracle():
     return O
 
 
+def _rcp_table():
+    """v_rcp_f32's results over the mantissas of [1, 2), read from the device by the test helper
+    tests/gpu_probe/librcp_probe.so (the voice oracle's kernel-arithmetic model, oracle/voice_ref.c);
+    None when the helper is not built."""
+    import ctypes
+    path = os.path.join(ROOT, "tests", "gpu_probe", "librcp_probe.so")
+    if not os.path.exists(path):
+        return None
+    L = ctypes.CDLL(path)
+    L.probe_rcp_table.argtypes = [ctypes.c_void_p]
+    tab = np.empty(1 << 23, np.uint32)
+    return tab if L.probe_rcp_table(tab.ctypes.data) == 0 else None
+
+
 def _oracle_bank(kind: str, p: np.ndarray, sr: float, o0: bool = False, ref: bool = False, notes=None,
-                 frames: int = 256):
+                 frames: int = 256, kernel_arith: bool = False):
     """CPU oracle bank of `kind` for params p [fields][m] (columns = instances): (step, banks,
     setter).  step(x [ch][frames][m] or None, threads) -> [och][frames][m]; setter(j, field, v)
     sets one C-ABI field of instance j (the chain's fields route to their stage)."""
@@ -180,7 +194,7 @@ def _oracle_bank(kind: str, p: np.ndarray, sr: float, o0: bool = False, ref: boo
                 bank.set(i, f, float(p[f, i]))
         return (lambda x, t=1: bank.process(x, t)), bank, (lambda j, f, v: bank.set(j, f, v))
     if kind in VOICE_KINDS:
-        bank = O.Voice(n, sr, moog=kind == "voice_moog", o0=o0)
+        bank = O.Voice(n, sr, moog=kind == "voice_moog", o0=o0, kernel_arith=kernel_arith)
         for i in range(n):
             bank.config(i, p[:, i])
             if notes is not None:
@@ -276,21 +290,27 @@ def parity_check(job: dict, sr: float) -> dict:
     last block with what the GPU produced (job filled in by run_workload)."""
     kind, idx, B = job["kind"], job["idx"], job["block"]
     m = len(idx)
-    step, _banks, setter = _oracle_bank(kind, job["params"], sr, notes=job.get("notes"), frames=B)
     voice = kind in VOICE_KINDS
-    bank = _banks if voice else None
     xs, pool_n = job.get("pool"), job.get("pool_n", 1)
-    y = None
-    for b in range(job["blocks"]):
-        if voice:
-            if b == job.get("note_off_block", -1):
-                for j in range(m):
-                    bank.note(j, False, int(job["notes"][j]))
-            for j, on, note in job.get("events", lambda b: [])(b):
-                bank.note(j, on, note)
-        for j, f, v in job.get("ccs", lambda b: [])(b):
-            setter(j, f, v)
-        y = step(None if voice else xs[b % pool_n])
+
+    def replay(kernel_arith=False):
+        step, _banks, setter = _oracle_bank(kind, job["params"], sr, notes=job.get("notes"), frames=B,
+                                            kernel_arith=kernel_arith)
+        bank = _banks if voice else None
+        y = None
+        for b in range(job["blocks"]):
+            if voice:
+                if b == job.get("note_off_block", -1):
+                    for j in range(m):
+                        bank.note(j, False, int(job["notes"][j]))
+                for j, on, note in job.get("events", lambda b: [])(b):
+                    bank.note(j, on, note)
+            for j, f, v in job.get("ccs", lambda b: [])(b):
+                setter(j, f, v)
+            y = step(None if voice else xs[b % pool_n])
+        return y
+
+    y = replay()
     g = job["gpu"]
     res = {"instances": m, "blocks": job["blocks"]}
     if voice:
@@ -302,6 +322,20 @@ def parity_check(job: dict, sr: float) -> dict:
         err = float(np.max(np.abs(a - r) / np.maximum(np.abs(r), rms))) if a.size else 0.0
         res.update({"check": f"max_rel_err<={VOICE_TOL:g}", "max_rel_err": err,
                     "ok": bool(same_fin and err <= VOICE_TOL), "finite_instances": int(fin.sum())})
+        # and bit-exact against the oracle's kernel-arithmetic mode (the measured v_rcp_f32 model)
+        tab = _rcp_table()
+        if tab is not None:
+            O = _oracle()
+            O.set_rcp_table(tab)
+            try:
+                yk = replay(kernel_arith=True)
+            finally:
+                O.set_rcp_table(None)
+            fk = np.isfinite(yk)
+            bad = int(np.count_nonzero(yk[fk].view(np.uint32) != np.ascontiguousarray(g)[fk].view(np.uint32)))
+            exact = bool(np.array_equal(fk, np.isfinite(g)) and bad == 0)
+            res.update({"check": f"bit-exact(karith)+rel<={VOICE_TOL:g}",
+                        "mismatched_samples_kernel_arith": bad, "ok": res["ok"] and exact})
     else:
         bad = int(np.count_nonzero(np.ascontiguousarray(g).view(np.uint32) != np.ascontiguousarray(y).view(np.uint32)))
         res.update({"check": "bit-exact", "ok": bad == 0, "mismatched_samples": bad})
