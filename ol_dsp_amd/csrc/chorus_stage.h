@@ -35,22 +35,14 @@ __device__ __forceinline__ Rsrc rsrc(const void *p, uint64_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0,
                                              (int)(uint32_t)(bytes > 0xFFFFFFFFull ? 0xFFFFFFFFull : bytes), 0x00020000);
 }
-// cache policy of the streamed accesses (block input/output, ring stores): 0 = default,
-// 2 = nt (gfx950 aux bit 1).  A/B knob; the shipped value is measured.
+// cache policy of the streamed accesses (block input/output, ring stores): 0 = default (nt, aux
+// bit 1, measured no better: DESIGN.md section 4)
+constexpr int kStreamAux = 0;
 // s_setprio 3 while the line-carry stage issues the next chunk's input loads and line loads (the
 // other wave of the SIMD yields its issue slots for those few instructions, so they leave earlier
 // and the chunk's arithmetic covers more of their latency): chorus ~1 % faster over six same-box
-// pairs, pitch-shift and chain (one wave per SIMD) unchanged.  0 = off.
-#ifndef OLFX_CH_PRIO
-#define OLFX_CH_PRIO 3
-#endif
-#ifndef OLFX_CH_PRIO_IN
-#define OLFX_CH_PRIO_IN 3
-#endif
-#ifndef OLFX_STREAM_AUX
-#define OLFX_STREAM_AUX 0
-#endif
-constexpr int kStreamAux = OLFX_STREAM_AUX;
+// pairs, pitch-shift and chain (one wave per SIMD) unchanged
+constexpr int kLoadPrio = 3;
 
 template <int AUX = 0>
 __device__ __forceinline__ float ld1(Rsrc r, uint32_t voff, uint32_t soff) {

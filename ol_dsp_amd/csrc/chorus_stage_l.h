@@ -35,10 +35,6 @@
 #include "chorus_stage.h"
 
 
-#ifndef OLFX_CH_CLAMP
-#define OLFX_CH_CLAMP 1
-#endif
-
 namespace olfx {
 namespace ch {
 
@@ -114,8 +110,8 @@ __device__ __forceinline__ PlanL plan_chunk_l(uint64_t lfo_acc, uint64_t lfo_inc
 // takes cooperative input but sinks into registers: OUT_LDS = false)
 template <bool FULL, bool COOP = false, bool OUT_LDS = COOP>
 struct ChStageL {
-    // window slots: kWin, then junk: one slot (patches, the straggler), two with clamped staging
-    static constexpr int kChunk = 16, kWin = 24, kSlots = kWin + (OLFX_CH_CLAMP ? 2 : 1);
+    // window slots: kWin, then two junk slots (patches, the straggler, clamped staging)
+    static constexpr int kChunk = 16, kWin = 24, kSlots = kWin + 2;
     // floats of LDS per wave: one window per tap (chorus 3 x 26 x 64 = 4,992 = 19.5 KB: 2 waves/SIMD,
     // 156 KB per CU; pitch-shift alone 3,328 + its output staging)
     // COOP output staging [ch][frame][instance] (kOutCh below): in the chorus it overlays the pitch
@@ -130,9 +126,6 @@ struct ChStageL {
     static_assert(!FULL || kOutFloats <= kPsvBase, "output staging must not reach the psv staging");
     static constexpr int kTaps = FULL ? 3 : 2;
     static_assert(2 * 32 * kStride <= kRegion, "staging must fit in the window region");
-    // window patches as stores to a clamped slot (out-of-window frames land in the junk slot) rather
-    // than exec-masked stores (A/B knob)
-    static constexpr bool kClampPatch = OLFX_CH_CLAMP != 0;
 
     uint32_t lane, j, ch, inst0, n, i;
     bool valid;
@@ -229,9 +222,7 @@ struct ChStageL {
     template <int HI>
     __device__ __forceinline__ void load_lines(const PlanL &p, uint32_t w, bool first) {
         constexpr int LO = HI ^ 1;
-#if OLFX_CH_PRIO
-        __builtin_amdgcn_s_setprio(OLFX_CH_PRIO);   // A/B knob: the line loads ahead of the other wave's arithmetic
-#endif
+        __builtin_amdgcn_s_setprio(kLoadPrio);      // the line loads ahead of the other wave's arithmetic
         const int s[3] = {p.sA, p.sB, p.sC};
         uint32_t s15n = 0;
         int pk[3];
@@ -270,9 +261,7 @@ struct ChStageL {
             strag_slot = need ? top - ((w + (uint32_t)p.sC)) : (uint32_t)kWin;
             if (need) strag = ld1(rC, own_cb() + (top & cmask) * 8u, 0);
         }
-#if OLFX_CH_PRIO
         __builtin_amdgcn_s_setprio(0);
-#endif
     }
 
     // lines of tap t -> the chunk's LDS window ([tap][slot][lane], slot = position - window start)
@@ -287,28 +276,14 @@ struct ChStageL {
             const int slo = 2 * (int)pm() - st;          // line L' piece -> slots slo, slo + 1
             const int shi = slo + 16;                     // line L'+1 piece
             const float4 a = ln[t][LO][r], b = ln[t][HI][r];
-            if constexpr (kClampPatch) {
-                // pieces outside the window go to the junk slots kWin, kWin + 1 (slo is even, so a
-                // piece is wholly inside or outside; slo < 0 wraps to a large unsigned value)
-                float *plo = base + min((uint32_t)slo, (uint32_t)kWin) * kRow + 2 * jj;
-                float *phi = base + min((uint32_t)shi, (uint32_t)kWin) * kRow + 2 * jj;
-                *(float2 *)plo = make_float2(a.x, a.y);
-                *(float2 *)(plo + kRow) = make_float2(a.z, a.w);
-                *(float2 *)phi = make_float2(b.x, b.y);
-                *(float2 *)(phi + kRow) = make_float2(b.z, b.w);
-            } else {
-                // only pieces inside the window are written (exec-masked)
-                if (slo >= 0) {
-                    float *plo = base + slo * kRow + 2 * jj;
-                    *(float2 *)plo = make_float2(a.x, a.y);
-                    *(float2 *)(plo + kRow) = make_float2(a.z, a.w);
-                }
-                if (shi < kWin) {
-                    float *phi = base + shi * kRow + 2 * jj;
-                    *(float2 *)phi = make_float2(b.x, b.y);
-                    *(float2 *)(phi + kRow) = make_float2(b.z, b.w);
-                }
-            }
+            // pieces outside the window go to the junk slots kWin, kWin + 1 (slo is even, so a piece
+            // is wholly inside or outside; slo < 0 wraps to a large unsigned value)
+            float *plo = base + min((uint32_t)slo, (uint32_t)kWin) * kRow + 2 * jj;
+            float *phi = base + min((uint32_t)shi, (uint32_t)kWin) * kRow + 2 * jj;
+            *(float2 *)plo = make_float2(a.x, a.y);
+            *(float2 *)(plo + kRow) = make_float2(a.z, a.w);
+            *(float2 *)phi = make_float2(b.x, b.y);
+            *(float2 *)(phi + kRow) = make_float2(b.z, b.w);
         }
         if (t == 2) base[strag_slot * kRow + lane] = strag;
     }
@@ -436,38 +411,20 @@ struct ChStageL {
             // psv_{c-1}'s frame k goes to slot k - 16 - sC when that lies in the window: all 16 read
             // first (a read after a store that may alias it would wait for the store, slot by slot),
             // then stored
-            if constexpr (kClampPatch) {
-                // branch-free: a slot outside the window becomes the junk slot kWin (unsigned min), so
-                // no exec-mask region per store (each cost a compare, a saveexec, an exec restore and a
-                // skip branch: instructions that a wave alone on its SIMD issues one by one)
-                if (started) {
-                    const float *prev = region + kPsvBase + j * kStride + ch;
-                    float pv[kChunk];
-#pragma unroll
-                    for (int k = 0; k < kChunk; ++k) pv[k] = prev[2 * k];
-                    stage_tap<PAR, 2>();
-                    const uint32_t nlo = (uint32_t)(-(kChunk + cur.sC));   // slot of frame k = k + nlo
-#pragma unroll
-                    for (int k = 0; k < kChunk; ++k) wC[min((uint32_t)k + nlo, (uint32_t)kWin) * kRow] = pv[k];
-                } else {
-                    stage_tap<PAR, 2>();
-                }
-            } else {
-                const bool need = started && cur.sC > -kWin - kChunk;
+            // branch-free: a slot outside the window becomes the junk slot kWin (unsigned min), so
+            // no exec-mask region per store (each cost a compare, a saveexec, an exec restore and a
+            // skip branch: instructions that a wave alone on its SIMD issues one by one)
+            if (started) {
+                const float *prev = region + kPsvBase + j * kStride + ch;
                 float pv[kChunk];
-                if (need) {
-                    const float *prev = region + kPsvBase + j * kStride + ch;
 #pragma unroll
-                    for (int k = 0; k < kChunk; ++k) pv[k] = prev[2 * k];
-                }
+                for (int k = 0; k < kChunk; ++k) pv[k] = prev[2 * k];
                 stage_tap<PAR, 2>();
-                if (need) {
-                    const int lo = kChunk + cur.sC;          // frames k in [lo, lo + kWin) land in the window
-                    float *pC = wC - lo * kRow;
+                const uint32_t nlo = (uint32_t)(-(kChunk + cur.sC));   // slot of frame k = k + nlo
 #pragma unroll
-                    for (int k = 0; k < kChunk; ++k)
-                        if (k >= lo && k < lo + kWin) pC[k * kRow] = pv[k];
-                }
+                for (int k = 0; k < kChunk; ++k) wC[min((uint32_t)k + nlo, (uint32_t)kWin) * kRow] = pv[k];
+            } else {
+                stage_tap<PAR, 2>();
             }
         }
         stage_tap<PAR, 0>();
@@ -477,31 +434,19 @@ struct ChStageL {
         {
             const int limA = kWin + cur.sA, limB = kWin + cur.sB;
             float *pA = wP0 - cur.sA * kRow, *pB = wP1 - cur.sB * kRow;
-            if constexpr (kClampPatch) {
-                // frame k -> slot min(k, lim) - s: past the window that is the junk slot kWin; past
-                // a short chunk's C frames, slot C - s, a position no frame of this chunk reads
-                const int mA = min(limA, C), mB = min(limB, C);
+            // frame k -> slot min(k, lim) - s: past the window that is the junk slot kWin; past a
+            // short chunk's C frames, slot C - s, a position no frame of this chunk reads
+            const int mA = min(limA, C), mB = min(limB, C);
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) {
-                    pA[min(k, mA) * kRow] = x[k];
-                    pB[min(k, mB) * kRow] = x[k];
-                }
-            } else {                                  // one compare per frame, exec-masked stores
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) {
-                    if (k < C && k < limA) pA[k * kRow] = x[k];
-                    if (k < C && k < limB) pB[k * kRow] = x[k];
-                }
+            for (int k = 0; k < kChunk; ++k) {
+                pA[min(k, mA) * kRow] = x[k];
+                pB[min(k, mB) * kRow] = x[k];
             }
         }
         started = true;
-#if OLFX_CH_PRIO_IN
-        __builtin_amdgcn_s_setprio(OLFX_CH_PRIO_IN);   // A/B knob: the next chunk's input loads too
-#endif
+        __builtin_amdgcn_s_setprio(kLoadPrio);      // the next chunk's input loads too
         prefetch();
-#if OLFX_CH_PRIO_IN
         __builtin_amdgcn_s_setprio(0);
-#endif
 
         const bool fast = C == kChunk && __all(cur.okA && cur.okB);
         if (fast) {

@@ -36,7 +36,17 @@ def edit_lbs(s):
     return s.replace(c, "", 1)
 
 
-EDITS = {"lbs": ("chorus_stage_l.h", edit_lbs)}
+def edit_desync(s):
+    # the second wave of each SIMD (odd wave slot, HW_ID bits 3:0) starts about half a chunk late, so
+    # the two waves of a SIMD are out of phase (one staging through LDS while the other computes)
+    a = "    Stage st;\n    st.init(a, lds + wib * Stage::kRegion, lane, inst0);"
+    assert a in s
+    b = ("    if (__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)) & 1u) {\n"
+         "        __builtin_amdgcn_s_sleep(127);\n        __builtin_amdgcn_s_sleep(40);\n    }\n")
+    return s.replace(a, b + a, 1)
+
+
+EDITS = {"lbs": ("chorus_stage_l.h", edit_lbs), "desync": ("chorus.hip", edit_desync)}
 
 
 def main():
