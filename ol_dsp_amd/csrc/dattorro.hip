@@ -10,11 +10,11 @@
 // per-instance pre-delays, those groups lie in 64 different 128-B lines per wave instruction, and
 // successive chunks of a lane touch one line eight times after it has left the caches: the gather
 // read 8x its bytes (dattorro_rpd +30 %, round 3).  Gather mode (the engine switches when the
-// pre-delays differ) keeps that ring instance-major and runs dattorro_predelay_v2 ahead of the
-// block: each instance's ring is read and written in whole 128-B lines (below) and the network
-// gets its pre-delayed block as a coalesced stream (PreBlock).  The network itself then reads no
-// input and writes no pre-delay ring.  Measured (65,536 instances, random pre-delays): pre-pass
-// 0.073 ms + network 0.479 ms = 0.552 ms against the uniform reverb's 0.514 ms (1.07x).
+// pre-delays differ) keeps that ring instance-major, read and written in whole 128-B lines: inside
+// the network's own launch (dattorro_block_v4f, round 5: one 32-frame piece ahead, through LDS) or,
+// for audio rows that are not 16-B aligned, in dattorro_predelay_v2 ahead of it (its pre-delayed
+// block as a coalesced stream, PreBlock).  Measured (65,536 instances, random pre-delays, same box):
+// v4f 0.589 ms, the round-4 pre-pass + network 0.597, the uniform reverb 0.554 (1.063x).
 #include "dattorro_stage.h"
 #include "chorus_stage.h"
 
@@ -220,105 +220,150 @@ __global__ __launch_bounds__(64) void dattorro_predelay_v2(DattorroArgs a) {
     }
 }
 
-// dattorro_predelay_v3: the whole call's block (<= 256 frames) at once.  The pass has no serial
-// dependence inside a block: every pre-delayed sample x[t - d] is either this block's own input
-// (d <= f, from LDS) or a ring position written before the block (d > f), so v2's chunk-by-chunk
-// chain of line loads becomes three phases per 32-instance workgroup (4 waves, 66 KB of LDS: two
-// workgroups per CU):
-//   1. the block's input rows (32 instances = 128 B per row and channel, 16-B pieces, all 16 loads
-//      in flight at once), mono (l + r) / 2 transposed into `mono` [instance][frame];
-//   2. per instance (wave-uniform), lanes = 64 consecutive frames: the ring reads t - d of one
-//      instance are consecutive positions of its instance-major row (two or three 128-B lines per
-//      instruction); d <= f reads `mono` instead; results into `outv` [instance][frame];
-//   3. the pre-delayed block out of `outv` as [F/4][n][4] rows (512 B per frame group) and the
-//      block's mono input into the ring (1 KB per instance), after every read of phase 2: a
-//      pre-delay above 8192 - F reads a slot this block overwrites, and reads it first, as
-//      DelayBuffer_process does (verb.cpp:107-110).
-// Needs 16-B aligned input rows (n % 4 == 0, plane % 4 == 0, in 16-B aligned); v2 otherwise.
+// dattorro_block_v4f: gather mode in ONE launch (round 5; VERDICT r4: the pre-pass round-tripped
+// the pre-delayed block through HBM).  The network's own wave (64 instances) keeps the pre-delay
+// path in LDS, one 32-frame piece ahead, with no serial dependence on the network:
+//   M[2][64][36]: a piece's mono input (l + r) / 2, [instance][frame]: loaded as cooperative rows
+//                 (2 dwordx4 per lane and chunk: 4 frames x 64 instances x 2 channels) during the
+//                 piece before, transposed on the way into LDS; the network's xin comes from here;
+//   W[2][64][36]: each instance's 36 ring positions from A = (T - d) & ~3 (its pre-delayed samples
+//                 of the piece, T = the piece's first position), loaded cooperatively (8 instances x
+//                 128 B per instruction, one per chunk, and the 36th-position group) during the
+//                 piece before.
+// At its first chunk a piece writes its own input into the instance-major ring (8 cooperative
+// 128-B stores, 8 instances each), so the window loads for the next piece, issued after, see every
+// position before that piece; positions inside the piece itself (d <= f) are read from M
+// (dt::PreFused).  A pre-delay up to 8191 reads positions the launch has not yet overwritten:
+// ring slots are only written one piece at a time, at the piece's start, and a window load reads
+// before the piece that would overwrite it, as DelayBuffer_process reads after its write only for
+// d = 0 (verb.cpp:107-110).  Dead lanes of the last wave mirror instance n - 1 exactly (its input
+// row, its window, its state), so their stores duplicate lane n - 1's.  Needs 16-B aligned input
+// rows (n % 4 == 0, plane % 4 == 0, in 16-B aligned); dattorro_predelay_v2 + dattorro_block_v4<true>
+// otherwise.  LDS 36 KB per wave: four waves per CU, as v4 (IN1 stays in HBM here).
 namespace {
-constexpr uint32_t kPd3J = 32;                      // instances per workgroup
-constexpr uint32_t kPd3F = 256;                     // frames per launch (the engine splits at 256)
-constexpr uint32_t kPd3Row = kPd3F + 1;             // LDS floats per instance row (odd)
+constexpr uint32_t kFuS = 36;                      // LDS row stride (floats): 16-B aligned rows
+constexpr uint32_t kFuPiece = 32;                  // frames per piece
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+}  // namespace
 
-__global__ __launch_bounds__(256) void dattorro_predelay_v3(DattorroArgs a) {
-    __shared__ float mono[kPd3J * kPd3Row];
-    __shared__ float outv[kPd3J * kPd3Row];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t n = a.n, F = a.n_frames, t0 = a.t0;
-    const uint32_t i0 = blockIdx.x * kPd3J, nv = min(n - i0, kPd3J);
+__global__ __launch_bounds__(64, 1) void dattorro_block_v4f(DattorroArgs a) {
+    __shared__ __attribute__((aligned(16))) float fM[2][64 * kFuS];
+    __shared__ __attribute__((aligned(16))) float fW[2][64 * kFuS];
+    const uint32_t lane = threadIdx.x, n = a.n, F = a.n_frames, t0 = a.t0;
+    const uint32_t i0 = blockIdx.x * 64u;
+    const uint32_t i = min(i0 + lane, n - 1u);            // dead lanes mirror instance n - 1
+    const uint32_t jrow = i - i0;                          // the LDS row this lane computes on
     const bool stereo = a.in_ch == 2;
     constexpr uint32_t kOob = 0xFFFFFFF0u;
-    {   // 1. input rows: piece pc (instances 4 pc .. 4 pc + 3) of rows r0 + 32 m
-        const ch::Rsrc rIn0 = ch::rsrc(a.in, (uint64_t)F * n * 4u);
-        const ch::Rsrc rIn1 = ch::rsrc(stereo ? a.in + a.plane : a.in, (uint64_t)F * n * 4u);
-        const uint32_t pc = tid & 7u, r0 = tid >> 3;
-        float4 l[8], r[8];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const uint32_t f = r0 + 32u * (uint32_t)m;
-            const uint32_t off = f < F && 4u * pc < nv ? (f * n + i0 + 4u * pc) * 4u : kOob;
-            l[m] = ch::ld4(rIn0, off);
-            r[m] = stereo ? ch::ld4(rIn1, off) : l[m];
-        }
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            float *dst = mono + 4u * pc * kPd3Row + r0 + 32u * (uint32_t)m;
-            dst[0] = stereo ? (l[m].x + r[m].x) / 2 : l[m].x;
-            dst[kPd3Row] = stereo ? (l[m].y + r[m].y) / 2 : l[m].y;
-            dst[2 * kPd3Row] = stereo ? (l[m].z + r[m].z) / 2 : l[m].z;
-            dst[3 * kPd3Row] = stereo ? (l[m].w + r[m].w) / 2 : l[m].w;
-        }
-    }
-    __syncthreads();
+    const ch::Rsrc rIn0 = ch::rsrc(a.in, (uint64_t)F * n * 4u);
+    const ch::Rsrc rIn1 = ch::rsrc(stereo ? a.in + a.plane : a.in, (uint64_t)F * n * 4u);
+    const uint32_t nv = min(n - i0, 64u);
     const ch::Rsrc rRing = ch::rsrc(a.pre_im + (size_t)i0 * kPreSize, (uint64_t)nv * kPreSize * 4u);
-    {   // 2. wave w: instances 8 w .. 8 w + 7, lane = frame within each 64-frame group
-        float rv[8][4];
-        uint32_t dj[8];
+
+    using Tin1 = olfx::dt::Tap<DT_IN1, 107, 0>;
+    DT_STAGE_X(a, i, olfx::dt::PreFused, (Tin1));
+    dt_prime(t0);
+
+    // cooperative geometry: input rows -- row r = lane / 16 (frame 4c + r), instances 4 (lane % 16)..;
+    // ring lines -- instance 8 m + lane / 8, 16-B group lane % 8
+    const uint32_t rq = lane & 15u, rr = lane >> 4, lj = lane >> 3, lg = lane & 7u;
+    auto load_rows = [&](uint32_t f, float4 &l, float4 &r) {     // frame f of the block, 4 instances
+        const uint32_t off = f < F && 4u * rq < nv ? (f * n + i0 + 4u * rq) * 4u : kOob;
+        l = ch::ld4(rIn0, off);
+        r = stereo ? ch::ld4(rIn1, off) : l;
+    };
+    auto put_rows = [&](float *M, uint32_t fp, const float4 &l, const float4 &r) {   // fp: frame in piece
+        float *dst = M + 4u * rq * kFuS + fp;
+        dst[0] = stereo ? (l.x + r.x) / 2 : l.x;
+        dst[kFuS] = stereo ? (l.y + r.y) / 2 : l.y;
+        dst[2 * kFuS] = stereo ? (l.z + r.z) / 2 : l.z;
+        dst[3 * kFuS] = stereo ? (l.w + r.w) / 2 : l.w;
+    };
+    // window group of the piece starting at T: instance 8 m + lj, positions A + 4 lg (lg < 8), with d
+    // of that instance from its own lane
+    auto win_off = [&](uint32_t T, uint32_t j, uint32_t d, uint32_t g) {
+        const uint32_t A = (T - d) & ~3u;
+        return j < nv ? (j * kPreSize + ((A + 4u * g) & (kPreSize - 1u))) * 4u : kOob;
+    };
+    auto d_of = [&](uint32_t j) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)dpre); };
+    // the piece starting at frame fp0 of the block: its window rows into W (all nine groups) and
+    // its input rows into M -- the prologue's form of what each chunk does for the next piece
+    auto fill_piece = [&](float *M, float *W, uint32_t fp0) {
+        const uint32_t T = t0 + fp0;
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-            const uint32_t j = 8u * w + (uint32_t)jj;
-            dj[jj] = (uint32_t)a.coef[DTC_PREDELAY * n + min(i0 + j, n - 1u)];   // exact integer 0..8191
+        for (uint32_t m = 0; m < 8; ++m) {
+            const uint32_t j = 8u * m + lj;
+            const float4 v = ch::ld4(rRing, win_off(T, j, d_of(j), lg));
+            *(float4 *)(W + j * kFuS + 4u * lg) = v;
+        }
+        const float4 v8 = ch::ld4(rRing, win_off(T, lane, d_of(lane), 8));
+        *(float4 *)(W + lane * kFuS + 32u) = v8;
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const uint32_t f = 64u * (uint32_t)g + lane;
-                const uint32_t off = j < nv && f < F && dj[jj] > f
-                                         ? (j * kPreSize + ((t0 + f - dj[jj]) & (kPreSize - 1u))) * 4u : kOob;
-                rv[jj][g] = ch::ld1(rRing, off, 0);
+        for (uint32_t c = 0; c < 8; ++c) {
+            float4 l, r;
+            load_rows(fp0 + 4u * c + rr, l, r);
+            put_rows(M, 4u * c + rr, l, r);
+        }
+    };
+    fill_piece(fM[0], fW[0], 0);
+    wave_sync();
+
+    const uint32_t pieces = (F + kFuPiece - 1u) / kFuPiece;
+    const ch::Rsrc rOut0 = ch::rsrc(a.out, (uint64_t)F * n * 4u);
+    const ch::Rsrc rOut1 = ch::rsrc(a.out + a.plane, (uint64_t)F * n * 4u);
+    const bool live = i0 + lane < n;
+    for (uint32_t p = 0; p < pieces; ++p) {
+        float *M = fM[p & 1u], *W = fW[p & 1u], *Mn = fM[(p + 1u) & 1u], *Wn = fW[(p + 1u) & 1u];
+        const uint32_t fp0 = p * kFuPiece, T = t0 + fp0, Tn = T + kFuPiece;
+        // 1. this piece's input into the instance-major ring (frames < F only), before any window
+        //    load of the next piece
+#pragma unroll
+        for (uint32_t m = 0; m < 8; ++m) {
+            const uint32_t j = 8u * m + lj;
+            const float4 v = *(const float4 *)(M + j * kFuS + 4u * lg);
+            const uint32_t off = j < nv && fp0 + 4u * lg < F ? (j * kPreSize + ((T + 4u * lg) & (kPreSize - 1u))) * 4u : kOob;
+            ch::st4(rRing, off, v);
+        }
+        // the next piece's 36th-position group, after this piece's ring stores
+        const bool more = fp0 + kFuPiece < F;
+        const float4 w8 = ch::ld4(rRing, more ? win_off(Tn, lane, dpre, 8) : kOob);
+        const uint32_t dfix = dpre, off0 = (T - dfix) & 3u;
+        pre.m = M + jrow * kFuS;
+        pre.w = W + jrow * kFuS;
+        pre.off0 = off0;
+#pragma unroll 1
+        for (uint32_t c = 0; c < 8; ++c) {
+            const uint32_t f0 = fp0 + 4u * c;
+            if (f0 >= F) break;
+            // 2. the next piece's loads: its frames 4c .. 4c + 3 (input rows) and window group m = c
+            float4 nl, nr;
+            load_rows(fp0 + kFuPiece + 4u * c + rr, nl, nr);
+            const uint32_t jw = 8u * c + lj;
+            const float4 nw = ch::ld4(rRing, more ? win_off(Tn, jw, d_of(jw), lg) : kOob);
+            // 3. the chunk: xin from M, the pre-delayed samples from M / W (PreFused)
+            const float4 xv = *(const float4 *)(pre.m + 4u * c);
+            const float xin[4] = {xv.x, xv.y, xv.z, xv.w};
+            pre.fc = (int)(4u * c);
+            float o_l[4], o_r[4];
+            dt_step(t0 + f0, f0 + 4u < F, xin, o_l, o_r);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t off = live ? ((f0 + (uint32_t)k) * n + i0 + lane) * 4u : kOob;
+                ch::st1(rOut0, off, 0, o_l[k]);
+                ch::st1(rOut1, off, 0, o_r[k]);
             }
+            // 4. the next piece's rows into LDS (its buffers: nothing of this piece reads them)
+            put_rows(Mn, 4u * c + rr, nl, nr);
+            *(float4 *)(Wn + jw * kFuS + 4u * lg) = nw;
         }
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-            const uint32_t j = 8u * w + (uint32_t)jj;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const uint32_t f = 64u * (uint32_t)g + lane;
-                outv[j * kPd3Row + f] = dj[jj] <= f ? mono[j * kPd3Row + f - dj[jj]] : rv[jj][g];
-            }
-        }
+        *(float4 *)(Wn + lane * kFuS + 32u) = w8;
+        wave_sync();
     }
-    __syncthreads();
-    {   // 3a. the pre-delayed block: frame groups gs + 8 m, instance j
-        const ch::Rsrc rBlk = ch::rsrc(a.pre_block, (uint64_t)F * n * 4u);
-        const uint32_t j = tid & 31u, gs = tid >> 5;
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const uint32_t g = gs + 8u * (uint32_t)m;
-            const float *src = outv + j * kPd3Row + 4u * g;
-            ch::st4(rBlk, 4u * g < F && j < nv ? (g * n + i0 + j) * 16u : kOob,
-                    make_float4(src[0], src[1], src[2], src[3]));
-        }
-    }
-    {   // 3b. the block's mono input into the ring: wave w's instances, lane = 4-position piece
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-            const uint32_t j = 8u * w + (uint32_t)jj;
-            const float *src = mono + j * kPd3Row + 4u * lane;
-            ch::st4(rRing, 4u * lane < F && j < nv ? (j * kPreSize + ((t0 + 4u * lane) & (kPreSize - 1u))) * 4u : kOob,
-                    make_float4(src[0], src[1], src[2], src[3]));
-        }
-    }
+    if (i0 + lane < n) dt_finish();
 }
 
 // the pre-delay ring between layouts: position-major groups [size/4][n][4] <-> instance-major
@@ -332,7 +377,8 @@ __global__ __launch_bounds__(256) void dattorro_pre_convert(DattorroArgs a, int 
     else *pm = *im;
 }
 
-// v3 when the rows allow it (16-B aligned input rows), else v2
+// 3 = the fused dattorro_block_v4f when the rows allow it (16-B aligned input rows), else 2 =
+// dattorro_predelay_v2 + dattorro_block_v4<true>
 int predelay_kernel(uint32_t n, uint64_t plane, const float *in) {
     return n % 4u == 0u && plane % 4u == 0u && ((uintptr_t)in & 15u) == 0u ? 3 : 2;
 }
@@ -348,13 +394,12 @@ hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s) {
     if (a.pre_im) {
         // per-workgroup ring resources: 64 instances x 32 KB; inputs and the block by 32-bit offsets
         if ((uint64_t)a.n_frames * a.n * 4u >= (1ull << 32)) return hipErrorInvalidValue;
-        const int v = predelay_kernel(a.n, a.plane, a.in);
-        if (v == 3 && a.n_frames > kPd3F) return hipErrorInvalidValue;   // the engine splits at 256
-        if (v == 2)
+        if (predelay_kernel(a.n, a.plane, a.in) == 3) {
+            hipLaunchKernelGGL(dattorro_block_v4f, dim3(blocks), dim3(threads), 0, s, a);   // one launch
+        } else {
             hipLaunchKernelGGL(dattorro_predelay_v2, dim3((a.n + 63) / 64), dim3(64), 0, s, a);
-        else
-            hipLaunchKernelGGL(dattorro_predelay_v3, dim3((a.n + kPd3J - 1) / kPd3J), dim3(256), 0, s, a);
-        hipLaunchKernelGGL(dattorro_block_v4<true>, dim3(blocks), dim3(threads), 0, s, a);
+            hipLaunchKernelGGL(dattorro_block_v4<true>, dim3(blocks), dim3(threads), 0, s, a);
+        }
     } else {
         hipLaunchKernelGGL(dattorro_block_v4<false>, dim3(blocks), dim3(threads), 0, s, a);
     }

@@ -228,7 +228,7 @@ struct PreTap {
     }
 };
 
-// Gather mode (per-instance pre-delays, verb.cpp:137-139): dattorro_predelay_v3 (or v2) has already written
+// Gather mode with unaligned rows (per-instance pre-delays, verb.cpp:137-139): dattorro_predelay_v2 has already written
 // the block's pre-delayed input, group by group, to a.pre_block ([n_frames/4][n][4]: 16 B per lane
 // and chunk, coalesced) and kept the ring itself, instance-major.  The network reads that stream:
 // no gather across lines here, and no ring write.
@@ -251,6 +251,30 @@ struct PreBlock {
         xpd[0] = cur.x; xpd[1] = cur.y; xpd[2] = cur.z; xpd[3] = cur.w;
     }
     __device__ __forceinline__ void advance(const float (&xin)[4]) { (void)xin; cur = pre; }
+    __device__ __forceinline__ void write(const DattorroArgs &, uint32_t, uint32_t, const float (&)[4]) const {}
+};
+
+// Fused gather mode (dattorro_block_v4f, dattorro.hip): the kernel itself keeps, per 32-frame
+// piece, the piece's mono input (M) and each instance's window of its pre-delay ring (W, the 36
+// positions from (T - d) & ~3) in LDS, filled one piece ahead.  Frame t of the piece (t = T + f)
+// reads x[t - d]: from M when t - d >= T (d <= f: this piece's own input), else from W.  The
+// caller points m / w at the lane's rows and sets fc (the chunk's first frame within the piece)
+// and off0 ((T - d) & 3) before each dt_step.
+struct PreFused {
+    const float *m, *w;
+    int fc;
+    uint32_t off0;
+    __device__ __forceinline__ void prime(const DattorroArgs &, uint32_t, uint32_t, uint32_t) {}
+    __device__ __forceinline__ void prefetch(const DattorroArgs &, uint32_t, uint32_t, uint32_t) {}
+    __device__ __forceinline__ void resolve(const float (&)[4], uint32_t d, float (&xpd)[4]) const {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q = fc + k - (int)d;
+            const float *src = q >= 0 ? m + q : w + (off0 + (uint32_t)(fc + k));
+            xpd[k] = *src;
+        }
+    }
+    __device__ __forceinline__ void advance(const float (&)[4]) {}
     __device__ __forceinline__ void write(const DattorroArgs &, uint32_t, uint32_t, const float (&)[4]) const {}
 };
 

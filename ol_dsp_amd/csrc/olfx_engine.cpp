@@ -439,7 +439,7 @@ struct olfx_engine {
     // pre-delay ring and the block's pre-delayed input, allocated on first need
     float *dt_pre_im = nullptr, *dt_pre_blk = nullptr;
     bool dt_gather = false;      // the pre-delay ring's content is instance-major (dt_pre_im)
-    int dt_pre_kernel = 3;       // gather mode's pre-delay pass at the last block (predelay_kernel)
+    int dt_pre_kernel = 3;       // gather mode's kernel at the last block (predelay_kernel: 3 fused v4f, 2 v2 + network)
     bool dt_pre_check = true;    // a pre-delay changed: re-decide the mode at the next block
     float *dt_state = nullptr;
     float *dt_coef = nullptr;
@@ -962,10 +962,7 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, uin
             bool uniform = true;
             for (uint32_t i = 1; i < e->n && uniform; ++i) uniform = dattorro_predelay_samples(pd[i]) == d0;
             if (uniform == e->dt_gather) {
-                if (!e->dt_pre_im) {
-                    HIPCHK(e, hipMalloc((void **)&e->dt_pre_im, (size_t)kDtSize[DT_PRE] * e->n * 4));
-                    HIPCHK(e, hipMalloc((void **)&e->dt_pre_blk, (size_t)256 * e->n * 4));
-                }
+                if (!e->dt_pre_im) HIPCHK(e, hipMalloc((void **)&e->dt_pre_im, (size_t)kDtSize[DT_PRE] * e->n * 4));
                 DattorroArgs ca = dt_args(nullptr, nullptr);
                 ca.pre_im = e->dt_pre_im;
                 // the ring's content into the other layout, on the stream, ahead of this block
@@ -983,8 +980,11 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, uin
             ga.n_frames = std::min(256u, n_frames - f0);
             ga.t0 = (t0 + f0) & 0xFFFFu;
             ga.pre_im = e->dt_pre_im;
-            ga.pre_block = e->dt_pre_blk;
             e->dt_pre_kernel = predelay_kernel(ga.n, ga.plane, ga.in);
+            // the pre-pass's block (v2 + network, unaligned rows only; the fused v4f needs none)
+            if (e->dt_pre_kernel == 2 && !e->dt_pre_blk)
+                HIPCHK(e, hipMalloc((void **)&e->dt_pre_blk, (size_t)256 * e->n * 4));
+            ga.pre_block = e->dt_pre_blk;
             r = launch_dattorro(ga, s);
         }
         break;
@@ -1738,11 +1738,10 @@ double olfx_algorithmic_read_bytes_per_frame(const olfx_engine *e) {
 const char *olfx_kernel_name(const olfx_engine *e) {
     if (!e) return "";
     switch (e->kind) {
-    case OLFX_KIND_DATTORRO:   // gather mode: the pre-delay pass ahead of the network, one launch pair per block
+    case OLFX_KIND_DATTORRO:   // gather mode: the fused network (aligned rows) or the pre-pass + network
         return !e->dt_gather ? "dattorro_block_v4"
-               : e->dt_pre_kernel == 1 ? "dattorro_predelay_v1+dattorro_block_v4"
-               : e->dt_pre_kernel == 2 ? "dattorro_predelay_v2+dattorro_block_v4"
-                                       : "dattorro_predelay_v3+dattorro_block_v4";
+               : e->dt_pre_kernel == 3 ? "dattorro_block_v4f"
+                                       : "dattorro_predelay_v2+dattorro_block_v4";
     case OLFX_KIND_CHORUS:
     case OLFX_KIND_PITCHSHIFT: return "chorus_block_v11";
     case OLFX_KIND_VOICE: return "voice_block_v5";

@@ -81,8 +81,8 @@ struct DattorroArgs {
     uint32_t t0;                // stream time (frames since create) of the first frame, mod 2^16
     uint32_t in_ch;             // 1 or 2
     // gather mode (standalone reverb with per-instance pre-delays, dattorro.hip): the pre-delay
-    // ring instance-major ([n][8192]) and the block's pre-delayed input ([n_frames/4][n][4]),
-    // written by the pre-delay pass (dattorro_predelay_v1/v2/v3) ahead of the block; nullptr otherwise
+    // ring instance-major ([n][8192]); with unaligned audio rows also the block's pre-delayed input
+    // ([n_frames/4][n][4]) written by dattorro_predelay_v2 ahead of the network; nullptr otherwise
     float *pre_im;
     float *pre_block;
 };

@@ -122,7 +122,7 @@ def test_full_size_stream_kinds(cuda, kind, n):
 @pytest.mark.parametrize("pset,kind", [("dattorro_rpd", "dattorro"), ("chain_rpd", "chain")])
 def test_full_size_random_predelay(cuda, pset, kind):
     """The bench's dattorro_rpd / chain_rpd legs at 65,536: a random pre-delay per instance
-    (verb.cpp:137-139), so the standalone reverb runs gather mode (dattorro_predelay_v3 ahead of
+    (verb.cpp:137-139), so the standalone reverb runs gather mode (dattorro_block_v4f, the fused form of
     the network) and the chain its per-lane pre-delay gather.  Two blocks; clones bit-identical,
     sampled instances (workgroup edges included) bit-exact against the oracle."""
     import torch
@@ -133,7 +133,7 @@ def test_full_size_random_predelay(cuda, pset, kind):
     e.set_params(0, p)
     y = _run(e, xs)
     if kind == "dattorro":
-        assert e.kernel_name.startswith("dattorro_predelay_v3")
+        assert e.kernel_name == "dattorro_block_v4f"
     assert torch.isfinite(y).all()
     _check_clones(y, n)
     idx = np.union1d(_sample_idx(n), np.array([30, 32, 34, 96, 65502, 65534], np.int64))

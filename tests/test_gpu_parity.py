@@ -111,7 +111,7 @@ def test_dattorro_per_instance_predelay(cuda):
 
 def test_dattorro_predelay_gather_mode_switches(cuda):
     """The standalone reverb switches its pre-delay ring between the position-major tap (one
-    pre-delay for every instance) and gather mode (per-instance pre-delays: dattorro_predelay_v3,
+    pre-delay for every instance) and gather mode (per-instance pre-delays: dattorro_block_v4f,
     instance-major ring) whenever the pre-delays become equal or differ; the ring's content is
     carried across each switch.  Uniform -> per instance (edges 0..8, 255..257, 4800, past the max)
     -> uniform -> per instance, calls of 256, 4, 1028 (gather mode splits at 256) and 60 frames,
@@ -155,23 +155,27 @@ def test_dattorro_predelay_gather_mode_switches(cuda):
     assert bits_equal(y2, yr2), first_mismatch(y2, yr2)
 
 
-@pytest.mark.parametrize("n,prepass", [(70, "v2"), (72, "v3")])
-def test_dattorro_gather_mode_long_run_wraps(cuda, n, prepass):
+@pytest.mark.parametrize("n,kernel", [(70, "dattorro_predelay_v2+dattorro_block_v4"), (72, "dattorro_block_v4f"),
+                                      (136, "dattorro_block_v4f")])
+def test_dattorro_gather_mode_long_run_wraps(cuda, n, kernel):
     """Gather mode (per-instance pre-delays) over 70,000 frames: the uint16 wrap of t at 65536 and
-    calls that start off v2's 32-frame line grid (60, 3900, 504 frames: first and last chunks
-    partial); pre-delays on the line and chunk edges 0, 1, 31..33, 63..65, 96, 4800 and 8191.
-    70 instances run v2 (rows not 16-B aligned; a partial 64-instance wave), 72 run v3 (a partial
-    32-instance workgroup).  Bit-exact against the oracle."""
+    calls that start off v2's 32-frame line grid and v4f's 32-frame pieces (60, 3900, 504 frames:
+    first and last chunks or pieces partial); pre-delays on the line, piece and window edges 0, 1,
+    31..37, 63..68, 96, 4800 and 8150..8191 (reads of ring slots the launch has not overwritten yet).
+    70 instances run v2 + the network (rows not 16-B aligned; a partial 64-instance wave), 72 and 136
+    the fused v4f (partial waves whose dead lanes mirror the last instance).  Bit-exact against the
+    oracle."""
     rng = np.random.default_rng(85)
     p = dt_params(rng, n, 0.0)
-    edge = np.array([0, 1, 31, 32, 33, 63, 64, 65, 96, 4800, 8191], np.float64) / 4800
+    edge = np.array([0, 1, 31, 32, 33, 35, 36, 37, 63, 64, 65, 67, 68, 96, 4800, 8150, 8160, 8190, 8191],
+                    np.float64) / 4800
     p[0, :] = rng.uniform(0, 1, n).astype(np.float32)
     p[0, :len(edge)] = edge.astype(np.float32)
     x = fast_noise(n, 70000, seed=85)
     e = engine("dattorro", n)
     e.set_params(0, p)
     y = run_gpu(e, x, [60] + [4096] * 16 + [3900, 504], cuda)
-    assert e.kernel_name.startswith("dattorro_predelay_" + prepass)
+    assert e.kernel_name == kernel
     ref = O.Dattorro(n)
     for i in range(n):
         for f in range(7):
