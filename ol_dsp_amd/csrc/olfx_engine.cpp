@@ -409,9 +409,12 @@ struct olfx_engine {
     int n_pending = 0;
     hipStream_t pending_stream = nullptr;
     // the stream of the engine's latest launch (olfx_process / olfx_mix): what reset, sync and
-    // destroy wait for (engine-scoped; the caller keeps that stream alive until then, olfx.h)
+    // destroy wait for (engine-scoped; the caller keeps that stream alive until then, olfx.h).  A
+    // block on another stream is ordered after it through `switched` (recorded on the old stream at
+    // the switch only: an event per block would cost a command-processor packet per block)
     hipStream_t last_stream = nullptr;
     bool have_last = false;
+    hipEvent_t switched = nullptr;
     std::vector<int32_t> ev_slot;         // voice -> its record in `folded` during fold_events, else -1
     struct Folded { uint32_t inst, op, freq, pad; };
     std::vector<Folded> folded;
@@ -1169,6 +1172,7 @@ int olfx_create(int kind, int device, uint32_t n_inst, float sample_rate, uint32
     if (r == hipSuccess) r = hipDeviceGetAttribute(&e->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking);
+    if (r == hipSuccess) r = hipEventCreateWithFlags(&e->switched, hipEventDisableTiming);
     e->each_slot([&](olfx_engine::Slot &x) {
         if (r == hipSuccess) r = hipEventCreateWithFlags(&x.copied, hipEventDisableTiming);
         if (r == hipSuccess) r = hipEventCreateWithFlags(&x.consumed, hipEventDisableTiming);
@@ -1298,6 +1302,7 @@ int olfx_destroy(olfx_engine *e) {
     if (e->d_out) (void)hipFree(e->d_out);
     if (e->mix_dev) (void)hipFree(e->mix_dev);
     if (e->mix_done) (void)hipEventDestroy(e->mix_done);
+    if (e->switched) (void)hipEventDestroy(e->switched);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return OLFX_OK;
@@ -1552,6 +1557,11 @@ int olfx_process(olfx_engine *e, const float *in, float *out, uint32_t n_frames,
     hipStream_t s = (hipStream_t)stream;   // NULL = the HIP default (null) stream
     const size_t fin = (size_t)in_channels(e->kind) * n_frames * e->n;
     const size_t fout = (size_t)out_channels(e->kind) * n_frames * e->n;
+    // a stream switch: this block's work (the control scatter included) after the previous launch
+    if (e->have_last && s != e->last_stream) {
+        HIPCHK(e, hipEventRecord(e->switched, e->last_stream));
+        HIPCHK(e, hipStreamWaitEvent(s, e->switched, 0));
+    }
     int rc = OLFX_OK;
     if (io_flags == OLFX_IO_HOST) {
         rc = ensure_staging(e, fin ? fin : 1, fout);

@@ -346,6 +346,37 @@ def test_chain_controls_slot_reuse_across_streams(cuda, monkeypatch, copy_bytes)
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
 
+def test_stream_switch_is_ordered_by_the_engine(cuda):
+    """Blocks alternating between two caller streams with NO ordering from the caller (no
+    wait_stream, no event): the engine orders each block after the previous one at the switch
+    (olfx.h, olfx_reset's note), so the state carries exactly -- bit-exact against the reference
+    reverb's restatement over 12 blocks of 8,192 instances (a block takes ~0.1 ms, long enough for
+    an unordered successor to overtake it)."""
+    import torch
+    n, blocks = 8192, 12
+    rng = np.random.default_rng(322)
+    p = dt_params(rng, n, 0.02)
+    e = engine("dattorro", n)
+    e.set_params(0, p)
+    ref = O.Dattorro(n)
+    for i in range(n):
+        for f in range(7):
+            ref.set(i, f, float(p[f, i]))
+    x = fast_noise(n, 256 * blocks, seed=322)
+    xd = torch.from_numpy(x).to(cuda)
+    streams = [torch.cuda.Stream(cuda), torch.cuda.Stream(cuda)]
+    torch.cuda.synchronize()
+    outs = []
+    for b in range(blocks):
+        s = streams[b & 1]
+        with torch.cuda.stream(s):
+            outs.append(e.process(xd[:, 256 * b:256 * (b + 1)].contiguous(), stream=s.cuda_stream))
+    torch.cuda.synchronize()
+    y = torch.cat(outs, 1).cpu().numpy()
+    yr = ref.process(x)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
 def test_reset_waits_for_the_engines_own_stream(cuda):
     """olfx_reset waits engine-scoped (the stream of its latest block, not the device): blocks
     queued on a caller stream without a host wait, then reset, then a block on the same stream --
