@@ -278,6 +278,54 @@ struct PreFused {
     __device__ __forceinline__ void write(const DattorroArgs &, uint32_t, uint32_t, const float (&)[4]) const {}
 };
 
+// The fused chain's pre-delay tap (chain.hip, round 5).  The chain keeps its pre-delay ring in ROWS
+// of 16 positions, per workgroup of 64 instances ([n/64][8192/16][64][16]: 64 B per instance and
+// row), so whatever the instances' pre-delays, a 16-frame chunk needs one new row per instance: 64 B
+// that one HBM request serves whole (the position-major groups of PreTap, read at 64 different
+// rows for 64 different delays, cost a 64-B request per 16 B read).  The chain's reverb wave stages
+// in LDS ([slot][lane] float4 columns):
+//   near (slot = group & 7): the inputs of this chunk and the one before (positions T - 16 .. T + 15);
+//   far (slot = group & 15): rows r0 - 1 .. r0 + 2 (r0 = (T - d) >> 4), for the positions before
+//        T - 16.  Row r0 + 2 is loaded during the chunk -- after the chunk's ring store, so it holds
+//        every position before T, all that far serves up to two chunks later -- a group per step
+//        (step m: group m, 16 B of the lane's 64-B row; the row's later groups hit the L2), and
+//        staged one step later over row r0 - 2 (group 3 at the next chunk's first step: group m of
+//        a row r0 + 1 is needed from step m on).  Load at one step, use at
+//        the next: the taps' prefetch pattern, whose waits stay exact inside the step loop (a row
+//        loaded before the loop and used after it cost a vmcnt(0) drain per chunk, +12 %).
+// Groups are 4-aligned and T % 4 == 0, so a group lies wholly in near or in far.
+struct PreRow {
+    const float4 *near, *far;   // this lane's columns: near[slot * 64], far[slot * 64]
+    float4 *farw;               // = far (written)
+    __amdgpu_buffer_rsrc_t rs;  // the workgroup's rows
+    uint32_t lane, T;           // T: the chunk's first position
+    int fc;                     // the step's first frame within the chunk (0, 4, 8, 12)
+    float4 pv;                  // the group loaded at the step before, for farw[pslot]
+    uint32_t pslot;
+    __device__ __forceinline__ void prime(const DattorroArgs &, uint32_t, uint32_t, uint32_t) {}
+    // step m of the chunk: stage the group loaded at the step before, then load group m of this
+    // lane's row r0 + 2
+    __device__ __forceinline__ void prefetch(const DattorroArgs &, uint32_t, uint32_t d, uint32_t) {
+        farw[pslot] = pv;
+        const uint32_t m = (uint32_t)fc >> 2, row = ((T - d) >> 4) + 2u;
+        const uint32_t off = ((row & (kDtSize[DT_PRE] / 16u - 1u)) * 64u + lane) * 64u + m * 16u;
+        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+        const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        pv = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+        pslot = ((row & 3u) * 4u + m) * 64u;
+    }
+    __device__ __forceinline__ void resolve(const float (&)[4], uint32_t d, float (&xpd)[4]) const {
+        const uint32_t s = (0u - d) & 3u;            // (T + fc - d) & 3
+        const int nr = fc - (int)(d + s);             // 4 x (first group - T / 4)
+        const uint32_t g0 = (T + (uint32_t)fc - d) >> 2;
+        const float4 *pa = nr >= -16 ? near + (g0 & 7u) * 64u : far + (g0 & 15u) * 64u;
+        const float4 *pb = nr >= -20 ? near + ((g0 + 1u) & 7u) * 64u : far + ((g0 + 1u) & 15u) * 64u;
+        shift4(s, *pa, *pb, xpd);                     // (s == 0: the second group is unused)
+    }
+    __device__ __forceinline__ void advance(const float (&)[4]) {}
+    __device__ __forceinline__ void write(const DattorroArgs &, uint32_t, uint32_t, const float (&)[4]) const {}
+};
+
 // The body of one 4-frame chunk (verb.cpp:273-299, 302-325).  Taps come by reference, so after
 // inlining every access is to the caller's locals.
 #define DT_ALL_TAPS(OP) OP(in0) OP(in1) OP(in2) OP(in3) OP(fbA) OP(fbB) OP(dl1a) OP(dl1b) OP(ap2a) OP(ap2b) \

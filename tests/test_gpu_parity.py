@@ -943,13 +943,16 @@ def _chain_oracle_set(c1, c2, d, n, pc, pp, pd):
 def test_chain_predelays_long_run_and_param_change(cuda):
     """The fused chain over 70,000 frames (the reverb's uint16 t passes the t = 32,768 modulation
     turn and wraps, the chorus and pitch rings wrap many times), per-instance pre-delays on both
-    sides of the register-history limit (0..12), the block edges and the maximum, a ragged
-    instance count (two groups, the second partial) and every parameter changed at frame 35,000:
-    bit-exact against the composed oracle."""
+    sides of the chunk and row edges of the row-layout ring (0..20, 28..33, 47, 48: a window partly
+    in the chunk's own input), the block edges, the maximum and past it (8176..8191 read positions
+    the launch has not yet overwritten; 8192 acts as 0), chunks starting off a row (blocks of 4 and
+    132 frames shift t0 by 4 and 8 mod 16), a ragged instance count (two groups, the second
+    partial) and every parameter changed at frame 35,000: bit-exact against the composed oracle."""
     n = 100
     rng = np.random.default_rng(41)
     pc, pp, pd = chorus_params(rng, n), chorus_params(rng, n)[[0, 7]], dt_params(rng, n, 0.0)
-    edge = np.array([0, 1, 3, 4, 7, 8, 9, 12, 13, 255, 256, 257, 4799, 4800], np.float32) / 4800
+    edge = np.array([0, 1, 3, 4, 7, 8, 9, 12, 13, 15, 16, 17, 19, 20, 28, 31, 32, 33, 47, 48, 255, 256, 257,
+                     4799, 4800, 8176, 8177, 8180, 8190, 8191, 8192, 8200], np.float64) / 4800
     pd[0] = rng.uniform(0, 1, n)
     pd[0, 64:64 + len(edge)] = edge
     pd[0, :8] = edge[:8]
