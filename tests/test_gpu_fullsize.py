@@ -123,7 +123,7 @@ def test_full_size_stream_kinds(cuda, kind, n):
 def test_full_size_random_predelay(cuda, pset, kind):
     """The bench's dattorro_rpd / chain_rpd legs at 65,536: a random pre-delay per instance
     (verb.cpp:137-139), so the standalone reverb runs gather mode (dattorro_block_v4f, the fused form of
-    the network) and the chain its per-lane pre-delay gather.  Two blocks; clones bit-identical,
+    the network) and the chain its pre-delay rows (dt::PreRow).  Two blocks; clones bit-identical,
     sampled instances (workgroup edges included) bit-exact against the oracle."""
     import torch
     n = 65536
