@@ -182,25 +182,26 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) 
         // store m of lane l is group l & 3 of instance 16 m + l / 4, one 1-KB run per row
         float4 *pre_far = (float4 *)(flags + kFlags), *pre_near = pre_far + 17 * 64;
         const uint32_t cj = lane >> 2, cg = lane & 3u;
-        constexpr uint32_t kRows = kDtSize[DT_PRE] / 16u;           // rows of a workgroup's region
+        constexpr uint32_t kRows = kDtSize[DT_PRE] / 16u;           // rows of the ring
+        const uint32_t nd = a.d.n;
         for (uint32_t g = blockIdx.x, gi = 0; g < ngroups; g += gridDim.x, ++gi) {
             const uint32_t i = g * 64u + lane, gc0 = gi * nchunks;   // < d.n (padded to 64)
             DT_STAGE_PRE(a.d, i, olfx::dt::PreRow);
             const uint32_t t0 = a.d.t0;
             dt_prime(t0);
-            float4 *const ring_g = (float4 *)a.d.ring[DT_PRE] + (size_t)g * kRows * 64u * 4u;
+            float4 *const ring_g = (float4 *)a.d.ring[DT_PRE] + (size_t)g * 64u * 4u;   // row r: + r * nd * 4
             uint32_t dj[4];                                   // the pre-delay of instance 16 m + l / 4
 #pragma unroll
             for (int m = 0; m < 4; ++m) dj[m] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((16u * m + cj) << 2), (int)dpre);
             pre.near = pre_near + lane;
             pre.far = pre_far + lane;
             pre.farw = pre_far + lane;
-            pre.rs = __builtin_amdgcn_make_buffer_rsrc(ring_g, (short)0, (int)(kRows * 64u * 64u), 0x00020000);
-            pre.lane = lane;
+            pre.ring = ring_g + lane * 4u;
+            pre.nd = nd;
             pre.pv = make_float4(0.f, 0.f, 0.f, 0.f);
             pre.pslot = 16u * 64u;                            // junk: nothing loaded yet
             // group cg of row ((T - d) >> 4) + plus of instance 16 m + cj, and its far slot
-            auto row_ptr = [&](uint32_t row, int m) { return ring_g + ((row & (kRows - 1u)) * 64u + 16u * m + cj) * 4u + cg; };
+            auto row_ptr = [&](uint32_t row, int m) { return ring_g + ((size_t)(row & (kRows - 1u)) * nd + 16u * m + cj) * 4u + cg; };
             auto put_row = [&](uint32_t T, uint32_t plus, int m) {
                 const uint32_t row = ((T - dj[m]) >> 4) + plus;
                 pre_far[((row & 3u) * 4u + cg) * 64u + 16u * m + cj] = *row_ptr(row, m);
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) 
             // group cg of the positions T .. T + 15 of instance 16 m + cj in the ring, and in near
             auto ring_at = [&](uint32_t T, int m) {
                 const uint32_t P = T + 4u * cg;
-                return ring_g + (((P >> 4) & (kRows - 1u)) * 64u + 16u * m + cj) * 4u + ((P >> 2) & 3u);
+                return ring_g + ((size_t)((P >> 4) & (kRows - 1u)) * nd + 16u * m + cj) * 4u + ((P >> 2) & 3u);
             };
             auto near_at = [&](uint32_t T, int m) { return pre_near + (((T >> 2) + cg) & 7u) * 64u + 16u * m + cj; };
             // the first chunk's rows r0, r0 + 1 and the chunk before it (the rest: PreRow, per chunk)

@@ -279,8 +279,8 @@ struct PreFused {
 };
 
 // The fused chain's pre-delay tap (chain.hip, round 5).  The chain keeps its pre-delay ring in ROWS
-// of 16 positions, per workgroup of 64 instances ([n/64][8192/16][64][16]: 64 B per instance and
-// row), so whatever the instances' pre-delays, a 16-frame chunk needs one new row per instance: 64 B
+// of 16 positions ([8192/16][n][16]: 64 B per instance and row, a workgroup's 64 rows one 4-KB
+// run), so whatever the instances' pre-delays, a 16-frame chunk needs one new row per instance: 64 B
 // that one HBM request serves whole (the position-major groups of PreTap, read at 64 different
 // rows for 64 different delays, cost a 64-B request per 16 B read).  The chain's reverb wave stages
 // in LDS ([slot][lane] float4 columns):
@@ -297,8 +297,8 @@ struct PreFused {
 struct PreRow {
     const float4 *near, *far;   // this lane's columns: near[slot * 64], far[slot * 64]
     float4 *farw;               // = far (written)
-    __amdgpu_buffer_rsrc_t rs;  // the workgroup's rows
-    uint32_t lane, T;           // T: the chunk's first position
+    const float4 *ring;         // group 0 of row 0 of this lane's instance
+    uint32_t nd, T;             // nd: instances of the ring (a multiple of 64); T: the chunk's first position
     int fc;                     // the step's first frame within the chunk (0, 4, 8, 12)
     float4 pv;                  // the group loaded at the step before, for farw[pslot]
     uint32_t pslot;
@@ -308,10 +308,7 @@ struct PreRow {
     __device__ __forceinline__ void prefetch(const DattorroArgs &, uint32_t, uint32_t d, uint32_t) {
         farw[pslot] = pv;
         const uint32_t m = (uint32_t)fc >> 2, row = ((T - d) >> 4) + 2u;
-        const uint32_t off = ((row & (kDtSize[DT_PRE] / 16u - 1u)) * 64u + lane) * 64u + m * 16u;
-        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-        const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-        pv = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+        pv = ring[(size_t)(row & (kDtSize[DT_PRE] / 16u - 1u)) * nd * 4u + m];
         pslot = ((row & 3u) * 4u + m) * 64u;
     }
     __device__ __forceinline__ void resolve(const float (&)[4], uint32_t d, float (&xpd)[4]) const {
