@@ -17,9 +17,11 @@ for k in sorted(avg):
     print(f"{k:36s} {avg[k]:16.1f}")
 g = avg.get("GRBM_GUI_ACTIVE")
 if g:
+    # GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles (≈ 8 x the kernel's cycles); the _sum counters sum
+    # 256 per-CU units: the average unit's busy fraction is (sum / 256) / (GRBM / 8)
     for k in ("TA_TA_BUSY_sum", "TD_TD_BUSY_sum", "TCP_PENDING_STALL_CYCLES_sum", "TA_ADDR_STALLED_BY_TC_CYCLES_sum"):
         if k in avg:
-            print(f"{k} / GRBM_GUI_ACTIVE = {avg[k] / g:.1f}  (per-unit count ~256 CUs)")
+            print(f"{k} / GRBM_GUI_ACTIVE = {avg[k] / g:.1f}  -> per-CU unit busy fraction {avg[k] / g * 8 / 256:.2f}")
 if "SQ_WAVE_CYCLES" in avg:
     wc = avg["SQ_WAVE_CYCLES"]
     for k in ("SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_VMEM", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY"):
