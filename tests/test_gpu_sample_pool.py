@@ -1,0 +1,83 @@
+"""The per-sample pool's depth (include/olfx_sample.h) for the object kinds other than the reverb
+(tests/test_dattorro_compat.py covers the verb.h names): the README's ChorusEffect shape and the
+fxlib rack, driven instance-major -- each object over a whole host buffer in turn, the per-plugin
+processBlock shape of modules/juce/host/host.cpp:682 -- with the depth the header gives for the
+buffer (buffer / block, or ceil(buffer / block) + 1 off the block grid).  Bit-exact against
+the oracle delayed by the documented latency D x block, a parameter change landing at the
+object's own next block boundary.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle as O
+import ol_dsp_amd as ofx
+from ol_dsp_amd import _lib
+from helpers import bits_equal, chorus_params, first_mismatch, fxrack_params
+
+pytestmark = pytest.mark.gpu
+
+
+def _objects(lib, kind, n, p):
+    objs = []
+    for i in range(n):
+        h = ctypes.c_void_p()
+        assert lib.olfx_sample_create(kind, 48000.0, ctypes.byref(h)) == 0
+        for f in range(p.shape[0]):
+            assert lib.olfx_sample_set_param(h, f, float(p[f, i])) == 0
+        objs.append(h)
+    return objs
+
+
+@pytest.mark.parametrize("kind_name,depth,buf", [("chorus", 2, 512), ("fxrack", 3, 768), ("chorus", 4, 600)])
+def test_sample_pool_instance_major(cuda, kind_name, depth, buf):
+    """3 objects, `buf` frames each per cycle, 4 cycles, instance-major, with the depth the header
+    gives for that buffer: buf / block, or ceil(buf / block) + 1 when the buffer is not a multiple
+    of the block (600 frames: 4)."""
+    lib = ofx.load()
+    B, n, cycles = 256, 3, 4
+    kind = {"chorus": _lib.KIND_CHORUS, "fxrack": _lib.KIND_FXRACK}[kind_name]
+    rng = np.random.default_rng(500 + depth + buf)
+    if kind_name == "chorus":
+        p = chorus_params(rng, n)
+        ref = O.Chorus(n)
+        field, value = 1, 0.9                        # OLFX_CH_MIX
+    else:
+        p = np.concatenate([fxrack_params(rng, n), np.zeros((1, n), np.float32)], 0)
+        ref = O.FxRack(n)
+        field, value = 1, 0.25                       # OLFX_FR_DELAY_FEEDBACK
+    for i in range(n):
+        for f in range(p.shape[0]):
+            ref.set(i, f, float(p[f, i]))
+    assert lib.olfx_sample_pool_config_depth(0, B, depth) == 0
+    try:
+        objs = _objects(lib, kind, n, p)
+        assert lib.olfx_sample_latency(objs[0]) == depth * B
+        T = buf * cycles
+        x = (rng.random((2, T, n), dtype=np.float32) - 0.5).astype(np.float32)
+        y = np.zeros((2, T, n), np.float32)
+        fin, fout = (ctypes.c_float * 2)(), (ctypes.c_float * 2)()
+        t_set = buf                                  # object 2's change before its second buffer
+        for c in range(cycles):
+            for i, h in enumerate(objs):
+                if i == 2 and c * buf == t_set:
+                    assert lib.olfx_sample_set_param(h, field, value) == 0
+                for t in range(c * buf, (c + 1) * buf):
+                    fin[0], fin[1] = float(x[0, t, i]), float(x[1, t, i])
+                    assert lib.olfx_sample_process(h, fin, fout) == 0, (c, i, t)
+                    y[0, t, i], y[1, t, i] = fout[0], fout[1]
+        for h in objs:
+            assert lib.olfx_sample_destroy(h) == 0
+    finally:
+        assert lib.olfx_sample_pool_config(0, B) == 0
+    L = depth * B
+    land = -(-t_set // B) * B                        # object 2's next block boundary at or after it
+    parts = [ref.process(np.ascontiguousarray(x[:, :land]))]
+    ref.set(2, field, value)
+    parts.append(ref.process(np.ascontiguousarray(x[:, land:])))
+    want = np.concatenate(parts, 1)
+    assert not np.any(y[:, :L])
+    got = y[:, L:]
+    assert bits_equal(got, want[:, :T - L]), first_mismatch(got, want[:, :T - L])
+    assert np.any(want != 0)
