@@ -81,3 +81,55 @@ def test_sample_pool_instance_major(cuda, kind_name, depth, buf):
     got = y[:, L:]
     assert bits_equal(got, want[:, :T - L]), first_mismatch(got, want[:, :T - L])
     assert np.any(want != 0)
+
+
+@pytest.mark.parametrize("kind_name", ["voice", "voice_moog"])
+def test_sample_pool_voices_instance_major(cuda, kind_name):
+    """SynthVoice objects through the pool at depth 2, each over a 512-frame buffer in turn: NoteOn
+    before every voice's first frame, voice 1's NoteOff and voice 2's filter cutoff (a member
+    Process reads itself, SynthVoice.h:42-52) before their second buffers.  Bit-identical to one
+    engine given the same configurations and events at the same block boundaries (the pool runs
+    that engine; the voice's numerics are checked against the oracle elsewhere), delayed by 2 blocks."""
+    from test_gpu_parity import _voice_run, engine
+    from helpers import voice_configs
+    lib = ofx.load()
+    B, n, depth, buf, cycles = 256, 3, 2, 512, 3
+    kind = {"voice": _lib.KIND_VOICE, "voice_moog": _lib.KIND_VOICE_MOOG}[kind_name]
+    rng = np.random.default_rng(77 if kind_name == "voice" else 78)
+    cfg = voice_configs(rng, n)
+    notes = [48, 60, 67]
+    assert lib.olfx_sample_pool_config_depth(0, B, depth) == 0
+    try:
+        objs = _objects(lib, kind, n, cfg)
+        T = buf * cycles
+        y = np.zeros((T, n), np.float32)
+        fout = (ctypes.c_float * 1)()
+        for c in range(cycles):
+            for i, h in enumerate(objs):
+                if c == 0:
+                    assert lib.olfx_sample_note(h, 1, notes[i], 100) == 0
+                if c == 1 and i == 1:
+                    assert lib.olfx_sample_note(h, 0, notes[i], 0) == 0
+                if c == 1 and i == 2:
+                    assert lib.olfx_sample_set_param(h, 0, 900.0) == 0     # OLFX_VC_FILTER_CUTOFF
+                for t in range(c * buf, (c + 1) * buf):
+                    assert lib.olfx_sample_process(h, None, fout) == 0, (c, i, t)
+                    y[t, i] = fout[0]
+        for h in objs:
+            assert lib.olfx_sample_destroy(h) == 0
+    finally:
+        assert lib.olfx_sample_pool_config(0, B) == 0
+    e = engine(kind_name, n)
+    e.set_params(0, cfg)
+    e.note_events([(i, 1, notes[i]) for i in range(n)])
+    blocks = []
+    for b in range(T // B):
+        if b * B == buf:
+            e.note_events([(1, 0, notes[1])])
+            e.set_params(0, np.array([[900.0]], np.float32), first=2)
+        blocks.append(_voice_run(e, B, cuda)[0])
+    want = np.concatenate(blocks, 0)
+    L = depth * B
+    assert not np.any(y[:L])
+    assert bits_equal(y[L:], want[:T - L]), first_mismatch(y[L:], want[:T - L])
+    assert np.any(want != 0)
