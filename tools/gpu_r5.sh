@@ -8,11 +8,9 @@
 #   p:<workload>         rocprofv3 kernel stats of that bench line (-> gpurun_out/prof_<w>)
 #   tr:<workload>        HBM traffic passes (tools/traffic_r2.sh)
 #   bench                the driver's default line
-#   ab:<workload>:<k>    A/B: the workload under the default and OLFX_CHORUS_KERNEL=<k>, twice each
 #   tl:<lib>:<k>         GPU tests matching <k> against an experimental build (OLFX_LIB=<lib>)
 #   te:<VAR=v>:<k>       GPU tests matching <k> with the environment variable VAR=v
 #   ts:<k>               GPU tests matching <k>, with their printed output (-s)
-#   vstamp               voice role stamps (build/ab/vcstamp.so, tools/voice_stamps.py) at 32,768 and 16,384
 #   abe:<workload>:<VAR=v> A/B: the workload under the default and VAR=v, three times each
 #   abm:<w1,w2>:<lib1,lib2> A/B of the main build against several libs over several workloads
 #   util:<workload>      utilisation counter passes (tools/pmc_util.sh)
@@ -51,11 +49,6 @@ for m in "$@"; do
       step "pytest_s_$(echo "$k" | tr -c 'a-zA-Z0-9_' '_')" 600 python -u -m pytest tests -m gpu -x -v -s -p no:cacheprovider \
           --timeout 120 --timeout-method thread -k "$k"
       grep -E "rel err|PASSED|FAILED" "$out/pytest_s_$(echo "$k" | tr -c 'a-zA-Z0-9_' '_').log" ;;
-    vstamp)
-      step vstamp_32768 120 env OLFX_LIB=$PWD/build/ab/vcstamp.so python tools/voice_stamps.py 32768
-      cat "$out/vstamp_32768.log"
-      step vstamp_16384 120 env OLFX_LIB=$PWD/build/ab/vcstamp.so python tools/voice_stamps.py 16384
-      cat "$out/vstamp_16384.log" ;;
     abl:*)
       r=${m#abl:}; w=${r%%:*}; lib=${r#*:}
       step "abl_$w" 600 bash tools/ab.sh "$w" main "$lib"
@@ -78,14 +71,6 @@ for m in "$@"; do
     tr:*)
       w=${m#tr:}
       step "traffic_$w" 600 bash tools/traffic_r2.sh "$w" ;;
-    ab:*)
-      r=${m#ab:}; w=${r%%:*}; kv=${r#*:}
-      for r in 1 2; do
-        step "ab_${w}_default_$r" 300 python bench.py --workload "$w" --also "" --steps 50 --warmup 5 \
-            --cpu-seconds 0 --no-parity --full-json ""
-        step "ab_${w}_k${kv}_$r" 300 env OLFX_CHORUS_KERNEL=$kv python bench.py --workload "$w" --also "" --steps 50 --warmup 5 --cpu-seconds 0 \
-            --no-parity --full-json ""
-      done ;;
     abe:*)
       r=${m#abe:}; w=${r%%:*}; kv=${r#*:}
       for r in 1 2 3; do
