@@ -1282,3 +1282,73 @@ def test_polyvoice_allocation_vs_oracle(cuda):
     assert np.all(np.isfinite(y))
     assert rel_err(y[0].T, yr[0].T) <= VOICE_TOL
     assert bits_equal(bus, O.mix_ref(y, groups))
+
+
+# ----------------------------------------------------------------------------- sample rates
+@pytest.mark.parametrize("sr", [44100.0, 96000.0])
+@pytest.mark.parametrize("kind", ["chorus", "pitchshift", "fxrack", "chain"])
+def test_effects_at_other_sample_rates(cuda, kind, sr):
+    """Every effect kind at 44.1 and 96 kHz (the reference's Init(sample_rate): RNBO's ms -> sample
+    conversions and ring sizes, DelayFx's time scale, mono-chorus's cutoff map; the reverb's delays
+    are in samples): bit-exact against the oracle built for the same rate, over ragged blocks."""
+    n = 70
+    rng = np.random.default_rng(int(sr) + len(kind))
+    x = fast_noise(n, 3000, seed=int(sr) % 1000 + len(kind))
+    e = engine(kind, n, sample_rate=sr)
+    if kind in ("chorus", "pitchshift"):
+        p = chorus_params(rng, n)
+        if kind == "pitchshift":
+            p = p[[0, 7]]
+        e.set_params(0, p)
+        ref = O.Chorus(n, sample_rate=sr, mode=0 if kind == "chorus" else 1)
+        for i in range(n):
+            for f in range(p.shape[0]):
+                ref.set(i, f if kind == "chorus" else ("pitch", "window")[f], float(p[f, i]))
+        yr = ref.process(x)
+    elif kind == "fxrack":
+        p = np.concatenate([fxrack_params(rng, n), (np.arange(n) % 5)[None, :].astype(np.float32)], 0)
+        e.set_params(0, p)
+        ref = O.FxRack(n, sample_rate=sr)
+        for i in range(n):
+            for f in range(p.shape[0]):
+                ref.set(i, f, float(p[f, i]))
+        yr = ref.process(x, threads=8)
+    else:
+        pc, pp, pd = chorus_params(rng, n), chorus_params(rng, n)[[0, 7]], dt_params(rng, n, 0.0)
+        pd[0] = rng.uniform(0, 1, n)
+        e.set_params(0, np.concatenate([pc, pp, pd], 0))
+        c1, c2, d = O.Chorus(n, sample_rate=sr), O.Chorus(n, sample_rate=sr, mode=1), O.Dattorro(n)
+        _chain_oracle_set(c1, c2, d, n, pc, pp, pd)
+        yr = d.process(c2.process(c1.process(x)))
+    y = run_gpu(e, x, [256, 4, 60, 1024, 300, 1356], cuda)
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
+@pytest.mark.parametrize("sr", [44100.0, 96000.0])
+@pytest.mark.parametrize("kind", ["voice", "voice_moog"])
+def test_voices_at_other_sample_rates(cuda, rcp_table, kind, sr):
+    """SynthVoice::Init(sample_rate) at 44.1 and 96 kHz (oscillator increment, envelope and
+    portamento rates, the Svf's / ladder's frequency maps): bit-exact against the oracle's
+    kernel-arithmetic mode for the same rate, through a NoteOn and a NoteOff."""
+    n = 64
+    rng = np.random.default_rng(int(sr) + 7)
+    cfg = voice_configs(rng, n)
+    notes = [int(v) for v in rng.integers(36, 97, n)]
+    e = engine(kind, n, sample_rate=sr)
+    ref = O.Voice(n, sample_rate=sr, moog=kind == "voice_moog", kernel_arith=True)
+    e.set_params(0, cfg)
+    for i in range(n):
+        ref.config(i, cfg[:, i])
+    e.note_events([(i, 1, notes[i]) for i in range(n)])
+    for i in range(n):
+        ref.note(i, True, notes[i])
+    ya = np.concatenate([_voice_run(e, 256, cuda) for _ in range(6)], 1)
+    yra = ref.process(1536)
+    e.note_events([(i, 0, notes[i]) for i in range(n)])
+    for i in range(n):
+        ref.note(i, False, notes[i])
+    yb = np.concatenate([_voice_run(e, 256, cuda) for _ in range(6)], 1)
+    yrb = ref.process(1536)
+    y, yr = np.concatenate([ya, yb], 1), np.concatenate([yra, yrb], 1)
+    assert np.any(y != 0)
+    assert voice_bits_equal(y, yr), first_mismatch(y, yr)
