@@ -15,7 +15,8 @@
  *                        Init / UpdateConfig / NoteOn / NoteOff / Process.
  *
  * and, one object per reference object (include/olfx_sample.h: per-sample calls batched into one
- * GPU block per generation, one block of latency, frame-major calls):
+ * GPU block per generation; D blocks of latency and any call order within D blocks, D = the pool
+ * depth, 1 by default: frame-major calls):
  *   olfx::ChorusEffect <- ChorusEffect (README.md:114-128): init / setDepth / setRate / process(float)
  *   olfx::SynthVoice   <- ol::synth::SynthVoice (SynthVoice.h:31-256): Init / UpdateConfig / NoteOn /
  *                         NoteOff / UpdateMidiControl / UpdateHardwareControl / Process(frame_out)
@@ -241,8 +242,9 @@ private:
 /* ------------------------------------------------------------------------------------------
  * Per-instance, per-sample operators: the reference's objects one for one.  The k-th Process /
  * process call returns the reference's output of frame k - latency() (zeros before); setters,
- * notes and controls land at the next block boundary.  Calls must be frame-major across the
- * instances of a generation (include/olfx_sample.h); a violation throws OLFX_E_STATE.
+ * notes and controls land at the next block boundary.  No instance of a generation may run the
+ * pool depth D (1 by default: frame-major calls) blocks ahead of the slowest one
+ * (include/olfx_sample.h); a violation throws OLFX_E_STATE.
  * ------------------------------------------------------------------------------------------ */
 class SampleOperator {
 public:
