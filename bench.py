@@ -14,6 +14,12 @@ and input stream from its global index (ol_dsp_amd.workload), so an N-GPU run pr
 the instances a one-GPU run of the same total would.  No data-path collective (weak scaling); one
 RCCL all-reduce after each timed region gathers the counters.
 
+Repetitions ("median of 5"): every leg is built first and kept alive; then each leg
+runs --reps timed regions of exactly --steps steps (barrier + device sync on both sides, max over
+ranks), the leg order rotated by one leg per repetition, after at least --leg-warmup untimed steps
+before a leg's first region and --rep-warmup before each later one.  Every reported time is the
+median region, with the min-max range beside it.
+
 Prints ONE compact JSON line (rank 0; the whole record, every leg in full, goes to --full-json):
   roofline     : algorithmic bytes of the dominant kernel / its HIP-event-timed duration vs 8 TB/s
                  (frac = read+write, frac_read = the read share: the north star's HBM-read roofline)
@@ -92,8 +98,14 @@ def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
                     help="ranks (one per GPU); without torchrun, N > 1 launches the N rank processes itself")
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=200, help="steps (blocks) in each timed region")
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=5,
+                    help="timed regions per leg (SURVEY 8d: median of 5), leg order rotated between them")
+    ap.add_argument("--leg-warmup", type=int, default=50,
+                    help="untimed steps before a leg's first region at least (the sustained clock: "
+                         "profiles/r5/chorus_launch_durations.txt)")
+    ap.add_argument("--rep-warmup", type=int, default=10, help="untimed steps before each later region of a leg")
     ap.add_argument("--workload", default="chorus", choices=sorted(WORKLOADS))
     ap.add_argument("--instances", type=int, default=0, help="instances per GPU (0 = workload default)")
     ap.add_argument("--also", default=None,
@@ -287,7 +299,7 @@ def sample_instances(n: int) -> np.ndarray:
 
 def parity_check(job: dict, sr: float) -> dict:
     """Replay the leg's W+K blocks for the sampled instances on the CPU oracle and compare the
-    last block with what the GPU produced (job filled in by run_workload)."""
+    last block with what the GPU produced (job filled in by Leg.finish)."""
     kind, idx, B = job["kind"], job["idx"], job["block"]
     m = len(idx)
     voice = kind in VOICE_KINDS
@@ -387,276 +399,358 @@ def _traffic(name: str, n: int, B: int, override: str = "", kernel: str = ""):
     return None
 
 
-def run_stub(name: str, n_per_gpu: int, args, rank: int, world: int) -> dict:
-    """--stub: the launcher's CPU check.  No engine and no GPU: each rank 'processes' its shard for
-    K steps (a host sleep per step), then the same single all-reduce as a real leg (gloo)."""
-    from ol_dsp_amd.dist import RunStats, reduce_stats, shard
-    total = n_per_gpu * world
-    first, n = shard(total, world, rank)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        time.sleep(0.001)
-    elapsed = time.perf_counter() - t0
-    st = reduce_stats(RunStats(elapsed, elapsed * 1e3 / args.steps, float(n) * args.block * args.steps,
-                               float(first), 1.0))
-    if rank != 0:
-        return {}
-    return {"metric": METRIC, "value": st.frames / st.elapsed_s, "unit": "stereo samples/s",
-            "ms_per_step": st.elapsed_s / args.steps * 1e3, "frames": st.frames, "ranks_reporting": int(st.ranks),
-            "config": {"workload": name, "instances_per_gpu": n_per_gpu, "instances_total": total,
-                       "block": args.block, "parallelism": f"instance-shard x{world} (stub: no GPU)"},
-            "roofline": None, "cpu_baseline": None, "output_checksum": st.checksum, "output_nonfinite_rank0": 0}
+class StubLeg:
+    """--stub: the launcher's CPU check.  No engine and no GPU: each rank 'processes' its shard (a
+    host sleep per step) through the same repetition, rotation and per-region all-reduce (gloo) as a
+    real leg."""
+
+    def __init__(self, name: str, n_per_gpu: int, args, rank: int, world: int):
+        from ol_dsp_amd.dist import shard
+        self.name, self.n_per_gpu, self.args, self.rank, self.world = name, n_per_gpu, args, rank, world
+        self.total = n_per_gpu * world
+        self.first, self.n = shard(self.total, world, rank)
+        self.reps = []
+
+    def warm(self, steps: int) -> None:
+        time.sleep(0.001 * steps)
+
+    def timed(self, steps: int) -> None:
+        from ol_dsp_amd.dist import RunStats, reduce_stats
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            time.sleep(0.001)
+        elapsed = time.perf_counter() - t0
+        if dist.is_initialized():
+            dist.barrier()
+        self.reps.append(reduce_stats(RunStats(elapsed, elapsed * 1e3 / steps, float(self.n) * self.args.block * steps,
+                                               0.0, 1.0)))
+
+    def finish(self) -> dict:
+        from ol_dsp_amd.dist import RunStats, reduce_stats
+        st = reduce_stats(RunStats(0.0, 0.0, 0.0, float(self.first), 1.0))   # the shard starts: distinct shards
+        if self.rank != 0:
+            return {}
+        res = _rep_summary(self.reps, self.args.steps)
+        res.update({"metric": METRIC, "unit": "stereo samples/s", "output_checksum": st.checksum,
+                    "config": {"workload": self.name, "instances_per_gpu": self.n_per_gpu, "instances_total": self.total,
+                               "block": self.args.block, "parallelism": f"instance-shard x{self.world} (stub: no GPU)"},
+                    "roofline": None, "cpu_baseline": None, "parity": None, "output_nonfinite_rank0": 0})
+        return res
 
 
-def run_workload(name: str, n_per_gpu: int, args, rank: int, world: int, dev, with_cpu: bool) -> dict:
-    import torch
+def _median(v):
+    s = sorted(v)
+    m = len(s)
+    return s[m // 2] if m % 2 else 0.5 * (s[m // 2 - 1] + s[m // 2])
 
-    import ol_dsp_amd as ofx
-    from ol_dsp_amd.dist import RunStats, reduce_stats, shard
-    from ol_dsp_amd.workload import instance_params, noise_torch, voice_notes
 
-    kind, _, desc = WORKLOADS[name]
-    total = n_per_gpu * world
-    first, n = shard(total, world, rank)
-    B = args.block
-    eng = ofx.Engine(kind, n, sample_rate=args.sample_rate, block=B, device=dev.index or 0)
-    pset = PARAM_SET.get(name, kind)
-    params = instance_params(pset, first, n)
-    eng.set_params(0, params)
-    ich, och = eng.info.in_channels, eng.info.out_channels
+def _rep_summary(reps, steps: int) -> dict:
+    """The leg's repetitions (each a barrier-bracketed region of `steps` steps, max over ranks):
+    value and ms_per_step from the median region, the kernel time median, the min-max spread."""
+    el = [r.elapsed_s for r in reps]
+    km = [r.kernel_ms for r in reps]
+    frames = reps[0].frames                     # per region, summed over ranks
+    e_med, k_med = _median(el), _median(km)
+    return {"value": frames / e_med, "ms_per_step": e_med / steps * 1e3, "frames": frames,
+            "ranks_reporting": int(reps[0].ranks), "kernel_ms_median": k_med,
+            "reps": {"n": len(reps), "steps_each": steps, "kernel_ms": km, "elapsed_s": el,
+                     "kernel_ms_min": min(km), "kernel_ms_max": max(km),
+                     "kernel_spread": (max(km) - min(km)) / k_med if k_med > 0 else None}}
 
-    # input pool: distinct synthetic blocks of each global instance's own stream, on the device
-    blk_bytes = max(ich, 1) * B * n * 4
-    pool_n = max(2, int(args.pool_bytes // blk_bytes)) if ich else 1
-    pool = noise_torch(first, n, B, ich, dev, blocks=pool_n) if ich else [None]
-    out = torch.empty((och, B, n), device=dev)
-    voice = kind in VOICE_KINDS
-    notes = voice_notes(first, n)
-    note_off = None
-    if voice:   # NoteOn for every voice at block 0, NoteOff at the middle of the timed blocks (SURVEY 8d)
-        eng.note_events(eng.make_events(np.arange(n), 1, notes))
-        note_off = eng.make_events(np.arange(n), 0, notes)
-    # control legs: the per-step calls are prebuilt (untimed), so a step is the library call only
-    gi = np.arange(first, first + n)
-    step_events = None
-    if name == "voice_events":     # voices i % 40 == k % 40 get NoteOn, i % 40 == (k + 20) % 40 NoteOff
-        step_events = []
-        for k in range(40):
-            on = np.nonzero(gi % 40 == k)[0]
-            off = np.nonzero(gi % 40 == (k + 20) % 40)[0]
-            ev_on = eng.make_events(on, 1, (notes[on] + 12 * (k & 1)) % 128)
-            ev_off = eng.make_events(off, 0, notes[off])
-            step_events.append(np.concatenate([ev_on, ev_off]))
-    step_ccs = None
-    if name == "chain_cc":         # chains i % 100 == k % 100 get a new value of one field per step
-        from ol_dsp_amd.workload import uniform01
-        fields = [("chorus_depth", .08, 1.0), ("chorus_mix", 0.0, 1.0), ("verb_decay", .25, .95),
-                  ("verb_damping", .05, .95), ("pitch_shift", 0.0, 3.0)]
-        step_ccs = []
-        for k in range(100):
-            sel = np.nonzero(gi % 100 == k)[0].astype(np.uint32)
-            fname, lo, hi = fields[k % len(fields)]
-            vals = (lo + (hi - lo) * uniform01(7, k, int(first), n)[sel]).astype(np.float32)
-            step_ccs.append((eng.field(fname), sel, vals))
-    bus = None
-    if name == "voice_poly":       # Polyvoice buses of 8 voices (Polyvoice.h:28-33)
-        bus_lists = [list(range(g, min(g + 8, n))) for g in range(0, n, 8)]
-        eng.mix_config(bus_lists)
-        bus = torch.zeros((B, eng.n_buses), device=dev)
-    stream = torch.cuda.Stream(dev)        # dedicated non-default stream: events see the kernels
-    torch.cuda.synchronize(dev)
-    K, W = args.steps, args.warmup
-    # Kernel timing: ONE event pair on the launch stream around the K timed steps: GPU time per
-    # step = the kernel's average launch duration plus the gap between launches.  (A pair per step
-    # adds two timestamp markers between consecutive kernels -- ~3-4 us each on the command
-    # processor, 10-20 % of a 35 us voice block, measured: tools/loop_probe.py.)  voice_poly's
-    # steps run two kernels: its mix is timed alone after the timed region (one pair around K mix
-    # launches), and the voice kernel's time is the step time less that.
-    region = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
 
-    # The timed loop calls the C-ABI directly with prebuilt arguments (Engine.process's checks and
-    # tensor handling cost ~20 us of Python per call, more than a voice block's kernel): the host
-    # must stay ahead of the GPU, or the event pairs below would time the host's launch latency.
-    import ctypes
+class Leg:
+    """One workload on this rank's GPU: its engine, input pool and prebuilt per-step calls, kept
+    alive across the repetitions so that main() can interleave the legs.  `warm(W)` runs W untimed
+    steps; `timed(K)` one region of exactly K steps bracketed by a barrier and a device sync on both
+    sides (max over ranks, one all-reduce after it); `finish()` the untimed checks and the result.
+    Steps are numbered over the whole run (inputs from the pool, event / control schedules, the
+    voices' NoteOff at the middle block), so the parity replay follows every block the engine ran."""
 
-    from ol_dsp_amd import _lib
-    lib, h = eng.lib, eng.handle
-    c_stream = ctypes.c_void_p(stream.cuda_stream)
-    c_out = ctypes.c_void_p(out.data_ptr())
-    proc_args = [(h, ctypes.c_void_p(p.data_ptr() if p is not None else 0), c_out, B, _lib.IO_DEVICE, c_stream)
-                 for p in pool]
-    ev_args = [(h, e_.ctypes.data_as(ctypes.POINTER(_lib.Event)), len(e_)) for e_ in step_events or []]
-    cc_args = [(h, f, sel.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
-                vals.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), len(sel)) for f, sel, vals in step_ccs or []]
+    def __init__(self, name: str, n_per_gpu: int, args, rank: int, world: int, dev, with_cpu: bool,
+                 total_blocks: int):
+        import torch
 
-    def step(k, t=None):
-        rc = 0
-        if voice and k == W + K // 2:
-            eng.note_events(note_off)
-        if ev_args:
-            rc |= lib.olfx_note_events(*ev_args[k % 40])
-        if cc_args:
-            rc |= lib.olfx_set_param_list(*cc_args[k % 100])
-        rc |= lib.olfx_process(*proc_args[k % pool_n])
-        if rc:
-            _lib.check(rc, h)
-        if bus is not None:
-            eng.mix(out, bus, stream=stream.cuda_stream)
+        import ol_dsp_amd as ofx
+        from ol_dsp_amd.dist import shard
+        from ol_dsp_amd.workload import instance_params, noise_torch, voice_notes
 
-    for k in range(W):
-        step(k)
-    torch.cuda.synchronize(dev)
-    if torch.distributed.is_initialized():
-        torch.distributed.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    region[0].record(stream)
-    for k in range(K):
-        step(W + k, k)
-    region[1].record(stream)
-    torch.cuda.synchronize(dev)
-    if torch.distributed.is_initialized():
-        torch.distributed.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    kern_ms = region[0].elapsed_time(region[1]) / K
-    mix_ms = None
+        self.name, self.args, self.rank, self.world, self.dev = name, args, rank, world, dev
+        self.with_cpu = with_cpu
+        kind, _, desc = WORKLOADS[name]
+        self.kind, self.desc, self.n_per_gpu = kind, desc, n_per_gpu
+        self.total = n_per_gpu * world
+        first, n = shard(self.total, world, rank)
+        self.first, self.n = first, n
+        B = self.B = args.block
+        eng = self.eng = ofx.Engine(kind, n, sample_rate=args.sample_rate, block=B, device=dev.index or 0)
+        self.pset = PARAM_SET.get(name, kind)
+        params = self.params = instance_params(self.pset, first, n)
+        eng.set_params(0, params)
+        ich, och = eng.info.in_channels, eng.info.out_channels
+        self.ich = ich
 
-    # sum |y| over the finite outputs of the last block (a voice whose Svf diverges -- possible in
-    # the reference DaisySP arithmetic at high cutoff, low resonance and high drive -- yields
-    # inf/NaN there too; DESIGN.md section 5); the count of non-finite samples beside it
-    finite = torch.isfinite(out)
-    nonfinite = int((~finite).sum().item())
-    checksum = float(torch.where(finite, out.abs(), torch.zeros_like(out)).sum().item())
-    bus_sum = float(bus.abs().sum().item()) if bus is not None else None
-    if bus is not None:            # the mix alone, K launches between one event pair (untimed for value)
-        scratch = torch.zeros_like(bus)
-        for _ in range(W):
-            eng.mix(out, scratch, stream=stream.cuda_stream)
-        mreg = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        mreg[0].record(stream)
-        for _ in range(K):
-            eng.mix(out, scratch, stream=stream.cuda_stream)
-        mreg[1].record(stream)
-        torch.cuda.synchronize(dev)
-        mix_ms = mreg[0].elapsed_time(mreg[1]) / K
-        kern_ms = max(kern_ms - mix_ms, 1e-6)
-
-    # untimed parity material: the last timed block of sampled instances, the pool blocks they read
-    # (read back from the device: exactly the timed inputs) and the leg's event / control schedule
-    parity_job = None
-    if rank == 0 and not args.no_parity:
-        if bus is not None:        # two whole buses (first, last) so the mix can be checked too
-            nb = len(bus_lists)
-            idx = np.array(sorted(set(bus_lists[0]) | set(bus_lists[nb - 1])), np.int64)
-        else:
-            idx = sample_instances(n)
-        ti = torch.from_numpy(idx).to(dev)
-        parity_job = {"kind": kind, "idx": idx, "block": B, "blocks": W + K,
-                      "params": np.ascontiguousarray(params[:, idx]),
-                      "gpu": out.index_select(2, ti).cpu().numpy()}
-        if ich:
-            parity_job["pool"] = [np.ascontiguousarray(p.index_select(2, ti).cpu().numpy()) for p in pool]
-            parity_job["pool_n"] = pool_n
-        if voice:
-            parity_job["notes"] = notes[idx].astype(np.int64)
-            parity_job["note_off_block"] = W + K // 2
-        if step_events is not None:
-            pos = {int(i): j for j, i in enumerate(idx)}
-            sched = []
+        # input pool: distinct synthetic blocks of each global instance's own stream, on the device
+        blk_bytes = max(ich, 1) * B * n * 4
+        self.pool_n = pool_n = max(2, int(args.pool_bytes // blk_bytes)) if ich else 1
+        self.pool = noise_torch(first, n, B, ich, dev, blocks=pool_n) if ich else [None]
+        self.out = torch.empty((och, B, n), device=dev)
+        self.voice = voice = kind in VOICE_KINDS
+        self.notes = notes = voice_notes(first, n)
+        self.note_off = None
+        self.note_off_block = total_blocks // 2
+        if voice:   # NoteOn for every voice at block 0, NoteOff at the middle block of the run (SURVEY 8d)
+            eng.note_events(eng.make_events(np.arange(n), 1, notes))
+            self.note_off = eng.make_events(np.arange(n), 0, notes)
+        # control legs: the per-step calls are prebuilt (untimed), so a step is the library call only
+        gi = self.gi = np.arange(first, first + n)
+        self.step_events = None
+        if name == "voice_events":     # voices i % 40 == k % 40 get NoteOn, i % 40 == (k + 20) % 40 NoteOff
+            self.step_events = []
             for k in range(40):
-                on = [(pos[int(i)], True, int((notes[i] + 12 * (k & 1)) % 128)) for i in idx if gi[i] % 40 == k]
-                off = [(pos[int(i)], False, int(notes[i])) for i in idx if gi[i] % 40 == (k + 20) % 40]
-                sched.append(on + off)
-            parity_job["events"] = lambda b, s=sched: s[b % 40]
-        if step_ccs is not None:
-            pos = {int(i): j for j, i in enumerate(idx)}
-            sched = []
-            for f, sel, vals in step_ccs:
-                sched.append([(pos[int(i)], f, float(v)) for i, v in zip(sel, vals) if int(i) in pos])
-            parity_job["ccs"] = lambda b, s=sched: s[b % 100]
-        if bus is not None:        # the mix of the last block into zeroed buses (untimed)
-            bus_chk = torch.zeros_like(bus)
-            eng.mix(out, bus_chk, stream=stream.cuda_stream)
+                on = np.nonzero(gi % 40 == k)[0]
+                off = np.nonzero(gi % 40 == (k + 20) % 40)[0]
+                ev_on = eng.make_events(on, 1, (notes[on] + 12 * (k & 1)) % 128)
+                ev_off = eng.make_events(off, 0, notes[off])
+                self.step_events.append(np.concatenate([ev_on, ev_off]))
+        self.step_ccs = None
+        if name == "chain_cc":         # chains i % 100 == k % 100 get a new value of one field per step
+            from ol_dsp_amd.workload import uniform01
+            fields = [("chorus_depth", .08, 1.0), ("chorus_mix", 0.0, 1.0), ("verb_decay", .25, .95),
+                      ("verb_damping", .05, .95), ("pitch_shift", 0.0, 3.0)]
+            self.step_ccs = []
+            for k in range(100):
+                sel = np.nonzero(gi % 100 == k)[0].astype(np.uint32)
+                fname, lo, hi = fields[k % len(fields)]
+                vals = (lo + (hi - lo) * uniform01(7, k, int(first), n)[sel]).astype(np.float32)
+                self.step_ccs.append((eng.field(fname), sel, vals))
+        self.bus = None
+        if name == "voice_poly":       # Polyvoice buses of 8 voices (Polyvoice.h:28-33)
+            self.bus_lists = [list(range(g, min(g + 8, n))) for g in range(0, n, 8)]
+            eng.mix_config(self.bus_lists)
+            self.bus = torch.zeros((B, eng.n_buses), device=dev)
+        self.stream = torch.cuda.Stream(dev)       # dedicated non-default stream: events see the kernels
+        torch.cuda.synchronize(dev)
+
+        # The timed loop calls the C-ABI directly with prebuilt arguments (Engine.process's checks and
+        # tensor handling cost ~20 us of Python per call, more than a voice block's kernel): the host
+        # must stay ahead of the GPU, or the event pair would time the host's launch latency.
+        import ctypes
+
+        from ol_dsp_amd import _lib
+        self._lib = _lib
+        self.lib, self.h = eng.lib, eng.handle
+        c_stream = ctypes.c_void_p(self.stream.cuda_stream)
+        c_out = ctypes.c_void_p(self.out.data_ptr())
+        self.proc_args = [(self.h, ctypes.c_void_p(p.data_ptr() if p is not None else 0), c_out, B, _lib.IO_DEVICE,
+                           c_stream) for p in self.pool]
+        self.ev_args = [(self.h, e_.ctypes.data_as(ctypes.POINTER(_lib.Event)), len(e_))
+                        for e_ in self.step_events or []]
+        self.cc_args = [(self.h, f, sel.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                         vals.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), len(sel))
+                        for f, sel, vals in self.step_ccs or []]
+        self.k = 0                     # steps run so far (= blocks processed)
+        self.reps = []
+
+    def step(self) -> None:
+        k = self.k
+        rc = 0
+        if self.voice and k == self.note_off_block:
+            self.eng.note_events(self.note_off)
+        if self.ev_args:
+            rc |= self.lib.olfx_note_events(*self.ev_args[k % 40])
+        if self.cc_args:
+            rc |= self.lib.olfx_set_param_list(*self.cc_args[k % 100])
+        rc |= self.lib.olfx_process(*self.proc_args[k % self.pool_n])
+        if rc:
+            self._lib.check(rc, self.h)
+        if self.bus is not None:
+            self.eng.mix(self.out, self.bus, stream=self.stream.cuda_stream)
+        self.k += 1
+
+    def warm(self, steps: int) -> None:
+        import torch
+        for _ in range(steps):
+            self.step()
+        torch.cuda.synchronize(self.dev)
+
+    def timed(self, steps: int) -> None:
+        """One region of exactly `steps` steps.  Kernel time: ONE event pair on the launch stream
+        around the region (GPU time per step = the launch duration plus the gap between launches; a
+        pair per step would add two timestamp markers between consecutive kernels, ~3-4 us each on
+        the command processor, 10-20 % of a 35 us voice block: tools/loop_probe.py)."""
+        import torch
+
+        from ol_dsp_amd.dist import RunStats, reduce_stats
+        dev = self.dev
+        region = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        torch.cuda.synchronize(dev)
+        if torch.distributed.is_initialized():
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        region[0].record(self.stream)
+        for _ in range(steps):
+            self.step()
+        region[1].record(self.stream)
+        torch.cuda.synchronize(dev)
+        if torch.distributed.is_initialized():
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        kern_ms = region[0].elapsed_time(region[1]) / steps
+        self.reps.append(reduce_stats(RunStats(elapsed, kern_ms, float(self.n) * self.B * steps, 0.0, 1.0), device=dev))
+
+    def finish(self) -> dict:
+        import torch
+
+        from ol_dsp_amd.dist import RunStats, reduce_stats
+        args, dev, n, B, eng = self.args, self.dev, self.n, self.B, self.eng
+        K = args.steps
+        out, bus, stream = self.out, self.bus, self.stream
+        # sum |y| over the finite outputs of the last block (a voice whose Svf diverges -- possible in
+        # the reference DaisySP arithmetic at high cutoff, low resonance and high drive -- yields
+        # inf/NaN there too; DESIGN.md section 5); the count of non-finite samples beside it
+        finite = torch.isfinite(out)
+        nonfinite = int((~finite).sum().item())
+        checksum = float(torch.where(finite, out.abs(), torch.zeros_like(out)).sum().item())
+        bus_sum = float(bus.abs().sum().item()) if bus is not None else None
+        mix_ms = None
+        if bus is not None:            # the mix alone, K launches between one event pair (untimed for value)
+            scratch = torch.zeros_like(bus)
+            for _ in range(args.warmup):
+                eng.mix(out, scratch, stream=stream.cuda_stream)
+            mreg = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            mreg[0].record(stream)
+            for _ in range(K):
+                eng.mix(out, scratch, stream=stream.cuda_stream)
+            mreg[1].record(stream)
             torch.cuda.synchronize(dev)
-            pos = {int(i): j for j, i in enumerate(idx)}
-            lists = [bus_lists[0], bus_lists[nb - 1]]
-            parity_job["bus_lists"] = [[pos[v] for v in bl] for bl in lists]
-            parity_job["bus_voices"] = parity_job["gpu"][0]
-            parity_job["bus_gpu"] = np.ascontiguousarray(bus_chk[:, [0, nb - 1]].cpu().numpy())
+            mix_ms = reduce_stats(RunStats(0.0, mreg[0].elapsed_time(mreg[1]) / K, 0.0, 0.0, 1.0), device=dev).kernel_ms
+            for r in self.reps:
+                r.kernel_ms = max(r.kernel_ms - mix_ms, 1e-6)
 
-    stats = reduce_stats(RunStats(elapsed, kern_ms, float(n) * B * K, checksum, 1.0), device=dev)
-    bpf, rbpf, kname = eng.algorithmic_bytes_per_frame, eng.algorithmic_read_bytes_per_frame, eng.kernel_name
-    eng.close()
-    del pool, out
-    torch.cuda.empty_cache()
-    if rank != 0:
-        return {}
+        # untimed parity material: the last block of sampled instances, the pool blocks they read
+        # (read back from the device: exactly the timed inputs) and the leg's event / control schedule
+        parity_job = None
+        if self.rank == 0 and not args.no_parity:
+            if bus is not None:        # two whole buses (first, last) so the mix can be checked too
+                nb = len(self.bus_lists)
+                idx = np.array(sorted(set(self.bus_lists[0]) | set(self.bus_lists[nb - 1])), np.int64)
+            else:
+                idx = sample_instances(n)
+            ti = torch.from_numpy(idx).to(dev)
+            parity_job = {"kind": self.kind, "idx": idx, "block": B, "blocks": self.k,
+                          "params": np.ascontiguousarray(self.params[:, idx]),
+                          "gpu": out.index_select(2, ti).cpu().numpy()}
+            if self.ich:
+                parity_job["pool"] = [np.ascontiguousarray(p.index_select(2, ti).cpu().numpy()) for p in self.pool]
+                parity_job["pool_n"] = self.pool_n
+            notes, gi = self.notes, self.gi
+            if self.voice:
+                parity_job["notes"] = notes[idx].astype(np.int64)
+                parity_job["note_off_block"] = self.note_off_block
+            if self.step_events is not None:
+                pos = {int(i): j for j, i in enumerate(idx)}
+                sched = []
+                for k in range(40):
+                    on = [(pos[int(i)], True, int((notes[i] + 12 * (k & 1)) % 128)) for i in idx if gi[i] % 40 == k]
+                    off = [(pos[int(i)], False, int(notes[i])) for i in idx if gi[i] % 40 == (k + 20) % 40]
+                    sched.append(on + off)
+                parity_job["events"] = lambda b, s=sched: s[b % 40]
+            if self.step_ccs is not None:
+                pos = {int(i): j for j, i in enumerate(idx)}
+                sched = []
+                for f, sel, vals in self.step_ccs:
+                    sched.append([(pos[int(i)], f, float(v)) for i, v in zip(sel, vals) if int(i) in pos])
+                parity_job["ccs"] = lambda b, s=sched: s[b % 100]
+            if bus is not None:        # the mix of the last block into zeroed buses (untimed)
+                bus_chk = torch.zeros_like(bus)
+                eng.mix(out, bus_chk, stream=stream.cuda_stream)
+                torch.cuda.synchronize(dev)
+                pos = {int(i): j for j, i in enumerate(idx)}
+                lists = [self.bus_lists[0], self.bus_lists[nb - 1]]
+                parity_job["bus_lists"] = [[pos[v] for v in bl] for bl in lists]
+                parity_job["bus_voices"] = parity_job["gpu"][0]
+                parity_job["bus_gpu"] = np.ascontiguousarray(bus_chk[:, [0, nb - 1]].cpu().numpy())
 
-    elapsed, kern_ms, frames = stats.elapsed_s, stats.kernel_ms, stats.frames
-    per_launch = n * B
-    achieved = bpf * per_launch / (kern_ms * 1e-3) / 1e9
-    achieved_r = rbpf * per_launch / (kern_ms * 1e-3) / 1e9
-    tr = _traffic(name, n, B, args.traffic_json if name == args.workload else "", kname)
-    traffic = tr.get("hbm_bytes_per_launch") if tr else None
-    # the PMC-measured HBM bytes of the same kernel (profiles/traffic_<workload>.json, separate
-    # --pmc passes) over this run's kernel time: what HBM actually moved, against the peak
-    measured = {"traffic_build": (tr or {}).get("libolfx_sha256", "none recorded for this libolfx.so")[:16]}
-    if tr and traffic:
-        measured["hbm_gbs_measured"] = traffic / (kern_ms * 1e-3) / 1e9
-        rd = tr.get("read_bytes_by_request_size")
-        if rd:
-            measured.update({"traffic_read": rd, "hbm_read_gbs_measured": rd / (kern_ms * 1e-3) / 1e9,
-                             "frac_read_measured": rd / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS})
-    timing = ("one HIP event pair around the K timed steps / K, less the mix's own time (one pair around K mix "
-              "launches after the timed region)" if bus is not None else
-              "one HIP event pair on the launch stream around the K timed steps / K (launch duration + launch gap)")
-    if voice:
-        fps = VOICE_MOOG_FLOPS_PER_SAMPLE if kind == "voice_moog" else VOICE_FLOPS_PER_SAMPLE
-        tflops = fps * per_launch / (kern_ms * 1e-3) / 1e12
-        roofline = {"bound": "valu", "achieved": tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,
-                    "kernel": kname, "kernel_ms": kern_ms, "kernel_timing": timing, "algorithmic_flops_per_frame": fps,
-                    "algorithmic_bytes_per_frame": bpf, "hbm_gbs": achieved, "frames_per_launch": per_launch}
-    else:
-        roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                    "achieved_read": achieved_r, "frac_read": achieved_r / HBM_PEAK_GBS,
-                    "kernel": kname, "kernel_ms": kern_ms, "kernel_timing": timing,
-                    "algorithmic_bytes_per_frame": bpf, "algorithmic_read_bytes_per_frame": rbpf,
-                    "frames_per_launch": per_launch, **measured}
-    res = {"metric": METRIC, "value": frames / elapsed,
-           "unit": "voice samples/s" if voice else "stereo samples/s",
-           "ms_per_step": elapsed / K * 1e3, "frames": frames, "ranks_reporting": int(stats.ranks),
-           "config": {"workload": name, "restates": desc, "instances_per_gpu": n_per_gpu,
-                      "instances_total": total, "block": B, "sample_rate": args.sample_rate,
-                      "input_pool_blocks": pool_n, "parallelism": f"instance-shard x{world} (no data-path collective)"},
-           "roofline": roofline,
-           "output_checksum": stats.checksum, "output_nonfinite_rank0": nonfinite}
-    if mix_ms is not None:
-        nb = (n + 7) // 8
-        mix_bytes = 4.0 * n * B + 8.0 * nb * B          # voice reads + bus read-modify-write
-        res["mix"] = {"kernel": "voice_mix_v4", "kernel_ms": mix_ms, "bound": "hbm",
-                      "achieved": mix_bytes / (mix_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                      "frac": mix_bytes / (mix_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                      "algorithmic_bytes_per_launch": mix_bytes, "bus_checksum_rank0": bus_sum}
-    if step_events is not None:
-        res["control"] = {"events_per_block": int(np.mean([len(e) for e in step_events])),
-                          "note": "NoteOn/NoteOff folded per voice on the host and applied by the voice kernel at "
-                                  "the block start (olfx_engine.cpp fold_events, voice.hip voice_event)"}
-    if step_ccs is not None:
-        res["control"] = {"instances_changed_per_block": int(np.mean([len(c[1]) for c in step_ccs])),
-                          "note": "changed coefficients re-derived on the host for those instances only and "
-                                  "scattered on the device ahead of the block (control.hip coef_scatter)"}
-    # the CPU baseline and the parity replay run after every GPU leg (main): no leg is timed right
-    # after a many-thread CPU run (a short-kernel leg measured 1.7x slow once, launch-bound behind it)
-    res["cpu_baseline"] = None
-    res["parity"] = None
-    if with_cpu and world == 1 and args.cpu_seconds > 0:
-        res["cpu_job"] = (kind, PARAM_SET.get(name, ""))
-    if parity_job is not None:
-        res["parity_job"] = parity_job
-    return res
+        cs = reduce_stats(RunStats(0.0, 0.0, 0.0, checksum, 1.0), device=dev)
+        bpf, rbpf, kname = eng.algorithmic_bytes_per_frame, eng.algorithmic_read_bytes_per_frame, eng.kernel_name
+        eng.close()
+        del self.pool, self.out
+        self.bus = None
+        torch.cuda.empty_cache()
+        if self.rank != 0:
+            return {}
+
+        res = _rep_summary(self.reps, K)
+        kern_ms = res.pop("kernel_ms_median")
+        voice = self.voice
+        per_launch = n * B
+        achieved = bpf * per_launch / (kern_ms * 1e-3) / 1e9
+        achieved_r = rbpf * per_launch / (kern_ms * 1e-3) / 1e9
+        tr = _traffic(self.name, n, B, args.traffic_json if self.name == args.workload else "", kname)
+        traffic = tr.get("hbm_bytes_per_launch") if tr else None
+        # the PMC-measured HBM bytes of the same kernel (profiles/traffic_<workload>.json, separate
+        # --pmc passes) over this run's kernel time: what HBM actually moved, against the peak
+        measured = {"traffic_build": (tr or {}).get("libolfx_sha256", "none recorded for this libolfx.so")[:16]}
+        if tr and traffic:
+            measured["hbm_gbs_measured"] = traffic / (kern_ms * 1e-3) / 1e9
+            rd = tr.get("read_bytes_by_request_size")
+            if rd:
+                measured.update({"traffic_read": rd, "hbm_read_gbs_measured": rd / (kern_ms * 1e-3) / 1e9,
+                                 "frac_read_measured": rd / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS})
+        timing = ("median over the repetitions of one HIP event pair around the K timed steps / K, less the mix's "
+                  "own time (one pair around K mix launches after the timed regions)" if bus is not None else
+                  "median over the repetitions of one HIP event pair on the launch stream around the K timed steps / K "
+                  "(launch duration + launch gap)")
+        if voice:
+            fps = VOICE_MOOG_FLOPS_PER_SAMPLE if self.kind == "voice_moog" else VOICE_FLOPS_PER_SAMPLE
+            tflops = fps * per_launch / (kern_ms * 1e-3) / 1e12
+            roofline = {"bound": "valu", "achieved": tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,
+                        "kernel": kname, "kernel_ms": kern_ms, "kernel_timing": timing,
+                        "algorithmic_flops_per_frame": fps, "algorithmic_bytes_per_frame": bpf, "hbm_gbs": achieved,
+                        "frames_per_launch": per_launch}
+        else:
+            roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                        "achieved_read": achieved_r, "frac_read": achieved_r / HBM_PEAK_GBS,
+                        "kernel": kname, "kernel_ms": kern_ms, "kernel_timing": timing,
+                        "algorithmic_bytes_per_frame": bpf, "algorithmic_read_bytes_per_frame": rbpf,
+                        "frames_per_launch": per_launch, **measured}
+        res.update({"metric": METRIC, "unit": "voice samples/s" if voice else "stereo samples/s",
+                    "config": {"workload": self.name, "restates": self.desc, "instances_per_gpu": self.n_per_gpu,
+                               "instances_total": self.total, "block": B, "sample_rate": args.sample_rate,
+                               "input_pool_blocks": self.pool_n,
+                               "parallelism": f"instance-shard x{self.world} (no data-path collective)"},
+                    "roofline": roofline, "output_checksum": cs.checksum, "output_nonfinite_rank0": nonfinite})
+        if mix_ms is not None:
+            nb = (n + 7) // 8
+            mix_bytes = 4.0 * n * B + 8.0 * nb * B          # voice reads + bus read-modify-write
+            res["mix"] = {"kernel": "voice_mix_v4", "kernel_ms": mix_ms, "bound": "hbm",
+                          "achieved": mix_bytes / (mix_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                          "frac": mix_bytes / (mix_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                          "algorithmic_bytes_per_launch": mix_bytes, "bus_checksum_rank0": bus_sum}
+        if self.step_events is not None:
+            res["control"] = {"events_per_block": int(np.mean([len(e) for e in self.step_events])),
+                              "note": "NoteOn/NoteOff folded per voice on the host and applied by the voice kernel at "
+                                      "the block start (olfx_engine.cpp fold_events, voice.hip voice_event)"}
+        if self.step_ccs is not None:
+            res["control"] = {"instances_changed_per_block": int(np.mean([len(c[1]) for c in self.step_ccs])),
+                              "note": "changed coefficients re-derived on the host for those instances only and "
+                                      "scattered on the device ahead of the block (control.hip coef_scatter)"}
+        # the CPU baseline and the parity replay run after every GPU leg (main): no leg is timed right
+        # after a many-thread CPU run (a short-kernel leg measured 1.7x slow once, launch-bound behind it)
+        res["cpu_baseline"] = None
+        res["parity"] = None
+        if self.with_cpu and self.world == 1 and args.cpu_seconds > 0:
+            res["cpu_job"] = (self.kind, PARAM_SET.get(self.name, ""))
+        if parity_job is not None:
+            res["parity_job"] = parity_job
+        return res
 
 
 def run_cpu_jobs(jobs, reuse, parity_jobs, args):
@@ -698,8 +792,13 @@ def compact_leg(r: dict) -> dict:
     """One leg in ~250 bytes: instances, kernel, time, throughput, roofline fractions, measured
     traffic per frame, the CPU baseline and the parity verdict."""
     rf = r["roofline"]
+    if rf is None:                  # --stub
+        return {"n": r["config"]["instances_per_gpu"], "value": _r(r["value"]), "ranks": r["ranks_reporting"]}
     c = {"n": r["config"]["instances_per_gpu"], "kernel": rf["kernel"], "kernel_ms": _r(rf["kernel_ms"]),
          "value": _r(r["value"]), "bound": rf["bound"], "frac": _r(rf["frac"], 3)}
+    reps = r.get("reps")
+    if reps:                        # the repetitions' kernel-time range around the median
+        c["ms_range"] = [_r(reps["kernel_ms_min"]), _r(reps["kernel_ms_max"])]
     if rf["bound"] == "hbm":
         c["frac_read"] = _r(rf["frac_read"], 3)
         if rf.get("traffic"):
@@ -741,32 +840,42 @@ def main():
         torch.cuda.set_device(dev)
 
     n = args.instances or WORKLOADS[args.workload][1]
-    cpu_jobs, cpu_reuse, parity_jobs = [], [], []
+    also = args.also if args.also is not None else (DEFAULT_ALSO if args.workload == "chorus" and not args.stub else "")
+    also_names = [a for a in also.split(",") if a]
+    R, K = max(1, args.reps), args.steps
+    W0 = max(args.warmup, args.leg_warmup)       # before a leg's first region: the sustained clock
+    Wr = args.rep_warmup                         # before each later region of the leg
+    total_blocks = W0 + R * K + (R - 1) * Wr
+    # every leg is built first and kept alive, then the regions run leg after leg, the order rotated
+    # by one leg per repetition (each leg's regions see different neighbours and clock states)
+    specs = [(args.workload, n, True, args.workload)]
+    for name in also_names:
+        twin = EVENT_FREE.get(name)
+        tkey = twin if twin != "chain" else "chain_16384"
+        # a control leg's CPU work per block is its twin's (the CPU oracle applies events and
+        # parameters per instance at block boundaries): the twin's measured baseline is reused
+        reuse = bool(twin and (twin in also_names or twin == args.workload))
+        specs.append((name, WORKLOADS[name][1], not reuse, name if name != "chain" else "chain_16384"))
     if args.stub:
-        main_res, also_res = run_stub(args.workload, n, args, rank, world), {}
+        legs = [StubLeg(name, npg, args, rank, world) for name, npg, _, _ in specs]
     else:
-        main_res = run_workload(args.workload, n, args, rank, world, dev, with_cpu=True)
-        if rank == 0 and "cpu_job" in main_res:
-            cpu_jobs.append((main_res, *main_res.pop("cpu_job")))
-        if rank == 0 and "parity_job" in main_res:
-            parity_jobs.append((main_res, main_res.pop("parity_job")))
-        also = args.also if args.also is not None else (DEFAULT_ALSO if args.workload == "chorus" else "")
-        also_res = {}
-        for name in [a for a in also.split(",") if a]:
-            twin = EVENT_FREE.get(name)
-            tkey = twin if twin != "chain" else "chain_16384"
-            # a control leg's CPU work per block is its twin's (the CPU oracle applies events and
-            # parameters per instance at block boundaries): the twin's measured baseline is reused
-            reuse = bool(twin and (tkey in also_res or twin in also.split(",") or twin == args.workload))
-            r = run_workload(name, WORKLOADS[name][1], args, rank, world, dev, with_cpu=not reuse)
-            if rank != 0:
-                continue
-            key = name if name != "chain" else "chain_16384"
-            also_res[key] = r
+        legs = [Leg(name, npg, args, rank, world, dev, with_cpu, total_blocks) for name, npg, with_cpu, _ in specs]
+    m = len(legs)
+    for r in range(R):
+        for leg in legs[r % m:] + legs[:r % m]:
+            leg.warm(W0 if r == 0 else Wr)
+            leg.timed(K)
+    results = [leg.finish() for leg in legs]
+    main_res = results[0]
+    also_res = {key: res for (_, _, _, key), res in zip(specs[1:], results[1:])}
+    cpu_jobs, cpu_reuse, parity_jobs = [], [], []
+    if rank == 0 and not args.stub:
+        for (name, _, with_cpu, key), r in zip(specs, results):
             if "cpu_job" in r:
                 cpu_jobs.append((r, *r.pop("cpu_job")))
-            elif reuse:
-                cpu_reuse.append((r, tkey))
+            elif name in EVENT_FREE and not with_cpu:
+                twin = EVENT_FREE[name]
+                cpu_reuse.append((r, twin if twin != "chain" else "chain_16384"))
             if "parity_job" in r:
                 parity_jobs.append((r, r.pop("parity_job")))
         # the control legs against their event-free twins (an `also` leg or the main workload)
@@ -793,7 +902,7 @@ def main():
             "unit": main_res["unit"],
             "n_gpus": world,
             "steps": args.steps,
-            "warmup": args.warmup,
+            "warmup": W0,
             "ms_per_step": main_res["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
@@ -805,6 +914,9 @@ def main():
                                                           "parallelism") if k in main_res["config"]},
             "frames": main_res["frames"],
             "ranks_reporting": main_res["ranks_reporting"],
+            "reps": {"n": R, "warmup_between": Wr, "leg_order": "rotated by one leg per repetition" if m > 1 else "one leg",
+                     "kernel_ms": [_r(v) for v in main_res["reps"]["kernel_ms"]],
+                     "kernel_spread": _r(main_res["reps"]["kernel_spread"], 3)},
         }
         if rf is not None:
             keep = ("bound", "achieved", "peak", "unit", "frac", "traffic", "achieved_read", "frac_read", "kernel",
@@ -829,7 +941,7 @@ def main():
             full["also"] = also_res
             res["also"] = {k: compact_leg(v) for k, v in also_res.items()}
             res["all_parity_ok"] = all((v.get("parity") or {}).get("ok", False) for v in
-                                       [main_res] + list(also_res.values())) if not args.no_parity else None
+                                       [main_res] + list(also_res.values())) if not (args.no_parity or args.stub) else None
         if args.full_json:
             try:
                 os.makedirs(os.path.dirname(args.full_json), exist_ok=True)

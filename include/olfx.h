@@ -228,9 +228,9 @@ int olfx_destroy(olfx_engine *e);
    olfx_destroy and olfx_sync it waits for THIS engine's queued work only (the stream of its latest
    olfx_process / olfx_mix, its own streams, its control packets), never for the whole device:
    other engines and the host's own kernels keep running.  The caller keeps the stream it passed
-   last alive until then (and until the next olfx_process on another stream, which the engine
-   orders after the previous launch itself: switching streams between blocks needs no event from
-   the caller; the caller's own buffers stay the caller's to order). */
+   last alive until then (and until the next olfx_process / olfx_mix on another stream, which the
+   engine orders after its previous launch itself: switching streams between calls needs no event
+   from the caller; the caller's own buffers stay the caller's to order). */
 int olfx_reset(olfx_engine *e);
 
 /* Set parameters of instances [first, first+count): `values` is field-major

@@ -15,8 +15,11 @@
 // for audio rows that are not 16-B aligned, in dattorro_predelay_v2 ahead of it (its pre-delayed
 // block as a coalesced stream, PreBlock).  Measured (65,536 instances, random pre-delays, same box):
 // v4f 0.589 ms, the round-4 pre-pass + network 0.597, the uniform reverb 0.554 (1.063x).
+#include <cstdlib>
+
 #include "dattorro_stage.h"
 #include "chorus_stage.h"
+#include "lds_flags.h"
 
 namespace olfx {
 
@@ -79,6 +82,248 @@ __global__ __launch_bounds__(64, 1) void dattorro_block_v4(DattorroArgs a) {
     }
     dt_finish();
     if constexpr (!GATHER) in1.lds_out(a, i);
+}
+
+// ---------------------------------------------------------------------------------------------
+// dattorro_block_v5: the network as three recurrences, one wave each (round 6).  Within a launch
+// of at most kV5MaxFrames frames the network is three independent recurrences joined only by
+// feed-forward values:
+//   DI  (wave 0): pre-delay, pre-LPF and the 4 input all-passes (verb.cpp:273-282) -> x;
+//   TA  (wave 1): tank half 0 (verb.cpp:284-295, i = 0): AP1A, DL1A, damping, AP2A, DL2A;
+//   TB  (wave 2): tank half 1: AP1B, DL1B, damping, AP2B, DL2B.
+// The halves exchange data only through postDampingDelay[1 - i]'s main tap (verb.cpp:286), 3163
+// (TA reads DL2B) and 3720 (TB reads DL2A) samples back: within a launch shorter than that they
+// read only what earlier launches wrote, and each wave reads back only rings it writes itself.  x
+// goes to both halves through an LDS queue.  The stereo taps (verb.cpp:302-325) are split at
+// their sum order: L = pL - oL5 - oL6 + oL7 with pL = oL1 + oL2 - oL3 + oL4 on half 1's rings and
+// oL5..7 on half 0's; R the mirror image.  So half 1 sends pL to half 0, which finishes L, and
+// half 0 sends pR to half 1, which finishes R (one float per frame each way, through LDS, one
+// step late so neither waits on the other's current step) -- the reference's exact additions.
+// Per 4-frame step: DI 5 taps, each half 11 taps (3 network + 1 modulated + 7 output) and 4
+// ring writes, where v4's single wave carried all 27: a workgroup of 64 instances runs three
+// waves (16,384 instances: 768 waves instead of 256), each with the register set of its own taps.
+// ---------------------------------------------------------------------------------------------
+namespace {
+constexpr uint32_t kV5Depth = 4;          // LDS queue slots (4-frame steps) per hand-off
+constexpr uint32_t kV5MaxFrames = 2048;   // < 3163 - queue skew: no cross-half read within a launch
+enum { V5F_X = 0, V5F_XT0, V5F_XT1, V5F_P0, V5F_P1, V5F_PT0, V5F_PT1, V5F_N };
+// V5F_X: steps of x published by DI; V5F_XT<h>: steps of x half h has taken; V5F_P<h>: partial
+// sums half h has published; V5F_PT<h>: half h's partials the other half has taken
+
+// The taps of tank half H.  P1..P4: the partial sum this half sends (half 0: pR = oR1 + oR2 -
+// oR3 + oR4 on DL1A, DL1A, AP2A, DL2A; half 1: pL = oL1 + oL2 - oL3 + oL4 on DL1B, DL1B, AP2B,
+// DL2B); T5..T7: the terms that finish the other half's sum into this half's channel (half 0,
+// L: oL5 DL1A, oL6 AP2A, oL7 DL2A; half 1, R: oR5 DL1B, oR6 AP2B, oR7 DL2B).
+template <int H> struct V5Half;
+template <> struct V5Half<0> {
+    static constexpr int kAP1 = DT_AP1A, kDL1 = DT_DL1A, kAP2 = DT_AP2A, kDL2 = DT_DL2A, kLp = DTS_LP_DAMP_A;
+    using FB = olfx::dt::Tap<DT_DL2B, 3163, 0>;
+    using DL1 = olfx::dt::Tap<DT_DL1A, 4453, 0>;
+    using AP2 = olfx::dt::Tap<DT_AP2A, 1800, 0>;
+    using AP1 = olfx::dt::ModTap<DT_AP1A, kDtDelay[DT_AP1A]>;
+    using P1 = olfx::dt::Tap<DT_DL1A, kDl1A_o1, 1>;
+    using P2 = olfx::dt::Tap<DT_DL1A, kDl1A_o2, 1>;
+    using P3 = olfx::dt::Tap<DT_AP2A, kAp2A_o2, 1>;
+    using P4 = olfx::dt::Tap<DT_DL2A, kDl2A_o2, 1>;
+    using T5 = olfx::dt::Tap<DT_DL1A, kDl1A_o3, 1>;
+    using T6 = olfx::dt::Tap<DT_AP2A, kAp2A_o1, 1>;
+    using T7 = olfx::dt::Tap<DT_DL2A, kDl2A_o1, 1>;
+};
+template <> struct V5Half<1> {
+    static constexpr int kAP1 = DT_AP1B, kDL1 = DT_DL1B, kAP2 = DT_AP2B, kDL2 = DT_DL2B, kLp = DTS_LP_DAMP_B;
+    using FB = olfx::dt::Tap<DT_DL2A, 3720, 0>;
+    using DL1 = olfx::dt::Tap<DT_DL1B, 4217, 0>;
+    using AP2 = olfx::dt::Tap<DT_AP2B, 2656, 0>;
+    using AP1 = olfx::dt::ModTap<DT_AP1B, kDtDelay[DT_AP1B]>;
+    using P1 = olfx::dt::Tap<DT_DL1B, kDl1B_o1, 1>;
+    using P2 = olfx::dt::Tap<DT_DL1B, kDl1B_o2, 1>;
+    using P3 = olfx::dt::Tap<DT_AP2B, kAp2B_o2, 1>;
+    using P4 = olfx::dt::Tap<DT_DL2B, kDl2B_o2, 1>;
+    using T5 = olfx::dt::Tap<DT_DL1B, kDl1B_o3, 1>;
+    using T6 = olfx::dt::Tap<DT_AP2B, kAp2B_o1, 1>;
+    using T7 = olfx::dt::Tap<DT_DL2B, kDl2B_o1, 1>;
+};
+
+__device__ __forceinline__ float4 f4(const float (&v)[4]) { return make_float4(v[0], v[1], v[2], v[3]); }
+
+// one tank half over the launch: x from qx, its partial to qmine, the other's from qother
+template <int H>
+__device__ __forceinline__ void v5_tank(const DattorroArgs &a, uint32_t i, uint32_t lane, bool live, uint32_t steps,
+                                        const float4 *qx, float4 *qmine, const float4 *qother, uint32_t *flags) {
+    using Hf = V5Half<H>;
+    const uint32_t n = a.n, t0 = a.t0;
+    const float g_dd1 = a.coef[DTC_DD1 * n + i];
+    const float g_damp = a.coef[DTC_DAMPING * n + i];
+    const float g_decay = a.coef[DTC_DECAY * n + i];
+    const float g_dd2 = a.coef[DTC_DD2 * n + i];
+    float lp = a.state[Hf::kLp * n + i];
+    typename Hf::FB fb; typename Hf::DL1 dl1; typename Hf::AP2 ap2; typename Hf::AP1 ap1;
+    typename Hf::P1 p1; typename Hf::P2 p2; typename Hf::P3 p3; typename Hf::P4 p4;
+    typename Hf::T5 t5; typename Hf::T6 t6; typename Hf::T7 t7;
+#define V5_TAPS(OP) OP(fb) OP(dl1) OP(ap2) OP(p1) OP(p2) OP(p3) OP(p4) OP(t5) OP(t6) OP(t7)
+#define V5_PRIME(T) T.prime(a, t0, i);
+#define V5_PREFETCH(T) T.prefetch(a, t, i);
+#define V5_ADVANCE(T) T.advance();
+    V5_TAPS(V5_PRIME)
+    ap1.prime(a, t0, i);
+    float* const out = a.out + (H ? a.plane : 0);
+    float q5[4], q6[4], q7[4];                        // the previous step's finishing terms
+    auto finish = [&](uint32_t s) {                   // channel H of step s: the other half's partial + q5..q7
+        const uint32_t slot = s % kV5Depth;
+        wait_for([&] { return flag_get(flags + V5F_P0 + (1 - H)) > s; });
+        const float4 po = qother[slot * 64u + lane];
+        flag_put(flags + V5F_PT0 + (1 - H), s + 1);
+        const float pv[4] = {po.x, po.y, po.z, po.w};
+        if (live) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float o = pv[k];
+                o -= q5[k]; o -= q6[k]; o += q7[k];
+                out[(size_t)(4u * s + (uint32_t)k) * n + i] = o;
+            }
+        }
+    };
+    for (uint32_t s = 0; s < steps; ++s) {
+        const uint32_t t = t0 + 4u * s, slot = s % kV5Depth;
+        V5_TAPS(V5_PREFETCH)
+        ap1.prefetch(a, t, i);
+        ap1.resolve();
+        wait_for([&] { return flag_get(flags + V5F_X) > s; });
+        const float4 xv = qx[slot * 64u + lane];
+        flag_put(flags + V5F_XT0 + H, s + 1);
+        const float x[4] = {xv.x, xv.y, xv.z, xv.w};
+        float w_ap1[4], w_dl1[4], w_ap2[4], w_dl2[4], pm[4], n5[4], n6[4], n7[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {                 // verb.cpp:286-294; the APF gain is -dd1
+            float y = x[k] + fb.get(k) * g_decay;
+            float d = ap1.v[k];
+            y += d * g_dd1; w_ap1[k] = y; y = d + y * -g_dd1;
+            w_dl1[k] = y;
+            lp += (dl1.get(k) - lp) * g_damp;
+            y = lp * g_decay;
+            d = ap2.get(k);
+            y += d * -g_dd2; w_ap2[k] = y; y = d + y * g_dd2;
+            w_dl2[k] = y;
+            float p = p1.get(k);
+            p += p2.get(k); p -= p3.get(k); p += p4.get(k);
+            pm[k] = p;
+            n5[k] = t5.get(k); n6[k] = t6.get(k); n7[k] = t7.get(k);
+        }
+        const uint32_t gw = t >> 2;
+        *olfx::dt::grpu<Hf::kAP1>(a, gw, i) = f4(w_ap1);
+        *olfx::dt::grpu<Hf::kDL1>(a, gw, i) = f4(w_dl1);
+        *olfx::dt::grpu<Hf::kAP2>(a, gw, i) = f4(w_ap2);
+        *olfx::dt::grpu<Hf::kDL2>(a, gw, i) = f4(w_dl2);
+        // this step's partial out, then the previous step's channel
+        wait_for([&] { return flag_get(flags + V5F_PT0 + H) + kV5Depth > s; });
+        qmine[slot * 64u + lane] = f4(pm);
+        flag_put(flags + V5F_P0 + H, s + 1);
+        if (s > 0) finish(s - 1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { q5[k] = n5[k]; q6[k] = n6[k]; q7[k] = n7[k]; }
+        V5_TAPS(V5_ADVANCE)
+        ap1.advance();
+    }
+    if (steps) finish(steps - 1);
+    if (live) a.state[Hf::kLp * n + i] = lp;
+#undef V5_TAPS
+#undef V5_PRIME
+#undef V5_PREFETCH
+#undef V5_ADVANCE
+}
+}  // namespace
+
+__global__ __launch_bounds__(192) void dattorro_block_v5(DattorroArgs a) {
+    __shared__ float4 in1_ring[kDtSize[DT_IN1] / 4u * 64u];     // DI's IN1 ring (32 KB), as v4
+    __shared__ float4 qx[kV5Depth * 64u], q0[kV5Depth * 64u], q1[kV5Depth * 64u];
+    __shared__ uint32_t flags[V5F_N];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t role = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint32_t n = a.n;
+    const uint32_t i0 = blockIdx.x * 64u + lane;
+    const bool live = i0 < n;
+    const uint32_t i = live ? i0 : n - 1u;             // dead lanes mirror instance n - 1 (same bits)
+    if (tid < V5F_N) flags[tid] = 0;
+    __syncthreads();
+    const uint32_t steps = a.n_frames / 4u;
+    if (role == 1) {
+        v5_tank<0>(a, i, lane, live, steps, qx, q0, q1, flags);
+        return;
+    }
+    if (role == 2) {
+        v5_tank<1>(a, i, lane, live, steps, qx, q1, q0, flags);
+        return;
+    }
+    // ---- DI: input (l + r) / 2 (ReverbFx.cpp:13-16), pre-delay, pre-LPF, 4 input all-passes ----
+    const uint32_t t0 = a.t0;
+    const size_t plane = a.plane;
+    const bool stereo = a.in_ch == 2;
+    const float g_pre = a.coef[DTC_PREFILTER * n + i];
+    const float g_in1 = a.coef[DTC_IN1 * n + i];
+    const float g_in2 = a.coef[DTC_IN2 * n + i];
+    const uint32_t dpre = (uint32_t)a.coef[DTC_PREDELAY * n + i];
+    float lp_pre = a.state[DTS_LP_PRE * n + i];
+    olfx::dt::Tap<DT_IN0, 142, 0> in0;
+    olfx::dt::LdsTap<DT_IN1, 107> in1;
+    olfx::dt::Tap<DT_IN2, 379, 0> in2;
+    olfx::dt::Tap<DT_IN3, 277, 0> in3;
+    olfx::dt::PreTap pre;
+    in1.lds = in1_ring + lane;
+    in1.lds_in(a, i);
+    in0.prime(a, t0, i); in1.prime(a, t0, i); in2.prime(a, t0, i); in3.prime(a, t0, i);
+    pre.prime(a, t0, dpre, i);
+    float in_l[4], in_r[4], nx_l[4], nx_r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        in_l[k] = a.in[(size_t)k * n + i];
+        in_r[k] = stereo ? a.in[plane + (size_t)k * n + i] : 0.f;
+    }
+    for (uint32_t s = 0; s < steps; ++s) {
+        const uint32_t t = t0 + 4u * s, slot = s % kV5Depth;
+        const uint32_t fn = s + 1 < steps ? 4u * s + 4u : 4u * s;   // next inputs, clamped
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            nx_l[k] = a.in[(size_t)(fn + k) * n + i];
+            nx_r[k] = stereo ? a.in[plane + (size_t)(fn + k) * n + i] : 0.f;
+        }
+        in0.prefetch(a, t, i); in1.prefetch(a, t, i); in2.prefetch(a, t, i); in3.prefetch(a, t, i);
+        pre.prefetch(a, t, dpre, i);
+        float xin[4], xpd[4], w0[4], w1[4], w2[4], w3[4], xo[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xin[k] = stereo ? (in_l[k] + in_r[k]) / 2 : in_l[k];
+        pre.resolve(xin, dpre, xpd);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {                 // verb.cpp:273-282
+            lp_pre += (xpd[k] - lp_pre) * g_pre;
+            float x = lp_pre;
+            float d = in0.get(k);
+            x += d * -g_in1; w0[k] = x; x = d + x * g_in1;
+            d = in1.get(k);
+            x += d * -g_in1; w1[k] = x; x = d + x * g_in1;
+            d = in2.get(k);
+            x += d * -g_in2; w2[k] = x; x = d + x * g_in2;
+            d = in3.get(k);
+            x += d * -g_in2; w3[k] = x; x = d + x * g_in2;
+            xo[k] = x;
+        }
+        const uint32_t gw = t >> 2;
+        pre.write(a, gw, i, xin);
+        *olfx::dt::grpu<DT_IN0>(a, gw, i) = f4(w0);
+        in1.write(a, gw, i, f4(w1));
+        *olfx::dt::grpu<DT_IN2>(a, gw, i) = f4(w2);
+        *olfx::dt::grpu<DT_IN3>(a, gw, i) = f4(w3);
+        wait_for([&] {
+            return flag_get(flags + V5F_XT0) + kV5Depth > s && flag_get(flags + V5F_XT1) + kV5Depth > s;
+        });
+        qx[slot * 64u + lane] = f4(xo);
+        flag_put(flags + V5F_X, s + 1);
+        in0.advance(); in1.advance(); in2.advance(); in3.advance();
+        pre.advance(xin);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { in_l[k] = nx_l[k]; in_r[k] = nx_r[k]; }
+    }
+    if (live) a.state[DTS_LP_PRE * n + i] = lp_pre;
+    in1.lds_out(a, i);
 }
 
 constexpr uint32_t kPreSize = kDtSize[DT_PRE];
@@ -383,6 +628,14 @@ int predelay_kernel(uint32_t n, uint64_t plane, const float *in) {
     return n % 4u == 0u && plane % 4u == 0u && ((uintptr_t)in & 15u) == 0u ? 3 : 2;
 }
 
+// A/B knob while the split network is measured against v4 (OLFX_DT_V4=1: the single-wave network)
+static bool dt_use_v4() {
+    static const bool v4 = [] { const char *e = std::getenv("OLFX_DT_V4"); return e && e[0] == '1'; }();
+    return v4;
+}
+
+const char *dattorro_uniform_kernel() { return dt_use_v4() ? "dattorro_block_v4" : "dattorro_block_v5"; }
+
 hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
     if ((a.t0 & 3u) || (a.n_frames & 3u)) return hipErrorInvalidValue;   // 4-frame chunks
@@ -400,8 +653,18 @@ hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s) {
             hipLaunchKernelGGL(dattorro_predelay_v2, dim3((a.n + 63) / 64), dim3(64), 0, s, a);
             hipLaunchKernelGGL(dattorro_block_v4<true>, dim3(blocks), dim3(threads), 0, s, a);
         }
-    } else {
+    } else if (dt_use_v4()) {
         hipLaunchKernelGGL(dattorro_block_v4<false>, dim3(blocks), dim3(threads), 0, s, a);
+    } else {
+        // pieces of at most kV5MaxFrames (the halves' cross taps then read earlier launches only)
+        for (uint32_t f0 = 0; f0 < a.n_frames; f0 += kV5MaxFrames) {
+            DattorroArgs p = a;
+            p.n_frames = min(kV5MaxFrames, a.n_frames - f0);
+            p.t0 = (a.t0 + f0) & 0xFFFFu;
+            p.in = a.in + (size_t)f0 * a.n;
+            p.out = a.out + (size_t)f0 * a.n;
+            hipLaunchKernelGGL(dattorro_block_v5, dim3(blocks), dim3(192), 0, s, p);
+        }
     }
     return hipGetLastError();
 }

@@ -1667,6 +1667,12 @@ int olfx_mix(olfx_engine *e, const float *voice_out, float *bus_out, uint32_t n_
     HIPCHK(e, hipSetDevice(e->device));
     if (!e->mix_done) HIPCHK(e, hipEventCreateWithFlags(&e->mix_done, hipEventDisableTiming));
     hipStream_t s = (hipStream_t)stream;
+    // a stream switch, as in olfx_process: the mix after the engine's previous launch, and the next
+    // launch (on whichever stream) after the mix
+    if (e->have_last && s != e->last_stream) {
+        HIPCHK(e, hipEventRecord(e->switched, e->last_stream));
+        HIPCHK(e, hipStreamWaitEvent(s, e->switched, 0));
+    }
     MixArgs a{};
     a.off = e->mix_dev;
     a.order = e->mix_dev + e->n_buses + 1;
@@ -1690,6 +1696,8 @@ int olfx_mix(olfx_engine *e, const float *voice_out, float *bus_out, uint32_t n_
         HIPCHK(e, hipMemcpyAsync(e->h_out, e->d_out, fout * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(e, hipStreamSynchronize(s));
         std::memcpy(bus_out, e->h_out, fout * 4);
+        e->last_stream = s;
+        e->have_last = true;
         return OLFX_OK;
     }
     a.in = voice_out;
@@ -1749,7 +1757,7 @@ const char *olfx_kernel_name(const olfx_engine *e) {
     if (!e) return "";
     switch (e->kind) {
     case OLFX_KIND_DATTORRO:   // gather mode: the fused network (aligned rows) or the pre-pass + network
-        return !e->dt_gather ? "dattorro_block_v4"
+        return !e->dt_gather ? dattorro_uniform_kernel()
                : e->dt_pre_kernel == 3 ? "dattorro_block_v4f"
                                        : "dattorro_predelay_v2+dattorro_block_v4";
     case OLFX_KIND_CHORUS:

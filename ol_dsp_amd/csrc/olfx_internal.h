@@ -382,6 +382,7 @@ struct ChainArgs {
 };
 
 hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s);
+const char *dattorro_uniform_kernel();   // the uniform-mode network launch_dattorro runs
 hipError_t launch_chain(const ChainArgs &a, hipStream_t s);
 hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s);
 // the chorus kernel launch_chorus picks for n instances, ring sizes and cooperative I/O

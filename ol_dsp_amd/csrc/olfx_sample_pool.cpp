@@ -173,10 +173,16 @@ int run_complete(Generation *g) {
         // release: an instance that reads the new count (acquire) sees this run's outputs, and may
         // refill input slot b % depth
         g->blocks.store(b + 1, std::memory_order_release);
+        // the calls queued for block b + 1 land now: queue_or_apply applies a later call with that
+        // target at once, so none may stay queued behind it (an instance's calls keep call order)
+        rc = apply_pending(g, b + 1);
+        if (rc) return rc;
     }
 }
 
-// a call lands at the instance's next block boundary at or after its position
+// a call lands at the instance's next block boundary at or after its position.  Invariant (held
+// under g->mu): every queued call targets a block past the engine's next one, so a call applied at
+// once never overtakes a queued call of the same instance
 int queue_or_apply(olfx_sample *s, PendingOp op) {
     Generation *g = s->g;
     std::lock_guard<std::mutex> lk(g->mu);

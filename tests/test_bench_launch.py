@@ -45,3 +45,25 @@ def test_gpus_1_runs_in_process():
     res = _run_bench("--stub", "--steps", "3", "--warmup", "0", "--instances", "64", "--full-json", "")
     assert res["n_gpus"] == 1 and res["ranks_reporting"] == 1
     assert res["frames"] == 64 * 256 * 3
+
+
+def test_gpus_4_end_to_end_with_legs():
+    """`bench.py --gpus 4` under gloo through the whole flow a GPU run takes: four
+    rank processes, two legs kept alive and interleaved over the repetitions (rotated order), one
+    all-reduce per region, rank 0's final line.  The line's value is the job's frames summed over
+    the four ranks divided by the median region's time (max over ranks)."""
+    n, steps, reps = 4096, 4, 3
+    res = _run_bench("--stub", "--gpus", "4", "--steps", str(steps), "--warmup", "0", "--leg-warmup", "0",
+                     "--reps", str(reps), "--instances", str(n), "--also", "chain", "--full-json", "", timeout=240)
+    assert res["n_gpus"] == 4
+    assert res["ranks_reporting"] == 4
+    assert res["config"]["instances_per_gpu"] == n
+    assert res["config"]["instances_total"] == 4 * n
+    assert res["frames"] == 4 * n * 256 * steps                 # one region of every rank's shard
+    elapsed = res["ms_per_step"] * steps / 1e3                   # the median region (max over ranks)
+    assert abs(res["value"] - res["frames"] / elapsed) <= 1e-6 * res["value"]
+    assert res["reps"]["n"] == reps and len(res["reps"]["kernel_ms"]) == reps
+    leg = res["also"]["chain_16384"]
+    assert leg["ranks"] == 4 and leg["n"] == 16384
+    from ol_dsp_amd.dist import shard
+    assert res["output_checksum"] == sum(shard(4 * n, 4, r)[0] for r in range(4))

@@ -377,6 +377,38 @@ def test_stream_switch_is_ordered_by_the_engine(cuda):
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
 
+def test_stream_switch_through_the_mix_is_ordered(cuda):
+    """olfx_process on one stream, olfx_mix on a second, the next olfx_process on a third, with no
+    ordering from the caller: the mix is ordered after the block it sums, and the next
+    block after the mix, hence after the previous block.  Voices and buses bit-identical to the
+    same calls on one stream."""
+    import torch
+    n, blocks = 32768, 9
+    cfg = voice_configs(np.random.default_rng(323), n)
+    notes = [36 + (i % 60) for i in range(n)]
+    buses = [list(range(g, g + 8)) for g in range(0, n, 8)]
+    res = []
+    for rotate in (False, True):
+        e = engine("voice", n)
+        e.set_params(0, cfg)
+        e.note_events([(i, 1, notes[i]) for i in range(n)])
+        e.mix_config(buses)
+        streams = [torch.cuda.Stream(cuda) for _ in range(3)]
+        outs = [torch.empty((1, 256, n), device=cuda) for _ in range(blocks)]
+        bus = [torch.zeros((256, len(buses)), device=cuda) for _ in range(blocks)]
+        torch.cuda.synchronize()
+        for b in range(blocks):
+            sp, sm = (streams[(2 * b) % 3], streams[(2 * b + 1) % 3]) if rotate else (streams[0], streams[0])
+            e.process(None, out=outs[b], stream=sp.cuda_stream)
+            e.mix(outs[b], bus[b], stream=sm.cuda_stream)
+        torch.cuda.synchronize()
+        res.append((torch.cat(outs, 1).cpu().numpy(), torch.cat(bus, 0).cpu().numpy()))
+        e.close()
+    assert bits_equal(res[1][0], res[0][0]), first_mismatch(res[1][0], res[0][0])
+    assert bits_equal(res[1][1], res[0][1]), first_mismatch(res[1][1], res[0][1])
+    assert np.any(res[0][1] != 0)
+
+
 def test_reset_waits_for_the_engines_own_stream(cuda):
     """olfx_reset waits engine-scoped (the stream of its latest block, not the device): blocks
     queued on a caller stream without a host wait, then reset, then a block on the same stream --

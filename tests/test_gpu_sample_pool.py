@@ -133,3 +133,92 @@ def test_sample_pool_voices_instance_major(cuda, kind_name):
     assert not np.any(y[:L])
     assert bits_equal(y[L:], want[:T - L]), first_mismatch(y[L:], want[:T - L])
     assert np.any(want != 0)
+
+
+@pytest.mark.parametrize("depth", [1, 2])
+def test_sample_pool_call_order_across_boundary(cuda, depth):
+    """Frame-major calls on both sides of a block's last frame keep call order: object
+    0's mix set to 0.1 before its frame 255 and to 0.9 before its frame 256 both land at the
+    boundary 256, the later value winning; the same pair again across 511/512 (0.3, then 0.05).
+    Bit-exact against the oracle with those values from block 1 and block 2."""
+    lib = ofx.load()
+    B, n, T = 256, 2, 4 * 256
+    rng = np.random.default_rng(900 + depth)
+    p = chorus_params(rng, n)
+    ref = O.Chorus(n)
+    for i in range(n):
+        for f in range(p.shape[0]):
+            ref.set(i, f, float(p[f, i]))
+    calls = {255: 0.1, 256: 0.9, 511: 0.3, 512: 0.05}      # frame -> OLFX_CH_MIX of object 0
+    assert lib.olfx_sample_pool_config_depth(0, B, depth) == 0
+    try:
+        objs = _objects(lib, _lib.KIND_CHORUS, n, p)
+        x = (rng.random((2, T, n), dtype=np.float32) - 0.5).astype(np.float32)
+        y = np.zeros((2, T, n), np.float32)
+        fin, fout = (ctypes.c_float * 2)(), (ctypes.c_float * 2)()
+        for t in range(T):
+            for i, h in enumerate(objs):
+                if i == 0 and t in calls:
+                    assert lib.olfx_sample_set_param(h, 1, calls[t]) == 0
+                fin[0], fin[1] = float(x[0, t, i]), float(x[1, t, i])
+                assert lib.olfx_sample_process(h, fin, fout) == 0, (i, t)
+                y[0, t, i], y[1, t, i] = fout[0], fout[1]
+        for h in objs:
+            assert lib.olfx_sample_destroy(h) == 0
+    finally:
+        assert lib.olfx_sample_pool_config(0, B) == 0
+    parts = [ref.process(np.ascontiguousarray(x[:, :B]))]
+    ref.set(0, 1, 0.9)
+    parts.append(ref.process(np.ascontiguousarray(x[:, B:2 * B])))
+    ref.set(0, 1, 0.05)
+    parts.append(ref.process(np.ascontiguousarray(x[:, 2 * B:])))
+    want = np.concatenate(parts, 1)
+    L = depth * B
+    assert not np.any(y[:, :L])
+    assert bits_equal(y[:, L:], want[:, :T - L]), first_mismatch(y[:, L:], want[:, :T - L])
+
+
+@pytest.mark.parametrize("depth", [1, 2])
+def test_sample_pool_note_on_off_across_boundary(cuda, depth):
+    """A voice's NoteOn before its frame 255 and NoteOff before its frame 256 (frame-major, two
+    voices) both land at the boundary 256 in call order, so the voice is released there: output
+    bit-identical to one engine given NoteOn then NoteOff at block 1 (and the other voice's NoteOn
+    at block 0), delayed by the pool's latency."""
+    from test_gpu_parity import _voice_run, engine
+    from helpers import voice_configs
+    lib = ofx.load()
+    B, n, T = 256, 2, 4 * 256
+    cfg = voice_configs(np.random.default_rng(950 + depth), n)
+    assert lib.olfx_sample_pool_config_depth(0, B, depth) == 0
+    try:
+        objs = _objects(lib, _lib.KIND_VOICE, n, cfg)
+        y = np.zeros((T, n), np.float32)
+        fout = (ctypes.c_float * 1)()
+        for t in range(T):
+            for i, h in enumerate(objs):
+                if t == 0 and i == 1:
+                    assert lib.olfx_sample_note(h, 1, 64, 100) == 0
+                if t == 255 and i == 0:
+                    assert lib.olfx_sample_note(h, 1, 60, 100) == 0
+                if t == 256 and i == 0:
+                    assert lib.olfx_sample_note(h, 0, 60, 0) == 0
+                assert lib.olfx_sample_process(h, None, fout) == 0, (i, t)
+                y[t, i] = fout[0]
+        for h in objs:
+            assert lib.olfx_sample_destroy(h) == 0
+    finally:
+        assert lib.olfx_sample_pool_config(0, B) == 0
+    e = engine("voice", n)
+    e.set_params(0, cfg)
+    e.note_events([(1, 1, 64)])
+    blocks = []
+    for b in range(T // B):
+        if b == 1:
+            e.note_events([(0, 1, 60)])
+            e.note_events([(0, 0, 60)])
+        blocks.append(_voice_run(e, B, cuda)[0])
+    want = np.concatenate(blocks, 0)
+    L = depth * B
+    assert not np.any(y[:L])
+    assert bits_equal(y[L:], want[:T - L]), first_mismatch(y[L:], want[:T - L])
+    assert np.any(want[:, 1] != 0)
