@@ -166,17 +166,15 @@ def _oracle():
 
 
 def _rcp_table():
-    """v_rcp_f32's results over the mantissas of [1, 2), read from the device by the test helper
-    tests/gpu_probe/librcp_probe.so (the voice oracle's kernel-arithmetic model, oracle/voice_ref.c);
-    None when the helper is not built."""
-    import ctypes
-    path = os.path.join(ROOT, "tests", "gpu_probe", "librcp_probe.so")
-    if not os.path.exists(path):
+    """The committed v_rcp_f32 model of gfx950 (tests/golden/rcp_f32_gfx950.npz through
+    oracle/rcp_model.py, sha256-checked: the voice oracle's kernel-arithmetic mode,
+    oracle/voice_ref.c); None when the fixture is absent."""
+    try:
+        _oracle()
+        import rcp_model
+        return rcp_model.load()
+    except (OSError, ValueError, ImportError):
         return None
-    L = ctypes.CDLL(path)
-    L.probe_rcp_table.argtypes = [ctypes.c_void_p]
-    tab = np.empty(1 << 23, np.uint32)
-    return tab if L.probe_rcp_table(tab.ctypes.data) == 0 else None
 
 
 def _oracle_bank(kind: str, p: np.ndarray, sr: float, o0: bool = False, ref: bool = False, notes=None,
@@ -580,7 +578,7 @@ class Leg:
         """One region of exactly `steps` steps.  Kernel time: ONE event pair on the launch stream
         around the region (GPU time per step = the launch duration plus the gap between launches; a
         pair per step would add two timestamp markers between consecutive kernels, ~3-4 us each on
-        the command processor, 10-20 % of a 35 us voice block: tools/loop_probe.py)."""
+        the command processor, 10-20 % of a 35 us voice block: notes r5 §4)."""
         import torch
 
         from ol_dsp_amd.dist import RunStats, reduce_stats

@@ -24,6 +24,7 @@
 #include <type_traits>
 
 #include "olfx_internal.h"
+#include "lds_flags.h"
 
 namespace olfx {
 namespace dt {
@@ -87,6 +88,31 @@ struct Tap {
     }
     // the ring's write, for a ring with this one tap (IN1)
     __device__ __forceinline__ void write(const DattorroArgs &a, uint32_t gw, uint32_t i, float4 v) { *grpu<L>(a, gw, i) = v; }
+};
+
+// A fixed tap prefetched TWO steps ahead (the split network's tank halves, whose register sets have
+// room for it): p1 = the group step s + 1 needs, loaded a step ago; p2, loaded at step s for s + 2.
+// Every fixed delay is >= 121 positions, so no prefetched group is written by the steps before it.
+template <int L, uint32_t D, uint32_t OFF>
+struct Tap2 {
+    static constexpr uint32_t S = (OFF - D) & 3u;
+    float4 cur, nxt, p1, p2;
+    __device__ __forceinline__ static uint32_t g0(uint32_t t0) { return (t0 + OFF - D) >> 2; }
+    __device__ __forceinline__ void prime(const DattorroArgs &a, uint32_t t0, uint32_t i) {
+        cur = *grpu<L>(a, g0(t0), i);
+        if (S) nxt = *grpu<L>(a, g0(t0) + 1u, i);
+        p1 = *grpu<L>(a, g0(t0) + (S ? 2u : 1u), i);
+    }
+    __device__ __forceinline__ void prefetch(const DattorroArgs &a, uint32_t t0, uint32_t i) {
+        p2 = *grpu<L>(a, g0(t0) + (S ? 3u : 2u), i);
+    }
+    __device__ __forceinline__ float get(int k) const {
+        return (int)S + k < 4 ? el(cur, (int)S + k) : el(nxt, (int)S + k - 4);
+    }
+    __device__ __forceinline__ void advance() {
+        if (S) { cur = nxt; nxt = p1; } else { cur = p1; }
+        p1 = p2;
+    }
 };
 
 // A fixed tap whose whole ring lives in LDS for the launch (the standalone reverb's IN1, 128
@@ -228,57 +254,7 @@ struct PreTap {
     }
 };
 
-// Gather mode with unaligned rows (per-instance pre-delays, verb.cpp:137-139): dattorro_predelay_v2 has already written
-// the block's pre-delayed input, group by group, to a.pre_block ([n_frames/4][n][4]: 16 B per lane
-// and chunk, coalesced) and kept the ring itself, instance-major.  The network reads that stream:
-// no gather across lines here, and no ring write.
-struct PreBlock {
-    float4 cur, pre;
-    uint32_t t0, last;
-    __device__ __forceinline__ void prime(const DattorroArgs &a, uint32_t t0_, uint32_t d, uint32_t i) {
-        (void)d;
-        t0 = t0_;
-        last = a.n_frames / 4u - 1u;
-        cur = ((const float4 *)a.pre_block)[i];
-    }
-    __device__ __forceinline__ void prefetch(const DattorroArgs &a, uint32_t t, uint32_t d, uint32_t i) {
-        (void)d;
-        const uint32_t g = min(((t - t0) >> 2) + 1u, last);
-        pre = ((const float4 *)a.pre_block)[(size_t)g * a.n + i];
-    }
-    __device__ __forceinline__ void resolve(const float (&xin)[4], uint32_t d, float (&xpd)[4]) const {
-        (void)xin; (void)d;
-        xpd[0] = cur.x; xpd[1] = cur.y; xpd[2] = cur.z; xpd[3] = cur.w;
-    }
-    __device__ __forceinline__ void advance(const float (&xin)[4]) { (void)xin; cur = pre; }
-    __device__ __forceinline__ void write(const DattorroArgs &, uint32_t, uint32_t, const float (&)[4]) const {}
-};
-
-// Fused gather mode (dattorro_block_v4f, dattorro.hip): the kernel itself keeps, per 32-frame
-// piece, the piece's mono input (M) and each instance's window of its pre-delay ring (W, the 36
-// positions from (T - d) & ~3) in LDS, filled one piece ahead.  Frame t of the piece (t = T + f)
-// reads x[t - d]: from M when t - d >= T (d <= f: this piece's own input), else from W.  The
-// caller points m / w at the lane's rows and sets fc (the chunk's first frame within the piece)
-// and off0 ((T - d) & 3) before each dt_step.
-struct PreFused {
-    const float *m, *w;
-    int fc;
-    uint32_t off0;
-    __device__ __forceinline__ void prime(const DattorroArgs &, uint32_t, uint32_t, uint32_t) {}
-    __device__ __forceinline__ void prefetch(const DattorroArgs &, uint32_t, uint32_t, uint32_t) {}
-    __device__ __forceinline__ void resolve(const float (&)[4], uint32_t d, float (&xpd)[4]) const {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int q = fc + k - (int)d;
-            const float *src = q >= 0 ? m + q : w + (off0 + (uint32_t)(fc + k));
-            xpd[k] = *src;
-        }
-    }
-    __device__ __forceinline__ void advance(const float (&)[4]) {}
-    __device__ __forceinline__ void write(const DattorroArgs &, uint32_t, uint32_t, const float (&)[4]) const {}
-};
-
-// The fused chain's pre-delay tap (chain.hip, round 5).  The chain keeps its pre-delay ring in ROWS
+// The pre-delay tap over rows (round 5 in the fused chain; round 6 also dattorro_block_v5).  The chain keeps its pre-delay ring in ROWS
 // of 16 positions ([8192/16][n][16]: 64 B per instance and row, a workgroup's 64 rows one 4-KB
 // run), so whatever the instances' pre-delays, a 16-frame chunk needs one new row per instance: 64 B
 // that one HBM request serves whole (the position-major groups of PreTap, read at 64 different
@@ -419,6 +395,299 @@ __device__ __forceinline__ void step_body(
     ap1a.advance();
     ap1b.advance();
     pre.advance(xin);
+}
+
+// ---------------------------------------------------------------------------------------------
+// The split network (round 6): DI, TA and TB as three waves (dattorro_block_v5, the chain's reverb
+// roles).  Within a launch of at most kSplitMaxFrames frames the network is three independent
+// recurrences joined only by feed-forward values:
+//   DI: pre-delay, pre-LPF and the 4 input all-passes (verb.cpp:273-282) -> x;
+//   TA: tank half 0 (verb.cpp:284-295, i = 0): AP1A, DL1A, damping, AP2A, DL2A;
+//   TB: tank half 1: AP1B, DL1B, damping, AP2B, DL2B.
+// The halves exchange data only through postDampingDelay[1 - i]'s main tap (verb.cpp:286), 3163
+// (TA reads DL2B) and 3720 (TB reads DL2A) samples back: within a launch shorter than that they
+// read only what earlier launches wrote, and each wave reads back only rings it writes itself.  x
+// goes to both halves through an LDS queue.  The stereo taps (verb.cpp:302-325) split at their sum
+// order: L = pL - oL5 - oL6 + oL7 with pL = oL1 + oL2 - oL3 + oL4 on half 1's rings and oL5..7 on
+// half 0's; R the mirror image.  So half 1 sends pL to half 0, which finishes L, and half 0 sends pR
+// to half 1, which finishes R (one float per frame each way, through LDS, one step late so neither
+// waits on the other's current step) -- the reference's additions in the reference's order.
+// Per 4-frame step: DI 5 taps, each half 11 (3 network + 1 modulated + 7 output) and 4 ring writes.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kSplitDepth = 4;          // LDS queue slots (4-frame steps) per hand-off
+constexpr uint32_t kSplitMaxFrames = 2048;   // < 3163 - queue skew: no cross-half read within a launch
+// progress counters (lds_flags.h), in steps: SPF_X x published by DI; SPF_XT<h> x taken by half h;
+// SPF_P<h> partial sums half h has published; SPF_PT<h> half h's partials the other half has taken
+enum { SPF_X = 0, SPF_XT0, SPF_XT1, SPF_P0, SPF_P1, SPF_PT0, SPF_PT1, SPF_N };
+
+struct SplitQ {
+    const float4 *qx;   // [kSplitDepth][64]: x of a step per lane
+    float4 *mine;       // this half's partial sums
+    const float4 *other;
+    uint32_t *flags;
+};
+
+__device__ __forceinline__ float4 f4(const float (&v)[4]) { return make_float4(v[0], v[1], v[2], v[3]); }
+
+// The taps of tank half H.  P1..P4: the partial sum this half sends (half 0: pR = oR1 + oR2 - oR3 +
+// oR4 on DL1A, DL1A, AP2A, DL2A; half 1: pL = oL1 + oL2 - oL3 + oL4 on DL1B, DL1B, AP2B, DL2B);
+// T5..T7: the terms that finish the other half's sum into this half's channel (half 0, L: oL5 DL1A,
+// oL6 AP2A, oL7 DL2A; half 1, R: oR5 DL1B, oR6 AP2B, oR7 DL2B).
+template <int H> struct SplitHalf;
+template <> struct SplitHalf<0> {
+    static constexpr int kAP1 = DT_AP1A, kDL1 = DT_DL1A, kAP2 = DT_AP2A, kDL2 = DT_DL2A, kLp = DTS_LP_DAMP_A;
+    using FB = Tap<DT_DL2B, 3163, 0>;
+    using DL1 = Tap<DT_DL1A, 4453, 0>;
+    using AP2 = Tap<DT_AP2A, 1800, 0>;
+    using AP1 = ModTap<DT_AP1A, kDtDelay[DT_AP1A]>;
+    using P1 = Tap<DT_DL1A, kDl1A_o1, 1>;
+    using P2 = Tap<DT_DL1A, kDl1A_o2, 1>;
+    using P3 = Tap<DT_AP2A, kAp2A_o2, 1>;
+    using P4 = Tap<DT_DL2A, kDl2A_o2, 1>;
+    using T5 = Tap<DT_DL1A, kDl1A_o3, 1>;
+    using T6 = Tap<DT_AP2A, kAp2A_o1, 1>;
+    using T7 = Tap<DT_DL2A, kDl2A_o1, 1>;
+};
+template <> struct SplitHalf<1> {
+    static constexpr int kAP1 = DT_AP1B, kDL1 = DT_DL1B, kAP2 = DT_AP2B, kDL2 = DT_DL2B, kLp = DTS_LP_DAMP_B;
+    using FB = Tap<DT_DL2A, 3720, 0>;
+    using DL1 = Tap<DT_DL1B, 4217, 0>;
+    using AP2 = Tap<DT_AP2B, 2656, 0>;
+    using AP1 = ModTap<DT_AP1B, kDtDelay[DT_AP1B]>;
+    using P1 = Tap<DT_DL1B, kDl1B_o1, 1>;
+    using P2 = Tap<DT_DL1B, kDl1B_o2, 1>;
+    using P3 = Tap<DT_AP2B, kAp2B_o2, 1>;
+    using P4 = Tap<DT_DL2B, kDl2B_o2, 1>;
+    using T5 = Tap<DT_DL1B, kDl1B_o3, 1>;
+    using T6 = Tap<DT_AP2B, kAp2B_o1, 1>;
+    using T7 = Tap<DT_DL2B, kDl2B_o1, 1>;
+};
+
+// DI's arithmetic for one 4-frame step (verb.cpp:275-282): the pre-delayed input xpd through the
+// pre-LPF and the 4 input all-passes -> x (xo), and the groups the step writes to IN0..IN3
+template <class T0, class T1, class T2, class T3>
+__device__ __forceinline__ void di_compute(const float (&xpd)[4], float &lp_pre, float g_pre, float g_in1, float g_in2,
+                                           T0 &in0, T1 &in1, T2 &in2, T3 &in3, float (&w0)[4], float (&w1)[4],
+                                           float (&w2)[4], float (&w3)[4], float (&xo)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        lp_pre += (xpd[k] - lp_pre) * g_pre;
+        float x = lp_pre;
+        float d = in0.get(k);
+        x += d * -g_in1; w0[k] = x; x = d + x * g_in1;
+        d = in1.get(k);
+        x += d * -g_in1; w1[k] = x; x = d + x * g_in1;
+        d = in2.get(k);
+        x += d * -g_in2; w2[k] = x; x = d + x * g_in2;
+        d = in3.get(k);
+        x += d * -g_in2; w3[k] = x; x = d + x * g_in2;
+        xo[k] = x;
+    }
+}
+
+// DI hands step gs's x to both halves (once both have taken step gs - kSplitDepth's)
+__device__ __forceinline__ void split_publish_x(float4 *qx, uint32_t *flags, uint32_t lane, uint32_t gs,
+                                                const float (&xo)[4]) {
+    wait_for([&] {
+        return flag_get(flags + SPF_XT0) + kSplitDepth > gs && flag_get(flags + SPF_XT1) + kSplitDepth > gs;
+    });
+    qx[(gs % kSplitDepth) * 64u + lane] = f4(xo);
+    flag_put(flags + SPF_X, gs + 1);
+}
+
+__device__ __forceinline__ void wsync() {      // LDS written by some lanes, read by others
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// DI over the pre-delay ring in ROWS of 16 positions ([8192/16][n][16], PreRow above) for the
+// instances 64 g .. 64 g + 63 (those >= d.n mirror instance d.n - 1 and store nothing): whatever
+// the instances' pre-delays, a 16-frame chunk costs one 64-B row per instance (verb.cpp:137-139,
+// :273).  stage: 25 x 64 float4 of LDS (far 17 x 64, near 8 x 64).  src(c, f0, C, xm) gives chunk c's
+// mono input xm[16] (frames f0 .. f0 + 15 of the launch, C of them real).  in1: IN1's tap, an HBM Tap
+// or an LdsTap (its write goes where it reads).  Each step's x goes to the tank halves through qx
+// (step numbers from gs0).
+template <class In1T, class Src>
+__device__ __forceinline__ void split_di_rows(const DattorroArgs &d, uint32_t g, uint32_t lane, uint32_t nf,
+                                              uint32_t gs0, float4 *stage, float4 *qx, uint32_t *flags,
+                                              In1T &in1, Src &&src) {
+    constexpr uint32_t kChunk = 16;
+    constexpr uint32_t kRows = kDtSize[DT_PRE] / 16u;
+    const uint32_t nd = d.n, base = g * 64u;
+    const uint32_t i = min(base + lane, nd - 1u);
+    const uint32_t cj = lane >> 2, cg = lane & 3u;
+    float4 *const far = stage, *const near = stage + 17 * 64;
+    const float g_pre = d.coef[DTC_PREFILTER * nd + i];
+    const float g_in1 = d.coef[DTC_IN1 * nd + i];
+    const float g_in2 = d.coef[DTC_IN2 * nd + i];
+    const uint32_t dpre = (uint32_t)d.coef[DTC_PREDELAY * nd + i];
+    float lp_pre = d.state[DTS_LP_PRE * nd + i];
+    Tap<DT_IN0, 142, 0> in0; Tap<DT_IN2, 379, 0> in2; Tap<DT_IN3, 277, 0> in3;
+    PreRow pre;
+    const uint32_t t0 = d.t0;
+    in0.prime(d, t0, i); in1.prime(d, t0, i); in2.prime(d, t0, i); in3.prime(d, t0, i);
+    float4 *const ring = (float4 *)d.ring[DT_PRE];    // row r of instance j: ring + (r * nd + j) * 4
+    uint32_t dj[4], jc[4];                            // cooperative instance 16 m + l / 4: its pre-delay, its index
+    bool jl[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        dj[m] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((16u * m + cj) << 2), (int)dpre);
+        jl[m] = base + 16u * m + cj < nd;
+        jc[m] = min(base + 16u * m + cj, nd - 1u);
+    }
+    pre.near = near + lane;
+    pre.far = far + lane;
+    pre.farw = far + lane;
+    pre.ring = ring + (size_t)i * 4u;
+    pre.nd = nd;
+    pre.pv = make_float4(0.f, 0.f, 0.f, 0.f);
+    pre.pslot = 16u * 64u;                            // junk: nothing loaded yet
+    auto row_ptr = [&](uint32_t row, int m) { return ring + ((size_t)(row & (kRows - 1u)) * nd + jc[m]) * 4u + cg; };
+    auto put_row = [&](uint32_t T, uint32_t plus, int m) {   // group cg of row ((T - d) >> 4) + plus -> far
+        const uint32_t row = ((T - dj[m]) >> 4) + plus;
+        far[((row & 3u) * 4u + cg) * 64u + 16u * m + cj] = *row_ptr(row, m);
+    };
+    auto ring_at = [&](uint32_t T, int m) {           // group cg of positions T .. T + 15 in the ring
+        const uint32_t P = T + 4u * cg;
+        return ring + ((size_t)((P >> 4) & (kRows - 1u)) * nd + jc[m]) * 4u + ((P >> 2) & 3u);
+    };
+    auto near_at = [&](uint32_t T, int m) { return near + (((T >> 2) + cg) & 7u) * 64u + 16u * m + cj; };
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        put_row(t0, 0, m);
+        put_row(t0, 1, m);
+        *near_at(t0 - kChunk, m) = *ring_at(t0 - kChunk, m);
+    }
+    const uint32_t nchunks = (nf + kChunk - 1) / kChunk;
+    for (uint32_t c = 0; c < nchunks; ++c) {
+        const uint32_t f0 = c * kChunk, T = t0 + f0;
+        const uint32_t C = min(kChunk, nf - f0);
+        float xm[kChunk];
+        src(c, f0, C, xm);
+        // the chunk's input -> near (over the chunk before the one before), then into the ring
+        // cooperatively (groups past a short chunk's C frames stay); the next rows' loads, issued
+        // during the steps below, see these stores (one wave, issue order)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            near[(((T >> 2) + (uint32_t)m) & 7u) * 64u + lane] = make_float4(xm[4 * m], xm[4 * m + 1], xm[4 * m + 2], xm[4 * m + 3]);
+        wsync();
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const float4 v = *near_at(T, m);
+            if (4u * cg < C && jl[m]) *ring_at(T, m) = v;
+        }
+        pre.T = T;
+        for (uint32_t s = 0; s < C; s += 4) {
+            const uint32_t t = T + s;
+            float xin[4], xpd[4], w0[4], w1[4], w2[4], w3[4], xo[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) xin[k] = xm[s + k];
+            pre.fc = (int)s;
+            in0.prefetch(d, t, i); in1.prefetch(d, t, i); in2.prefetch(d, t, i); in3.prefetch(d, t, i);
+            pre.prefetch(d, t, dpre, i);
+            pre.resolve(xin, dpre, xpd);
+            di_compute(xpd, lp_pre, g_pre, g_in1, g_in2, in0, in1, in2, in3, w0, w1, w2, w3, xo);
+            const uint32_t gw = t >> 2;
+            *grpu<DT_IN0>(d, gw, i) = f4(w0);
+            in1.write(d, gw, i, f4(w1));
+            *grpu<DT_IN2>(d, gw, i) = f4(w2);
+            *grpu<DT_IN3>(d, gw, i) = f4(w3);
+            split_publish_x(qx, flags, lane, gs0 + (f0 + s) / 4u, xo);
+            in0.advance(); in1.advance(); in2.advance(); in3.advance();
+        }
+        wsync();                                      // this chunk's LDS reads before the next one's writes
+    }
+    if (base + lane < nd) d.state[DTS_LP_PRE * nd + i] = lp_pre;
+}
+
+// Tank half H of instance i over `steps` 4-frame steps from stream time t0; gs0 = the queues' step
+// number of its first step (a workgroup's instance groups run back to back in the chain).  Channel
+// H of frame f goes to out[f * out_n + i] for live lanes (out: the channel's plane).
+template <int H>
+__device__ __forceinline__ void split_tank(const DattorroArgs &a, uint32_t i, uint32_t lane, bool live, uint32_t t0,
+                                           uint32_t steps, uint32_t gs0, float *out, uint32_t out_n,
+                                           const SplitQ &q) {
+    using Hf = SplitHalf<H>;
+    const uint32_t n = a.n;
+    const float g_dd1 = a.coef[DTC_DD1 * n + i];
+    const float g_damp = a.coef[DTC_DAMPING * n + i];
+    const float g_decay = a.coef[DTC_DECAY * n + i];
+    const float g_dd2 = a.coef[DTC_DD2 * n + i];
+    float lp = a.state[Hf::kLp * n + i];
+    typename Hf::FB fb; typename Hf::DL1 dl1; typename Hf::AP2 ap2; typename Hf::AP1 ap1;
+    typename Hf::P1 p1; typename Hf::P2 p2; typename Hf::P3 p3; typename Hf::P4 p4;
+    typename Hf::T5 t5; typename Hf::T6 t6; typename Hf::T7 t7;
+#define SPLIT_TAPS(OP) OP(fb) OP(dl1) OP(ap2) OP(p1) OP(p2) OP(p3) OP(p4) OP(t5) OP(t6) OP(t7)
+#define SPLIT_PRIME(T) T.prime(a, t0, i);
+#define SPLIT_PREFETCH(T) T.prefetch(a, t, i);
+#define SPLIT_ADVANCE(T) T.advance();
+    SPLIT_TAPS(SPLIT_PRIME)
+    ap1.prime(a, t0, i);
+    uint32_t *const flags = q.flags;
+    float q5[4], q6[4], q7[4];                        // the previous step's finishing terms
+    auto finish = [&](uint32_t s) {                   // channel H of step s: the other half's partial + q5..q7
+        const uint32_t gs = gs0 + s;
+        wait_for([&] { return flag_get(flags + SPF_P0 + (1 - H)) > gs; });
+        const float4 po = q.other[(gs % kSplitDepth) * 64u + lane];
+        flag_put(flags + SPF_PT0 + (1 - H), gs + 1);
+        const float pv[4] = {po.x, po.y, po.z, po.w};
+        if (live) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float o = pv[k];
+                o -= q5[k]; o -= q6[k]; o += q7[k];
+                out[(size_t)(4u * s + (uint32_t)k) * out_n + i] = o;
+            }
+        }
+    };
+    for (uint32_t s = 0; s < steps; ++s) {
+        const uint32_t t = t0 + 4u * s, gs = gs0 + s, slot = gs % kSplitDepth;
+        SPLIT_TAPS(SPLIT_PREFETCH)
+        ap1.prefetch(a, t, i);
+        ap1.resolve();
+        wait_for([&] { return flag_get(flags + SPF_X) > gs; });
+        const float4 xv = q.qx[slot * 64u + lane];
+        flag_put(flags + SPF_XT0 + H, gs + 1);
+        const float x[4] = {xv.x, xv.y, xv.z, xv.w};
+        float w_ap1[4], w_dl1[4], w_ap2[4], w_dl2[4], pm[4], n5[4], n6[4], n7[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {                 // verb.cpp:286-294; the APF gain is -dd1
+            float y = x[k] + fb.get(k) * g_decay;
+            float d = ap1.v[k];
+            y += d * g_dd1; w_ap1[k] = y; y = d + y * -g_dd1;
+            w_dl1[k] = y;
+            lp += (dl1.get(k) - lp) * g_damp;
+            y = lp * g_decay;
+            d = ap2.get(k);
+            y += d * -g_dd2; w_ap2[k] = y; y = d + y * g_dd2;
+            w_dl2[k] = y;
+            float p = p1.get(k);
+            p += p2.get(k); p -= p3.get(k); p += p4.get(k);
+            pm[k] = p;
+            n5[k] = t5.get(k); n6[k] = t6.get(k); n7[k] = t7.get(k);
+        }
+        const uint32_t gw = t >> 2;
+        *grpu<Hf::kAP1>(a, gw, i) = f4(w_ap1);
+        *grpu<Hf::kDL1>(a, gw, i) = f4(w_dl1);
+        *grpu<Hf::kAP2>(a, gw, i) = f4(w_ap2);
+        *grpu<Hf::kDL2>(a, gw, i) = f4(w_dl2);
+        // this step's partial out, then the previous step's channel
+        wait_for([&] { return flag_get(flags + SPF_PT0 + H) + kSplitDepth > gs; });
+        q.mine[slot * 64u + lane] = f4(pm);
+        flag_put(flags + SPF_P0 + H, gs + 1);
+        if (s > 0) finish(s - 1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { q5[k] = n5[k]; q6[k] = n6[k]; q7[k] = n7[k]; }
+        SPLIT_TAPS(SPLIT_ADVANCE)
+        ap1.advance();
+    }
+    if (steps) finish(steps - 1);
+    if (live) a.state[Hf::kLp * n + i] = lp;
+#undef SPLIT_TAPS
+#undef SPLIT_PRIME
+#undef SPLIT_PREFETCH
+#undef SPLIT_ADVANCE
 }
 
 }  // namespace dt

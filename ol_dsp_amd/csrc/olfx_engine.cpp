@@ -440,10 +440,9 @@ struct olfx_engine {
     float *dt_rings = nullptr;
     // standalone reverb, per-instance pre-delays (dattorro.hip gather mode): the instance-major
     // pre-delay ring and the block's pre-delayed input, allocated on first need
-    float *dt_pre_im = nullptr, *dt_pre_blk = nullptr;
-    bool dt_gather = false;      // the pre-delay ring's content is instance-major (dt_pre_im)
-    int dt_pre_kernel = 3;       // gather mode's kernel at the last block (predelay_kernel: 3 fused v4f, 2 v2 + network)
-    bool dt_pre_check = true;    // a pre-delay changed: re-decide the mode at the next block
+    float *dt_pre_tmp = nullptr; // a copy of the pre-delay ring while its layout changes
+    bool dt_rows = false;        // the pre-delay ring's layout: rows (dattorro_block_v5) or position-major (v4)
+    bool dt_pre_check = true;    // a pre-delay changed: re-decide the network at the next block
     float *dt_state = nullptr;
     float *dt_coef = nullptr;
 
@@ -880,7 +879,7 @@ int init_state(olfx_engine *e) {
         std::fill(e->params.begin() + (size_t)f * e->n, e->params.begin() + (size_t)(f + 1) * e->n, d[f]);
     e->configured.assign(e->n, 0);
     e->n_components = 0;
-    e->dt_gather = false;          // the zeroed ring is position-major again
+    e->dt_rows = false;            // the zeroed ring is valid in either layout: decided at the next block
     e->dt_pre_check = true;
     e->events.clear();
     e->ev_slot.assign(e->n, -1);
@@ -934,6 +933,7 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, uin
         a.n_frames = n_frames;
         a.t0 = t0 & 0xFFFFu;
         a.in_ch = 2;
+        a.cus = (uint32_t)e->cus;
         return a;
     };
     auto ch_args = [&](float *pr, float *cr, uint32_t *st, const uint32_t *cf, const float *in,
@@ -957,39 +957,24 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, uin
     switch (e->kind) {
     case OLFX_KIND_DATTORRO: {
         if (e->dt_pre_check) {
-            // one pre-delay for all instances: the position-major ring and its coalesced tap;
-            // several: gather mode (dattorro.hip), its ring instance-major
+            // one pre-delay for all instances or several: the network (dattorro.hip dattorro_rows)
+            // and so the pre-delay ring's layout; its content is converted when that changes
             e->dt_pre_check = false;
             const float *pd = e->params.data() + (size_t)OLFX_DT_PREDELAY * e->n;
             const uint32_t d0 = dattorro_predelay_samples(pd[0]);
             bool uniform = true;
             for (uint32_t i = 1; i < e->n && uniform; ++i) uniform = dattorro_predelay_samples(pd[i]) == d0;
-            if (uniform == e->dt_gather) {
-                if (!e->dt_pre_im) HIPCHK(e, hipMalloc((void **)&e->dt_pre_im, (size_t)kDtSize[DT_PRE] * e->n * 4));
-                DattorroArgs ca = dt_args(nullptr, nullptr);
-                ca.pre_im = e->dt_pre_im;
-                // the ring's content into the other layout, on the stream, ahead of this block
-                r = launch_dattorro_pre_convert(ca, !uniform, s);
-                if (r != hipSuccess) return e->hip_fail(r, "pre-delay ring conversion");
-                e->dt_gather = !uniform;
+            const bool rows = dattorro_rows(e->n_dt, (uint32_t)e->cus, uniform);
+            if (rows != e->dt_rows) {
+                if (e->frames > 0) {      // a fresh (zeroed) ring needs no conversion
+                    if (!e->dt_pre_tmp) HIPCHK(e, hipMalloc((void **)&e->dt_pre_tmp, (size_t)kDtSize[DT_PRE] * e->n_dt * 4));
+                    r = launch_dattorro_pre_layout(dt_args(nullptr, nullptr), e->dt_pre_tmp, rows, s);
+                    if (r != hipSuccess) return e->hip_fail(r, "pre-delay ring layout");
+                }
+                e->dt_rows = rows;
             }
         }
-        if (!e->dt_gather) {
-            r = launch_dattorro(dt_args(din, dout), s);
-            break;
-        }
-        for (uint32_t f0 = 0; f0 < n_frames && r == hipSuccess; f0 += 256) {   // dt_pre_blk holds 256 frames
-            DattorroArgs ga = dt_args(din + (size_t)f0 * e->n, dout + (size_t)f0 * e->n);
-            ga.n_frames = std::min(256u, n_frames - f0);
-            ga.t0 = (t0 + f0) & 0xFFFFu;
-            ga.pre_im = e->dt_pre_im;
-            e->dt_pre_kernel = predelay_kernel(ga.n, ga.plane, ga.in);
-            // the pre-pass's block (v2 + network, unaligned rows only; the fused v4f needs none)
-            if (e->dt_pre_kernel == 2 && !e->dt_pre_blk)
-                HIPCHK(e, hipMalloc((void **)&e->dt_pre_blk, (size_t)256 * e->n * 4));
-            ga.pre_block = e->dt_pre_blk;
-            r = launch_dattorro(ga, s);
-        }
+        r = launch_dattorro(dt_args(din, dout), e->dt_rows, s);
         break;
     }
     case OLFX_KIND_CHORUS:
@@ -1291,8 +1276,7 @@ int olfx_destroy(olfx_engine *e) {
         if (sl.consumed) (void)hipEventDestroy(sl.consumed);
     });
     if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
-    if (e->dt_pre_im) (void)hipFree(e->dt_pre_im);
-    if (e->dt_pre_blk) (void)hipFree(e->dt_pre_blk);
+    if (e->dt_pre_tmp) (void)hipFree(e->dt_pre_tmp);
     if (e->tile_in) (void)hipFree(e->tile_in);
     if (e->tile_out) (void)hipFree(e->tile_out);
     if (e->d_mem) (void)hipFree(e->d_mem);
@@ -1756,15 +1740,13 @@ double olfx_algorithmic_read_bytes_per_frame(const olfx_engine *e) {
 const char *olfx_kernel_name(const olfx_engine *e) {
     if (!e) return "";
     switch (e->kind) {
-    case OLFX_KIND_DATTORRO:   // gather mode: the fused network (aligned rows) or the pre-pass + network
-        return !e->dt_gather ? dattorro_uniform_kernel()
-               : e->dt_pre_kernel == 3 ? "dattorro_block_v4f"
-                                       : "dattorro_predelay_v2+dattorro_block_v4";
+    case OLFX_KIND_DATTORRO:   // the network of the last block (dattorro.hip dattorro_rows)
+        return e->dt_rows ? "dattorro_block_v5" : "dattorro_block_v4";
     case OLFX_KIND_CHORUS:
     case OLFX_KIND_PITCHSHIFT: return "chorus_block_v11";
     case OLFX_KIND_VOICE: return "voice_block_v5";
     case OLFX_KIND_VOICE_MOOG: return "voice_block_v4";
-    case OLFX_KIND_CHAIN: return "chain_block_v5";
+    case OLFX_KIND_CHAIN: return chain_kernel();
     case OLFX_KIND_FXRACK: return "fxrack_block_v3";
     default: return "";
     }

@@ -80,18 +80,13 @@ struct DattorroArgs {
     uint32_t n_frames;
     uint32_t t0;                // stream time (frames since create) of the first frame, mod 2^16
     uint32_t in_ch;             // 1 or 2
-    // gather mode (standalone reverb with per-instance pre-delays, dattorro.hip): the pre-delay
-    // ring instance-major ([n][8192]); with unaligned audio rows also the block's pre-delayed input
-    // ([n_frames/4][n][4]) written by dattorro_predelay_v2 ahead of the network; nullptr otherwise
-    float *pre_im;
-    float *pre_block;
+    uint32_t cus;               // compute units of the device (olfx_create)
 };
-// standalone reverb: the pre-delay ring's layout changed between position-major (uniform
-// pre-delays, dattorro_block_v4's own tap) and instance-major (gather mode): the ring's content
-// is copied into the other layout (to_im: position-major -> instance-major)
-hipError_t launch_dattorro_pre_convert(const DattorroArgs &a, bool to_im, hipStream_t s);
-// gather mode's pre-delay pass for these rows: 3 (16-B aligned input rows), else 2
-int predelay_kernel(uint32_t n, uint64_t plane, const float *in);
+// Standalone reverb: the network for these pre-delays (dattorro.hip): true = dattorro_block_v5 with
+// the pre-delay ring in rows ([8192/16][n][16]), false = dattorro_block_v4, ring position-major
+bool dattorro_rows(uint32_t n, uint32_t cus, bool uniform);
+// the pre-delay ring's content into the other layout (tmp: a device buffer of the ring's size)
+hipError_t launch_dattorro_pre_layout(const DattorroArgs &a, float *tmp, bool to_rows, hipStream_t s);
 
 // ----------------------------------------------------------------------------------------------
 // Deterministic cos(2*pi*x): used by the chorus LFO (RNBO cycle~).  Branch-free (selects only, no
@@ -381,9 +376,9 @@ struct ChainArgs {
     uint32_t cus;               // compute units of the device (the persistent grid), from olfx_create
 };
 
-hipError_t launch_dattorro(const DattorroArgs &a, hipStream_t s);
-const char *dattorro_uniform_kernel();   // the uniform-mode network launch_dattorro runs
+hipError_t launch_dattorro(const DattorroArgs &a, bool rows, hipStream_t s);
 hipError_t launch_chain(const ChainArgs &a, hipStream_t s);
+const char *chain_kernel();              // the chain kernel launch_chain runs
 hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s);
 // the chorus kernel launch_chorus picks for n instances, ring sizes and cooperative I/O
 

@@ -1,4 +1,5 @@
-"""The committed v_rcp_f32 model of gfx950 (TEST INFRASTRUCTURE).
+"""oracle/rcp_model.py -- the committed v_rcp_f32 model of gfx950 (TEST INFRASTRUCTURE: the
+checker's data, never loaded by the product).
 
 The voice oracle's kernel-arithmetic mode (oracle/voice_ref.c) needs what gfx950's v_rcp_f32
 returns for every mantissa of [1, 2).  The instruction is within one ulp of the correctly rounded
@@ -11,7 +12,8 @@ import os
 
 import numpy as np
 
-PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "rcp_f32_gfx950.npz")
+PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                    "rcp_f32_gfx950.npz")
 
 
 def correctly_rounded() -> np.ndarray:

@@ -122,7 +122,7 @@ def test_full_size_stream_kinds(cuda, kind, n):
 @pytest.mark.parametrize("pset,kind", [("dattorro_rpd", "dattorro"), ("chain_rpd", "chain")])
 def test_full_size_random_predelay(cuda, pset, kind):
     """The bench's dattorro_rpd / chain_rpd legs at 65,536: a random pre-delay per instance
-    (verb.cpp:137-139), so the standalone reverb runs gather mode (dattorro_block_v4f, the fused form of
+    (verb.cpp:137-139), so the standalone reverb runs the split network with its pre-delay ring in rows (dattorro_block_v5, the form of
     the network) and the chain its pre-delay rows (dt::PreRow).  Two blocks; clones bit-identical,
     sampled instances (workgroup edges included) bit-exact against the oracle."""
     import torch
@@ -133,13 +133,49 @@ def test_full_size_random_predelay(cuda, pset, kind):
     e.set_params(0, p)
     y = _run(e, xs)
     if kind == "dattorro":
-        assert e.kernel_name == "dattorro_block_v4f"
+        assert e.kernel_name == "dattorro_block_v5"
     assert torch.isfinite(y).all()
     _check_clones(y, n)
     idx = np.union1d(_sample_idx(n), np.array([30, 32, 34, 96, 65502, 65534], np.int64))
     x = torch.cat(xs, 1)[:, :, idx].cpu().numpy()
     yr = _oracle(kind, p, idx, np.ascontiguousarray(x))
     yg = y[:, :, idx].cpu().numpy()
+    assert bits_equal(yg, yr), first_mismatch(yg, yr)
+    e.close()
+
+
+def test_reverb_network_switches_at_full_size(cuda):
+    """configs[2]'s 65,536 reverbs: uniform pre-delays run dattorro_block_v4 (pre-delay ring
+    position-major), per-instance pre-delays dattorro_block_v5 (ring in rows); each switch converts
+    the ring's content (dattorro_pre_layout).  Uniform -> per instance -> uniform, two blocks each,
+    one 2,048-frame call at the end (v5 splits longer calls; v4 does not): sampled instances
+    bit-exact against the oracle over the whole run."""
+    import torch
+    from ol_dsp_amd.workload import instance_params
+    n = 65536
+    p = instance_params("dattorro", 0, n)
+    rpd = instance_params("dattorro_rpd", 0, n)[0]
+    e = _engine("dattorro", n)
+    e.set_params(0, p)
+    idx = np.union1d(_sample_idx(n), np.array([1, 63, 65, 32767, 65535], np.int64))
+    d = O.Dattorro(len(idx))
+    for k, i in enumerate(idx):
+        for f in range(7):
+            d.set(k, f, float(p[f, i]))
+    ys, yrs, kernels = [], [], []
+    for phase, pd in enumerate([None, rpd, p[0], None]):
+        if pd is not None:
+            e.set_params("pre_delay", np.ascontiguousarray(pd[None, :]))
+            for k, i in enumerate(idx):
+                d.set(k, 0, float(pd[i]))
+        xs = _inputs(1000 * phase, n, 2, cuda, clone=False) if phase < 3 else \
+            [torch.cat(_inputs(3000, n, 8, cuda, clone=False), 1)]
+        y = _run(e, xs)
+        kernels.append(e.kernel_name)
+        ys.append(y[:, :, idx].cpu().numpy())
+        yrs.append(d.process(np.ascontiguousarray(torch.cat(xs, 1)[:, :, idx].cpu().numpy())))
+    assert kernels == ["dattorro_block_v4", "dattorro_block_v5", "dattorro_block_v4", "dattorro_block_v4"]
+    yg, yr = np.concatenate(ys, 1), np.concatenate(yrs, 1)
     assert bits_equal(yg, yr), first_mismatch(yg, yr)
     e.close()
 

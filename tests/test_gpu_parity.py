@@ -110,12 +110,11 @@ def test_dattorro_per_instance_predelay(cuda):
 
 
 def test_dattorro_predelay_gather_mode_switches(cuda):
-    """The standalone reverb switches its pre-delay ring between the position-major tap (one
-    pre-delay for every instance) and gather mode (per-instance pre-delays: dattorro_block_v4f,
-    instance-major ring) whenever the pre-delays become equal or differ; the ring's content is
-    carried across each switch.  Uniform -> per instance (edges 0..8, 255..257, 4800, past the max)
-    -> uniform -> per instance, calls of 256, 4, 1028 (gather mode splits at 256) and 60 frames,
-    bit-exact against the oracle throughout; reset() returns to the position-major ring."""
+    """Per-instance pre-delays switched on and off mid-run (verb.cpp:137-139): uniform -> per
+    instance (edges 0..8, 255..257, 4800, past the max) -> uniform -> per instance, calls of 256, 4,
+    1028 and 60 frames, bit-exact against the oracle throughout; reset() starts over.  At this size
+    both kinds run dattorro_block_v5 with the pre-delay ring in rows (test_gpu_fullsize.py covers the
+    layout conversions of the large engines, where uniform pre-delays run v4)."""
     n = 96
     rng = np.random.default_rng(81)
     p = dt_params(rng, n, 0.2)
@@ -155,16 +154,14 @@ def test_dattorro_predelay_gather_mode_switches(cuda):
     assert bits_equal(y2, yr2), first_mismatch(y2, yr2)
 
 
-@pytest.mark.parametrize("n,kernel", [(70, "dattorro_predelay_v2+dattorro_block_v4"), (72, "dattorro_block_v4f"),
-                                      (136, "dattorro_block_v4f")])
-def test_dattorro_gather_mode_long_run_wraps(cuda, n, kernel):
-    """Gather mode (per-instance pre-delays) over 70,000 frames: the uint16 wrap of t at 65536 and
-    calls that start off v2's 32-frame line grid and v4f's 32-frame pieces (60, 3900, 504 frames:
-    first and last chunks or pieces partial); pre-delays on the line, piece and window edges 0, 1,
-    31..37, 63..68, 96, 4800 and 8150..8191 (reads of ring slots the launch has not overwritten yet).
-    70 instances run v2 + the network (rows not 16-B aligned; a partial 64-instance wave), 72 and 136
-    the fused v4f (partial waves whose dead lanes mirror the last instance).  Bit-exact against the
-    oracle."""
+@pytest.mark.parametrize("n", [70, 72, 136])
+def test_dattorro_gather_mode_long_run_wraps(cuda, n):
+    """Per-instance pre-delays over 70,000 frames: the uint16 wrap of t at 65536 and calls that start
+    off the 16-position rows and the 4,096-frame launches off the 2,048-frame pieces (60, 3900, 504
+    frames); pre-delays on row and window edges 0, 1, 31..37, 63..68, 96, 4800 and 8150..8191 (reads
+    of ring slots the launch has not overwritten yet).  Partial 64-instance groups (70, 72, 136)
+    whose dead lanes mirror the last instance.  dattorro_block_v5, bit-exact against the oracle."""
+    kernel = "dattorro_block_v5"
     rng = np.random.default_rng(85)
     p = dt_params(rng, n, 0.0)
     edge = np.array([0, 1, 31, 32, 33, 35, 36, 37, 63, 64, 65, 67, 68, 96, 4800, 8150, 8160, 8190, 8191],

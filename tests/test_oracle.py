@@ -480,3 +480,18 @@ def test_mix_ref_is_the_in_order_float32_sum():
             for i in vs:
                 acc = np.float32(acc + v[0, f, i])
             assert got[f, b].tobytes() == acc.tobytes()
+
+
+def test_committed_rcp_model():
+    """tests/golden/rcp_f32_gfx950.npz, the voice oracle's committed v_rcp_f32 model (VERDICT r5 #4;
+    written on an MI355X by tools/rcp_dump.py): it decodes to the table its own sha256 names, every
+    entry is within one ulp of the correctly rounded 1/x, and it has the exception counts measured
+    in round 5: 897,675 mantissas of 2^23 one ulp off, 761,701 down and 135,974
+    up.  The GPU tests compare the device with this table before using it (conftest rcp_table)."""
+    import rcp_model
+    tab = rcp_model.load()
+    d = tab.astype(np.int64) - rcp_model.correctly_rounded().astype(np.int64)
+    assert tab.shape == (1 << 23,) and np.abs(d).max() == 1
+    assert int(np.count_nonzero(d)) == 897675
+    assert int(np.count_nonzero(d == -1)) == 761701 and int(np.count_nonzero(d == 1)) == 135974
+    assert rcp_model.decode(rcp_model.encode(tab)).tobytes() == tab.tobytes()

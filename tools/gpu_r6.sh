@@ -6,7 +6,7 @@
 #   tests                every GPU test, then smoke()
 #   b:<workload>         one workload's bench line (20 steps, no CPU baseline)
 #   p:<workload>         rocprofv3 kernel stats of that bench line (-> gpurun_out/prof_<w>)
-#   tr:<workload>        HBM traffic passes (tools/traffic_r2.sh)
+#   tr:<workload>        HBM traffic passes (tools/traffic.sh)
 #   bench                the driver's default line
 #   tl:<lib>:<k>         GPU tests matching <k> against an experimental build (OLFX_LIB=<lib>)
 #   te:<VAR=v>:<k>       GPU tests matching <k> with the environment variable VAR=v
@@ -72,7 +72,7 @@ for m in "$@"; do
       find "$out/prof_$w" -name '*kernel_trace.csv' -delete ;;
     tr:*)
       w=${m#tr:}
-      step "traffic_$w" 600 bash tools/traffic_r2.sh "$w" ;;
+      step "traffic_$w" 600 bash tools/traffic.sh "$w" ;;
     abe:*)
       r=${m#abe:}; w=${r%%:*}; kv=${r#*:}
       for r in 1 2 3; do

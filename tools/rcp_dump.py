@@ -4,7 +4,7 @@ oracle's kernel-arithmetic model, oracle/voice_ref.c) through tests/gpu_probe/li
 write it as the committed fixture tests/golden/rcp_f32_gfx950.npz: the instruction's result minus
 the correctly rounded 1/x, in ulps (-1, 0 or +1), two bits per mantissa, plus the sha256 of the
 full uint32 table.  The fixture is then the model the bit-exact voice tests use
-(tests/conftest.py rcp_table), and the device under test is only checked against it.
+(tests/conftest.py rcp_table; oracle/rcp_model.py), and the device under test is only checked against it.
 
 Usage (repo root, on the GPU box):  python tools/rcp_dump.py gpurun_out/rcp_f32_gfx950.npz
 """
@@ -16,7 +16,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 
 def main(dst: str) -> None:

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # tools/save_traffic.sh -- summarise the PMC traffic passes merged from the GPU box
-# (gpurun_out/pmc_<workload>, tools/traffic_r2.sh) into profiles/traffic_<workload>.json, each
+# (gpurun_out/pmc_<workload>, tools/traffic.sh) into profiles/traffic_<workload>.json, each
 # stamped with the libolfx.so hash the counters were taken with (tools/pmc_profile.sh).
 # Usage: bash tools/save_traffic.sh <workload>...
 set -eu

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
-# tools/traffic_r2.sh -- HBM traffic passes (one rocprofv3 --pmc run per pass, kernel trace only)
+# tools/traffic.sh -- HBM traffic passes (one rocprofv3 --pmc run per pass, kernel trace only)
 # for the given bench workloads.  Any failure ends the script (no retries).
-# Usage (repo root, via gpurun): bash tools/traffic_r2.sh <workload>...
+# Usage (repo root, via gpurun): bash tools/traffic.sh <workload>...
 set -u
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
