@@ -30,8 +30,6 @@
 #include "dattorro_stage.h"
 #include "lds_flags.h"
 
-#include <cstdlib>
-
 namespace olfx {
 
 namespace {
@@ -265,176 +263,6 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) 
     }
 }
 
-// chain_block_v6 (round 6): v5 with the reverb role split as dattorro_block_v5 -- six single-role
-// waves per 64 instances: C0, C1 (chorus), P (pitch-shift), DI (pre-delay rows, pre-LPF, input
-// all-passes), TA and TB (the tank halves with their output taps; dattorro_stage.h "The split
-// network").  P hands DI the mono mix (l + r) / 2 of its output (the reverb's input,
-// ReverbFx.cpp:13-16; the same addition and division the reverb role made), DI hands x to both
-// halves, each half finishes one output channel.  Every wave's register set is its own role's, so
-// a CU holds the six (v5's reverb wave carried all 27 taps at 256 VGPR + 142 AGPR, one wave per
-// SIMD).  Launches of at most dt::kSplitMaxFrames frames (the halves' cross taps, 3163 / 3720 back).
-namespace {
-constexpr int kChain6Threads = 384;               // 6 waves
-constexpr int kQM = 16 * 64 + 16;                 // one mono queue buffer: [16 frames][64 instances] + pad
-constexpr int kFlags6 = 16;                       // F_* at 0.., the split counters (dt::SPF_*) at 8..
-constexpr int kSplitLds = 3 * (int)dt::kSplitDepth * 64 * 4;   // qx, q0, q1: [kSplitDepth][64] float4 each
-constexpr int kChain6Lds = 4 * kChainRegion + kDepth * kQBuf + kDepth * kQM + kFlags6 + kPreLds + kSplitLds;
-static_assert(kChain6Lds * 4 <= 160 * 1024, "chain_block_v6 LDS");
-}  // namespace
-
-template <bool COOP>
-__global__ __launch_bounds__(kChain6Threads, 1) void chain_block_v6(ChainArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    constexpr int kChunk = 16;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t wib = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
-    const uint32_t lane = tid & 63u;
-    const uint32_t n = a.n, nf = a.n_frames;
-    const uint32_t nchunks = (nf + kChunk - 1) / kChunk;
-    const uint32_t nsteps = nf / 4u;
-    const uint32_t ngroups = (n + 63u) / 64u;
-    float *q1 = lds + 4 * kChainRegion;                    // chorus -> pitch   [kDepth][2 ch][16][64]
-    float *q2 = q1 + kDepth * kQBuf;                       // pitch -> DI, mono [kDepth][16][64]
-    uint32_t *flags = (uint32_t *)(q2 + kDepth * kQM);
-    float4 *pre_far = (float4 *)(flags + kFlags6);         // DI's pre-delay row staging (25 x 64 float4)
-    float4 *sq = pre_far + 25 * 64;                        // split queues
-    const dt::SplitQ q_a{sq, sq + dt::kSplitDepth * 64, sq + 2 * dt::kSplitDepth * 64, flags + 8};
-    const dt::SplitQ q_b{sq, sq + 2 * dt::kSplitDepth * 64, sq + dt::kSplitDepth * 64, flags + 8};
-    if (tid < kFlags6) flags[tid] = 0;
-    __syncthreads();                                       // the only barrier
-
-    if (wib < 2) {
-        // ---------------- C: the chorus, per (instance, channel) lane (as v5) ----------------
-        using StageC = ch::ChStageL<true, COOP, false>;
-        StageC s1;
-        const ch::Rsrc rIn = ch::rsrc(a.in, (a.plane + (uint64_t)nf * n) * 4);
-        const uint32_t frame_b = n * 4u;
-        for (uint32_t g = blockIdx.x, gi = 0; g < ngroups; g += gridDim.x, ++gi) {
-            const uint32_t base = g * 64u, gc0 = gi * nchunks;
-            const uint32_t inst0 = base + 32u * wib;
-            s1.init(a.c1, lds + wib * kChainRegion, lane, inst0);
-            const uint32_t io_v = s1.ch * (uint32_t)a.plane * 4u + s1.i * 4u;
-            const uint32_t qcol = s1.ch * kQCh + 32u * wib + s1.j;
-            const uint32_t pinst = inst0 + (lane & 7u) * 4u;
-            auto row_v = [&](int q, uint32_t f0) {
-                const uint32_t r = StageC::coop_row(q, lane);
-                return (r & 1u) * (uint32_t)a.plane * 4u + min(f0 + (r >> 1), nf - 1u) * frame_b + pinst * 4u;
-            };
-            float x[kChunk], xn[kChunk];
-            float4 xq[4];
-            int C = (int)min((uint32_t)kChunk, nf);
-            if constexpr (COOP) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) xq[q] = ch::ld4(rIn, row_v(q, 0));
-                s1.begin(x, C, xq);
-            } else {
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) x[k] = k < C ? ch::ld1(rIn, io_v, (uint32_t)k * frame_b) : 0.f;
-                s1.begin(x, C);
-            }
-            auto step = [&](auto par, uint32_t f0, uint32_t c) {
-                C = (int)min((uint32_t)kChunk, nf - f0);
-                const int Cn = f0 + kChunk < nf ? (int)min((uint32_t)kChunk, nf - f0 - kChunk) : 0;
-                auto prefetch = [&]() {
-                    if constexpr (COOP) {
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) xq[q] = ch::ld4(rIn, row_v(q, f0 + kChunk));
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < kChunk; ++k) {
-                            const float v = ch::ld1(rIn, io_v, min(f0 + kChunk + (uint32_t)k, nf - 1u) * frame_b);
-                            xn[k] = k < Cn ? v : 0.f;
-                        }
-                    }
-                };
-                float y[kChunk];
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) y[k] = __builtin_nondeterministic_value(0.f);
-                s1.template chunk<decltype(par)::value>(x, xn, C, Cn, [&](int k, float v) { y[k] = v; }, prefetch, xq);
-                const uint32_t gc = gc0 + c;
-                wait_for([&] { return flag_get(flags + F_PIN) + kDepth > gc; });
-                float *q = q1 + (gc % kDepth) * kQBuf + qcol;
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) q[k * 64] = y[k];
-                flag_put(flags + F_C0 + wib, gc + 1);
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) x[k] = xn[k];
-            };
-            for (uint32_t f0 = 0, c = 0; f0 < nf; f0 += 2 * kChunk, c += 2) {
-                step(std::integral_constant<int, 0>{}, f0, c);
-                if (f0 + kChunk < nf) step(std::integral_constant<int, 1>{}, f0 + kChunk, c + 1);
-            }
-            s1.finish(a.c1);
-        }
-    } else if (wib == 2) {
-        // ---------------- P: the pitch-shifter, one lane per instance; out: the mono mix ----------------
-        ch::PStageS sp;
-        static_assert(ch::PStageS::kRegion <= 2 * kChainRegion, "P's LDS share");
-        for (uint32_t g = blockIdx.x, gi = 0; g < ngroups; g += gridDim.x, ++gi) {
-            const uint32_t gc0 = gi * nchunks;
-            sp.init(a.c2, lds + 2 * kChainRegion, lane, g * 64u);
-            int C = (int)min((uint32_t)kChunk, nf);
-            sp.begin(C);
-            auto step = [&](auto par, uint32_t f0, uint32_t c) {
-                constexpr int P = decltype(par)::value;
-                C = (int)min((uint32_t)kChunk, nf - f0);
-                const int Cn = f0 + kChunk < nf ? (int)min((uint32_t)kChunk, nf - f0 - kChunk) : 0;
-                const uint32_t gc = gc0 + c;
-                wait_for([&] { return flag_get(flags + F_C0) > gc && flag_get(flags + F_C1) > gc; });
-                const float *qi = q1 + (gc % kDepth) * kQBuf + lane;
-                float2 x[kChunk];
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) x[k] = make_float2(qi[k * 64], qi[kQCh + k * 64]);
-                flag_put(flags + F_PIN, gc + 1);
-                float2 y[kChunk];
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) y[k] = make_float2(__builtin_nondeterministic_value(0.f), __builtin_nondeterministic_value(0.f));
-                sp.template chunk<P>(x, C, Cn, [&](int k, float2 v) { y[k] = v; });
-                wait_for([&] { return flag_get(flags + F_DIN) + kDepth > gc; });
-                float *qo = q2 + (gc % kDepth) * kQM + lane;
-#pragma unroll
-                for (int k = 0; k < kChunk; ++k) qo[k * 64] = (y[k].x + y[k].y) / 2;   // ReverbFx.cpp:13-16
-                flag_put(flags + F_POUT, gc + 1);
-            };
-            for (uint32_t f0 = 0, c = 0; f0 < nf; f0 += 2 * kChunk, c += 2) {
-                step(std::integral_constant<int, 0>{}, f0, c);
-                if (f0 + kChunk < nf) step(std::integral_constant<int, 1>{}, f0 + kChunk, c + 1);
-            }
-            sp.finish(a.c2);
-        }
-    } else if (wib == 3) {
-        // ---------------- DI: pre-delay rows, pre-LPF, input all-passes (dt::split_di_rows) ----------------
-        for (uint32_t g = blockIdx.x, gi = 0; g < ngroups; g += gridDim.x, ++gi) {
-            const uint32_t gc0 = gi * nchunks;
-            dt::Tap<DT_IN1, 107, 0> in1;
-            dt::split_di_rows(a.d, g, lane, nf, gi * nsteps, pre_far, sq, flags + 8, in1,
-                              [&](uint32_t c, uint32_t, uint32_t, float (&xm)[kChunk]) {
-                                  const uint32_t gc = gc0 + c;
-                                  wait_for([&] { return flag_get(flags + F_POUT) > gc; });
-                                  const float *q = q2 + (gc % kDepth) * kQM + lane;
-#pragma unroll
-                                  for (int k = 0; k < kChunk; ++k) xm[k] = q[k * 64];
-                                  flag_put(flags + F_DIN, gc + 1);
-                              });
-        }
-    } else {
-        // ---------------- TA / TB: the tank halves, each finishing one output channel ----------------
-        const uint32_t h = wib - 4u;
-        for (uint32_t g = blockIdx.x, gi = 0; g < ngroups; g += gridDim.x, ++gi) {
-            const uint32_t i = g * 64u + lane;
-            if (h == 0) dt::split_tank<0>(a.d, i, lane, i < n, a.d.t0, nsteps, gi * nsteps, a.out, n, q_a);
-            else dt::split_tank<1>(a.d, i, lane, i < n, a.d.t0, nsteps, gi * nsteps, a.out + a.plane, n, q_b);
-        }
-    }
-}
-
-// A/B knob while chain_block_v6 is measured against v5 (OLFX_CHAIN_V5=1: the four-role kernel)
-static bool chain_use_v5() {
-    static const bool v5 = [] { const char *e = std::getenv("OLFX_CHAIN_V5"); return e && e[0] == '1'; }();
-    return v5;
-}
-const char *chain_kernel() { return chain_use_v5() ? "chain_block_v5" : "chain_block_v6"; }
-
 hipError_t launch_chain(const ChainArgs &a, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
     if ((a.n_frames & 3u) || (a.c1.t0 & 3u) || (a.d.t0 & 3u) || a.d.n < ((a.n + 63u) & ~63u)) return hipErrorInvalidValue;
@@ -446,23 +274,8 @@ hipError_t launch_chain(const ChainArgs &a, hipStream_t s) {
     const uint32_t groups = (a.n + 63u) / 64u;
     const uint32_t blocks = groups < a.cus ? groups : a.cus;
     const bool coop = (a.n & 3u) == 0 && (a.plane & 3u) == 0 && (((uintptr_t)a.in | (uintptr_t)a.out) & 15u) == 0;
-    if (chain_use_v5()) {
-        if (coop) hipLaunchKernelGGL(chain_block_v5<true>, dim3(blocks), dim3(kChainThreads), (size_t)kChainLds * sizeof(float), s, a);
-        else hipLaunchKernelGGL(chain_block_v5<false>, dim3(blocks), dim3(kChainThreads), (size_t)kChainLds * sizeof(float), s, a);
-        return hipGetLastError();
-    }
-    // pieces of at most kSplitMaxFrames frames (the split reverb's cross-half taps)
-    for (uint32_t f0 = 0; f0 < a.n_frames; f0 += dt::kSplitMaxFrames) {
-        ChainArgs p = a;
-        p.n_frames = min(dt::kSplitMaxFrames, a.n_frames - f0);
-        p.c1.t0 = a.c1.t0 + f0;
-        p.c2.t0 = a.c2.t0 + f0;
-        p.d.t0 = (a.d.t0 + f0) & 0xFFFFu;
-        p.in = a.in + (size_t)f0 * a.n;
-        p.out = a.out + (size_t)f0 * a.n;
-        if (coop) hipLaunchKernelGGL(chain_block_v6<true>, dim3(blocks), dim3(kChain6Threads), (size_t)kChain6Lds * sizeof(float), s, p);
-        else hipLaunchKernelGGL(chain_block_v6<false>, dim3(blocks), dim3(kChain6Threads), (size_t)kChain6Lds * sizeof(float), s, p);
-    }
+    if (coop) hipLaunchKernelGGL(chain_block_v5<true>, dim3(blocks), dim3(kChainThreads), (size_t)kChainLds * sizeof(float), s, a);
+    else hipLaunchKernelGGL(chain_block_v5<false>, dim3(blocks), dim3(kChainThreads), (size_t)kChainLds * sizeof(float), s, a);
     return hipGetLastError();
 }
 

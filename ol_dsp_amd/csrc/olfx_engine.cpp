@@ -1746,7 +1746,7 @@ const char *olfx_kernel_name(const olfx_engine *e) {
     case OLFX_KIND_PITCHSHIFT: return "chorus_block_v11";
     case OLFX_KIND_VOICE: return "voice_block_v5";
     case OLFX_KIND_VOICE_MOOG: return "voice_block_v4";
-    case OLFX_KIND_CHAIN: return chain_kernel();
+    case OLFX_KIND_CHAIN: return "chain_block_v5";
     case OLFX_KIND_FXRACK: return "fxrack_block_v3";
     default: return "";
     }

@@ -378,7 +378,6 @@ struct ChainArgs {
 
 hipError_t launch_dattorro(const DattorroArgs &a, bool rows, hipStream_t s);
 hipError_t launch_chain(const ChainArgs &a, hipStream_t s);
-const char *chain_kernel();              // the chain kernel launch_chain runs
 hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s);
 // the chorus kernel launch_chorus picks for n instances, ring sizes and cooperative I/O
 
