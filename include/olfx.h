@@ -207,11 +207,11 @@ typedef struct olfx_kind_info {
     uint32_t in_channels;       /* channels olfx_process reads */
     uint32_t out_channels;      /* channels olfx_process writes */
     uint64_t state_bytes_per_instance;   /* device state (rings + scalars + params); a reverb
-                                            engine whose instances get different pre-delays adds
-                                            gather mode's 32 KB per instance (the instance-major
-                                            pre-delay ring; + 1 KB for the pre-delayed block when
-                                            the audio rows are not 16-B aligned), allocated at the
-                                            first such block, kept until destroy */
+                                            engine of 2 x 64 x CUs instances or more whose
+                                            pre-delays come to differ adds 32 KB per instance (a
+                                            copy of the pre-delay ring while its layout changes,
+                                            DESIGN.md section 4), allocated at the first such
+                                            block, kept until destroy */
 } olfx_kind_info;
 
 int olfx_abi_version(void);

@@ -438,8 +438,7 @@ struct olfx_engine {
     uint32_t *fr_state = nullptr, *fr_coef = nullptr;
     uint32_t n_dt = 0;           // reverb-stage instances: n, or n rounded up to 64 for the chain
     float *dt_rings = nullptr;
-    // standalone reverb, per-instance pre-delays (dattorro.hip gather mode): the instance-major
-    // pre-delay ring and the block's pre-delayed input, allocated on first need
+    // standalone reverb: the network (dattorro.hip dattorro_rows) and so its pre-delay ring's layout
     float *dt_pre_tmp = nullptr; // a copy of the pre-delay ring while its layout changes
     bool dt_rows = false;        // the pre-delay ring's layout: rows (dattorro_block_v5) or position-major (v4)
     bool dt_pre_check = true;    // a pre-delay changed: re-decide the network at the next block
