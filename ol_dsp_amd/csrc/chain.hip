@@ -42,11 +42,6 @@ constexpr int kFlags = 8;                     // LDS progress counters
 constexpr int kPreLds = (17 + 8) * 64 * 4;    // DT's pre-delay staging (dt::PreRow): far [17][64], near [8][64] float4
 constexpr int kChainLds = 4 * kChainRegion + 2 * kDepth * kQBuf + kFlags + kPreLds;
 enum { F_C0 = 0, F_C1, F_PIN, F_POUT, F_DIN };   // chunks published by C0 / C1, taken by P, published by P, taken by DT
-__device__ __forceinline__ void wave_sync() {     // LDS written by some lanes, read by others
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 }  // namespace
 
@@ -177,88 +172,30 @@ __global__ __launch_bounds__(kChainThreads, 1) void chain_block_v5(ChainArgs a) 
         }
     } else {
         // ---------------- DT: the reverb, lane = instance, input from the queue ----------------
-        // the pre-delay ring in rows of 16 positions (dt::PreRow): per chunk each lane loads its
-        // instance's next row (64 B) at the first step; the chunk's input leaves cooperatively --
-        // store m of lane l is group l & 3 of instance 16 m + l / 4, one 1-KB run per row
-        float4 *pre_far = (float4 *)(flags + kFlags), *pre_near = pre_far + 17 * 64;
-        const uint32_t cj = lane >> 2, cg = lane & 3u;
-        constexpr uint32_t kRows = kDtSize[DT_PRE] / 16u;           // rows of the ring
-        const uint32_t nd = a.d.n;
+        // the network in one wave over the pre-delay ring in rows (dt::rows_network, dt::PreRow)
+        float4 *const stage = (float4 *)(flags + kFlags);
         for (uint32_t g = blockIdx.x, gi = 0; g < ngroups; g += gridDim.x, ++gi) {
             const uint32_t i = g * 64u + lane, gc0 = gi * nchunks;   // < d.n (padded to 64)
-            DT_STAGE_PRE(a.d, i, olfx::dt::PreRow);
-            const uint32_t t0 = a.d.t0;
-            dt_prime(t0);
-            float4 *const ring_g = (float4 *)a.d.ring[DT_PRE] + (size_t)g * 64u * 4u;   // row r: + r * nd * 4
-            uint32_t dj[4];                                   // the pre-delay of instance 16 m + l / 4
-#pragma unroll
-            for (int m = 0; m < 4; ++m) dj[m] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((16u * m + cj) << 2), (int)dpre);
-            pre.near = pre_near + lane;
-            pre.far = pre_far + lane;
-            pre.farw = pre_far + lane;
-            pre.ring = ring_g + lane * 4u;
-            pre.nd = nd;
-            pre.pv = make_float4(0.f, 0.f, 0.f, 0.f);
-            pre.pslot = 16u * 64u;                            // junk: nothing loaded yet
-            // group cg of row ((T - d) >> 4) + plus of instance 16 m + cj, and its far slot
-            auto row_ptr = [&](uint32_t row, int m) { return ring_g + ((size_t)(row & (kRows - 1u)) * nd + 16u * m + cj) * 4u + cg; };
-            auto put_row = [&](uint32_t T, uint32_t plus, int m) {
-                const uint32_t row = ((T - dj[m]) >> 4) + plus;
-                pre_far[((row & 3u) * 4u + cg) * 64u + 16u * m + cj] = *row_ptr(row, m);
-            };
-            // group cg of the positions T .. T + 15 of instance 16 m + cj in the ring, and in near
-            auto ring_at = [&](uint32_t T, int m) {
-                const uint32_t P = T + 4u * cg;
-                return ring_g + ((size_t)((P >> 4) & (kRows - 1u)) * nd + 16u * m + cj) * 4u + ((P >> 2) & 3u);
-            };
-            auto near_at = [&](uint32_t T, int m) { return pre_near + (((T >> 2) + cg) & 7u) * 64u + 16u * m + cj; };
-            // the first chunk's rows r0, r0 + 1 and the chunk before it (the rest: PreRow, per chunk)
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                put_row(t0, 0, m);
-                put_row(t0, 1, m);
-                *near_at(t0 - kChunk, m) = *ring_at(t0 - kChunk, m);
-            }
             const bool valid = i < n;
-            for (uint32_t c = 0; c < nchunks; ++c) {
-                const uint32_t f0 = c * kChunk, gc = gc0 + c, T = t0 + f0;
-                const uint32_t C = min((uint32_t)kChunk, nf - f0);
-                wait_for([&] { return flag_get(flags + F_POUT) > gc; });
-                const float *q = q2 + (gc % kDepth) * kQBuf + lane;
-                float xm[kChunk];                             // the chunk's mono input, (l + r) / 2
+            dt::rows_network<false>(
+                a.d, g, lane, nf, stage,
+                [&](uint32_t c, uint32_t, uint32_t, float (&xm)[kChunk]) {   // the chunk's mono input, (l + r) / 2
+                    const uint32_t gc = gc0 + c;
+                    wait_for([&] { return flag_get(flags + F_POUT) > gc; });
+                    const float *q = q2 + (gc % kDepth) * kQBuf + lane;
 #pragma unroll
-                for (int k = 0; k < kChunk; ++k) xm[k] = (q[k * 64] + q[kQCh + k * 64]) / 2;
-                flag_put(flags + F_DIN, gc + 1);
-                // the chunk's input -> near (over the chunk before the one before)
-#pragma unroll
-                for (int m = 0; m < 4; ++m)
-                    pre_near[(((T >> 2) + (uint32_t)m) & 7u) * 64u + lane] = make_float4(xm[4 * m], xm[4 * m + 1], xm[4 * m + 2], xm[4 * m + 3]);
-                wave_sync();
-                // the input into the ring (groups past a short chunk's C frames stay), then the next
-                // chunk's rows: the loads see these stores (one wave, issue order)
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const float4 v = *near_at(T, m);
-                    if (4u * cg < C) *ring_at(T, m) = v;
-                }
-                pre.T = T;
-                for (uint32_t s = 0; s < C; s += 4) {
-                    float xin[4], o_l[4], o_r[4];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) xin[k] = xm[s + k];
-                    pre.fc = (int)s;
-                    dt_step(T + s, f0 + s + 4 < nf, xin, o_l, o_r);
+                    for (int k = 0; k < kChunk; ++k) xm[k] = (q[k * 64] + q[kQCh + k * 64]) / 2;
+                    flag_put(flags + F_DIN, gc + 1);
+                },
+                [&](uint32_t f, const float (&o_l)[4], const float (&o_r)[4]) {
                     if (valid) {
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {
-                            a.out[(size_t)(f0 + s + k) * n + i] = o_l[k];
-                            a.out[a.plane + (size_t)(f0 + s + k) * n + i] = o_r[k];
+                            a.out[(size_t)(f + k) * n + i] = o_l[k];
+                            a.out[a.plane + (size_t)(f + k) * n + i] = o_r[k];
                         }
                     }
-                }
-                wave_sync();                                  // this chunk's LDS reads before the next one's writes
-            }
-            dt_finish();
+                });
         }
     }
 }

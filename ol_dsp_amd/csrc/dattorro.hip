@@ -138,28 +138,30 @@ __global__ __launch_bounds__(256) void dattorro_pre_layout(const float4 *__restr
     }
 }
 
-// The network for these pre-delays: v5 (rows) below two v4 waves per CU or for per-instance
-// pre-delays, else v4 (same box, profiles/r6/NOTES.md: 16,384 instances v5 0.138 against v4
-// 0.166 ms; 32,768 v4 0.2764 against 0.2797; 65,536 v4 0.5551 against 0.5736).  OLFX_DT_V4=1 / =0
-// forces v4 / v5 for uniform pre-delays (A/B timing).
-bool dattorro_rows(uint32_t n, uint32_t cus, bool uniform) {
+// The network for these pre-delays ("Which network"): v4 for one pre-delay
+// once v4 has two waves per CU, else v5 (same box, profiles/r6/NOTES.md: 16,384 instances v5 0.138
+// against v4 0.166 ms; 32,768 v4 0.2764 against v5 0.2797; 65,536 v4 0.5551 against v5 0.5736).
+// OLFX_DT_V4=1 / =0 forces v4 / v5 for uniform pre-delays (A/B timing).
+int dattorro_network(uint32_t n, uint32_t cus, bool uniform) {
     static const int force = [] {
         const char *e = std::getenv("OLFX_DT_V4");
         return e && e[0] ? (e[0] == '1' ? 1 : 0) : -1;
     }();
-    if (!uniform) return true;
-    if (force >= 0) return force == 0;
-    return (uint64_t)(n + 63u) / 64u < 2ull * (cus ? cus : 256u);
+    if (!uniform) return DT_NET_V5;
+    if (force >= 0) return force ? DT_NET_V4 : DT_NET_V5;
+    return (uint64_t)(n + 63u) / 64u >= 2ull * (cus ? cus : 256u) ? DT_NET_V4 : DT_NET_V5;
 }
 
-hipError_t launch_dattorro(const DattorroArgs &a, bool rows, hipStream_t s) {
+const char *dattorro_network_name(int net) { return net == DT_NET_V4 ? "dattorro_block_v4" : "dattorro_block_v5"; }
+
+hipError_t launch_dattorro(const DattorroArgs &a, int net, hipStream_t s) {
     if (a.n == 0 || a.n_frames == 0) return hipSuccess;
     if ((a.t0 & 3u) || (a.n_frames & 3u)) return hipErrorInvalidValue;   // 4-frame steps
     // the modulated taps' buffer loads take 32-bit offsets into their (1024-position) rings
     if ((uint64_t)kDtSize[DT_AP1A] * a.n * 4u >= (1ull << 32) || (uint64_t)kDtSize[DT_AP1B] * a.n * 4u >= (1ull << 32))
         return hipErrorInvalidValue;
     const uint32_t blocks = (a.n + 63u) / 64u;   // one 64-instance group per workgroup
-    if (!rows) {
+    if (net == DT_NET_V4) {
         hipLaunchKernelGGL(dattorro_block_v4, dim3(blocks), dim3(64), 0, s, a);
         return hipGetLastError();
     }

@@ -752,3 +752,90 @@ __device__ __forceinline__ void split_tank(const DattorroArgs &a, uint32_t i, ui
         dt_args.state[DTS_LP_DAMP_A * dt_n + dt_i] = lp_a;                                               \
         dt_args.state[DTS_LP_DAMP_B * dt_n + dt_i] = lp_b;                                               \
     }
+
+namespace olfx {
+namespace dt {
+
+// The whole network in one wave (DT_STAGE_X, all 27 taps) over the pre-delay ring in ROWS (PreRow),
+// for the instances 64 g .. 64 g + 63: the fused chain's reverb role.
+// CLAMP: instances >= d.n mirror instance d.n - 1 and store nothing (the chain pads d.n to 64).
+// src(c, f0, C, xm) gives chunk c's mono input (16 frames from f0, C real); out(f, o_l, o_r) takes
+// the 4 frames from f.  stage: 25 x 64 float4 of LDS (far 17 x 64, near 8 x 64).
+template <bool CLAMP, class Src, class Out>
+__device__ __forceinline__ void rows_network(const DattorroArgs &d, uint32_t g, uint32_t lane, uint32_t nf,
+                                             float4 *stage, Src &&src, Out &&out) {
+    constexpr uint32_t kChunk = 16;
+    constexpr uint32_t kRows = kDtSize[DT_PRE] / 16u;
+    const uint32_t nd = d.n, base = g * 64u;
+    const uint32_t cj = lane >> 2, cg = lane & 3u;
+    float4 *const far = stage, *const near = stage + 17 * 64;
+    DT_STAGE_PRE(d, (CLAMP ? min(base + lane, nd - 1u) : base + lane), olfx::dt::PreRow);
+    const uint32_t t0 = d.t0;
+    dt_prime(t0);
+    float4 *const ring = (float4 *)d.ring[DT_PRE];    // row r of instance j: ring + (r * nd + j) * 4
+    uint32_t dj[4], jc[4];                            // cooperative instance 16 m + l / 4: its pre-delay, its index
+    bool jl[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        dj[m] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((16u * m + cj) << 2), (int)dpre);
+        jl[m] = !CLAMP || base + 16u * m + cj < nd;
+        jc[m] = CLAMP ? min(base + 16u * m + cj, nd - 1u) : base + 16u * m + cj;
+    }
+    pre.near = near + lane;
+    pre.far = far + lane;
+    pre.farw = far + lane;
+    pre.ring = ring + (size_t)dt_i * 4u;
+    pre.nd = nd;
+    pre.pv = make_float4(0.f, 0.f, 0.f, 0.f);
+    pre.pslot = 16u * 64u;                            // junk: nothing loaded yet
+    auto row_ptr = [&](uint32_t row, int m) { return ring + ((size_t)(row & (kRows - 1u)) * nd + jc[m]) * 4u + cg; };
+    auto put_row = [&](uint32_t T, uint32_t plus, int m) {   // group cg of row ((T - d) >> 4) + plus -> far
+        const uint32_t row = ((T - dj[m]) >> 4) + plus;
+        far[((row & 3u) * 4u + cg) * 64u + 16u * m + cj] = *row_ptr(row, m);
+    };
+    auto ring_at = [&](uint32_t T, int m) {           // group cg of positions T .. T + 15 in the ring
+        const uint32_t P = T + 4u * cg;
+        return ring + ((size_t)((P >> 4) & (kRows - 1u)) * nd + jc[m]) * 4u + ((P >> 2) & 3u);
+    };
+    auto near_at = [&](uint32_t T, int m) { return near + (((T >> 2) + cg) & 7u) * 64u + 16u * m + cj; };
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {                     // the first chunk's rows r0, r0 + 1 and the chunk before
+        put_row(t0, 0, m);
+        put_row(t0, 1, m);
+        *near_at(t0 - kChunk, m) = *ring_at(t0 - kChunk, m);
+    }
+    const uint32_t nchunks = (nf + kChunk - 1) / kChunk;
+    for (uint32_t c = 0; c < nchunks; ++c) {
+        const uint32_t f0 = c * kChunk, T = t0 + f0;
+        const uint32_t C = min(kChunk, nf - f0);
+        float xm[kChunk];
+        src(c, f0, C, xm);
+        // the chunk's input -> near (over the chunk before the one before), then into the ring
+        // cooperatively (groups past a short chunk's C frames stay); the next rows' loads, issued
+        // during the steps below (PreRow::prefetch), see these stores (one wave, issue order)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            near[(((T >> 2) + (uint32_t)m) & 7u) * 64u + lane] = make_float4(xm[4 * m], xm[4 * m + 1], xm[4 * m + 2], xm[4 * m + 3]);
+        wsync();
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const float4 v = *near_at(T, m);
+            if (4u * cg < C && jl[m]) *ring_at(T, m) = v;
+        }
+        pre.T = T;
+        auto step = [&](uint32_t s) {
+            float xin[4], o_l[4], o_r[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) xin[k] = xm[s + k];
+            pre.fc = (int)s;
+            dt_step(T + s, f0 + s + 4 < nf, xin, o_l, o_r);
+            out(f0 + s, o_l, o_r);
+        };
+        for (uint32_t s = 0; s < C; s += 4) step(s);
+        wsync();                                      // this chunk's LDS reads before the next one's writes
+    }
+    if (!CLAMP || base + lane < nd) dt_finish();
+}
+
+}  // namespace dt
+}  // namespace olfx

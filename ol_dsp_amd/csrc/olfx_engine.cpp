@@ -440,7 +440,7 @@ struct olfx_engine {
     float *dt_rings = nullptr;
     // standalone reverb: the network (dattorro.hip dattorro_rows) and so its pre-delay ring's layout
     float *dt_pre_tmp = nullptr; // a copy of the pre-delay ring while its layout changes
-    bool dt_rows = false;        // the pre-delay ring's layout: rows (dattorro_block_v5) or position-major (v4)
+    int dt_net = DT_NET_V4;      // the network of the last block; its pre-delay ring layout: rows unless v4
     bool dt_pre_check = true;    // a pre-delay changed: re-decide the network at the next block
     float *dt_state = nullptr;
     float *dt_coef = nullptr;
@@ -878,7 +878,7 @@ int init_state(olfx_engine *e) {
         std::fill(e->params.begin() + (size_t)f * e->n, e->params.begin() + (size_t)(f + 1) * e->n, d[f]);
     e->configured.assign(e->n, 0);
     e->n_components = 0;
-    e->dt_rows = false;            // the zeroed ring is valid in either layout: decided at the next block
+    e->dt_net = DT_NET_V4;         // the zeroed ring is valid in either layout: decided at the next block
     e->dt_pre_check = true;
     e->events.clear();
     e->ev_slot.assign(e->n, -1);
@@ -963,17 +963,16 @@ int launch(olfx_engine *e, const float *din, float *dout, uint32_t n_frames, uin
             const uint32_t d0 = dattorro_predelay_samples(pd[0]);
             bool uniform = true;
             for (uint32_t i = 1; i < e->n && uniform; ++i) uniform = dattorro_predelay_samples(pd[i]) == d0;
-            const bool rows = dattorro_rows(e->n_dt, (uint32_t)e->cus, uniform);
-            if (rows != e->dt_rows) {
-                if (e->frames > 0) {      // a fresh (zeroed) ring needs no conversion
-                    if (!e->dt_pre_tmp) HIPCHK(e, hipMalloc((void **)&e->dt_pre_tmp, (size_t)kDtSize[DT_PRE] * e->n_dt * 4));
-                    r = launch_dattorro_pre_layout(dt_args(nullptr, nullptr), e->dt_pre_tmp, rows, s);
-                    if (r != hipSuccess) return e->hip_fail(r, "pre-delay ring layout");
-                }
-                e->dt_rows = rows;
+            const int net = dattorro_network(e->n_dt, (uint32_t)e->cus, uniform);
+            const bool rows = net != DT_NET_V4;
+            if (rows != (e->dt_net != DT_NET_V4) && e->frames > 0) {   // a fresh (zeroed) ring needs no conversion
+                if (!e->dt_pre_tmp) HIPCHK(e, hipMalloc((void **)&e->dt_pre_tmp, (size_t)kDtSize[DT_PRE] * e->n_dt * 4));
+                r = launch_dattorro_pre_layout(dt_args(nullptr, nullptr), e->dt_pre_tmp, rows, s);
+                if (r != hipSuccess) return e->hip_fail(r, "pre-delay ring layout");
             }
+            e->dt_net = net;
         }
-        r = launch_dattorro(dt_args(din, dout), e->dt_rows, s);
+        r = launch_dattorro(dt_args(din, dout), e->dt_net, s);
         break;
     }
     case OLFX_KIND_CHORUS:
@@ -1740,7 +1739,7 @@ const char *olfx_kernel_name(const olfx_engine *e) {
     if (!e) return "";
     switch (e->kind) {
     case OLFX_KIND_DATTORRO:   // the network of the last block (dattorro.hip dattorro_rows)
-        return e->dt_rows ? "dattorro_block_v5" : "dattorro_block_v4";
+        return dattorro_network_name(e->dt_net);
     case OLFX_KIND_CHORUS:
     case OLFX_KIND_PITCHSHIFT: return "chorus_block_v11";
     case OLFX_KIND_VOICE: return "voice_block_v5";

@@ -82,9 +82,11 @@ struct DattorroArgs {
     uint32_t in_ch;             // 1 or 2
     uint32_t cus;               // compute units of the device (olfx_create)
 };
-// Standalone reverb: the network for these pre-delays (dattorro.hip): true = dattorro_block_v5 with
-// the pre-delay ring in rows ([8192/16][n][16]), false = dattorro_block_v4, ring position-major
-bool dattorro_rows(uint32_t n, uint32_t cus, bool uniform);
+// Standalone reverb: the network for these pre-delays (dattorro.hip): v4 with the pre-delay ring
+// position-major, v5 with it in rows ([8192/16][n][16])
+enum { DT_NET_V4 = 0, DT_NET_V5 };
+int dattorro_network(uint32_t n, uint32_t cus, bool uniform);
+const char *dattorro_network_name(int net);
 // the pre-delay ring's content into the other layout (tmp: a device buffer of the ring's size)
 hipError_t launch_dattorro_pre_layout(const DattorroArgs &a, float *tmp, bool to_rows, hipStream_t s);
 
@@ -376,7 +378,7 @@ struct ChainArgs {
     uint32_t cus;               // compute units of the device (the persistent grid), from olfx_create
 };
 
-hipError_t launch_dattorro(const DattorroArgs &a, bool rows, hipStream_t s);
+hipError_t launch_dattorro(const DattorroArgs &a, int net, hipStream_t s);
 hipError_t launch_chain(const ChainArgs &a, hipStream_t s);
 hipError_t launch_chorus(const ChorusArgs &a, hipStream_t s);
 // the chorus kernel launch_chorus picks for n instances, ring sizes and cooperative I/O

@@ -122,8 +122,8 @@ def test_full_size_stream_kinds(cuda, kind, n):
 @pytest.mark.parametrize("pset,kind", [("dattorro_rpd", "dattorro"), ("chain_rpd", "chain")])
 def test_full_size_random_predelay(cuda, pset, kind):
     """The bench's dattorro_rpd / chain_rpd legs at 65,536: a random pre-delay per instance
-    (verb.cpp:137-139), so the standalone reverb runs the split network with its pre-delay ring in rows (dattorro_block_v5, the form of
-    the network) and the chain its pre-delay rows (dt::PreRow).  Two blocks; clones bit-identical,
+    (verb.cpp:137-139), so the standalone reverb runs the split network over its pre-delay ring in
+    rows (dattorro_block_v5) and the chain its pre-delay rows (dt::PreRow).  Two blocks; clones bit-identical,
     sampled instances (workgroup edges included) bit-exact against the oracle."""
     import torch
     n = 65536
@@ -144,12 +144,48 @@ def test_full_size_random_predelay(cuda, pset, kind):
     e.close()
 
 
+def test_v5_large_ragged_long_run(cuda):
+    """dattorro_block_v5 for per-instance pre-delays at the sizes where uniform ones run v4, with a
+    partial last 64-instance group: n = CUs x 128 + 37 instances, pre-delays on row and window edges
+    (0, 1, 15..17, 31..33, 4800, 8191) among random ones, 18 calls of 256 frames and, between them, of
+    4 and 1,020 frames moving t0 off the 16-position rows.  Sampled instances, the partial group's
+    included, bit-exact against the oracle."""
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n = cus * 128 + 37
+    rng = np.random.default_rng(606)
+    from helpers import dt_params
+    p = dt_params(rng, n, 0.0)
+    edge = np.array([0, 1, 15, 16, 17, 31, 32, 33, 4800, 8191], np.float64) / 4800
+    p[0, :] = rng.uniform(0, 1, n).astype(np.float32)
+    p[0, -len(edge):] = edge.astype(np.float32)
+    p[0, :len(edge)] = edge.astype(np.float32)
+    e = _engine("dattorro", n)
+    e.set_params(0, p)
+    idx = np.unique(np.concatenate([np.arange(12), np.array([63, 64, 127, n // 2]), np.arange(n - 40, n)]))
+    d = O.Dattorro(len(idx))
+    for k, i in enumerate(idx):
+        for f in range(7):
+            d.set(k, f, float(p[f, i]))
+    from ol_dsp_amd.workload import noise_torch
+    ys, yrs = [], []
+    for F in [256] * 10 + [4, 1020] + [256] * 6:
+        x = torch.cat(noise_torch(len(ys) * 7, n, F, 2, cuda, blocks=1), 1)
+        y = e.process(x)
+        torch.cuda.synchronize()
+        ys.append(y[:, :, idx].cpu().numpy())
+        yrs.append(d.process(np.ascontiguousarray(x[:, :, idx].cpu().numpy())))
+    assert e.kernel_name == "dattorro_block_v5"
+    yg, yr = np.concatenate(ys, 1), np.concatenate(yrs, 1)
+    assert bits_equal(yg, yr), first_mismatch(yg, yr)
+    e.close()
+
+
 def test_reverb_network_switches_at_full_size(cuda):
     """configs[2]'s 65,536 reverbs: uniform pre-delays run dattorro_block_v4 (pre-delay ring
     position-major), per-instance pre-delays dattorro_block_v5 (ring in rows); each switch converts
     the ring's content (dattorro_pre_layout).  Uniform -> per instance -> uniform, two blocks each,
-    one 2,048-frame call at the end (v5 splits longer calls; v4 does not): sampled instances
-    bit-exact against the oracle over the whole run."""
+    then one 2,048-frame call: sampled instances bit-exact against the oracle over the whole run."""
     import torch
     from ol_dsp_amd.workload import instance_params
     n = 65536
