@@ -17,6 +17,8 @@
 #   abl:<workload>:<lib> A/B of the main build against <lib> (tools/ab.sh)
 #   occ:<workloads>:<ns> kernel time against instances (tools/occ_scale.sh), e.g. occ:dattorro,chain:16384,65536
 #   occe:<VAR=v>:<workloads>:<ns>  the same under an environment variable
+#   probe                tools/bw_probe (built here: hipcc ... -o tools/bw_probe), then the chorus's
+#                        bench line, on the same box
 set -u
 out=gpurun_out
 mkdir -p "$out"
@@ -94,6 +96,12 @@ for m in "$@"; do
       r=${m#occe:}; kv=${r%%:*}; r=${r#*:}; w=${r%%:*}; ns=${r#*:}
       step "occe_$(echo "$kv$w$ns" | tr -c 'a-zA-Z0-9_' '_')" 600 env "$kv" bash tools/occ_scale.sh "${w//,/ }" "${ns//,/ }"
       cat "$out/occe_$(echo "$kv$w$ns" | tr -c 'a-zA-Z0-9_' '_').log" ;;
+    probe)
+      step bw_probe 300 tools/bw_probe
+      cat "$out/bw_probe.log"
+      step bench_chorus_probe 300 python bench.py --workload chorus --also "" --steps 20 --cpu-seconds 0 --no-parity \
+          --full-json ""
+      cat "$out/bench_chorus_probe.log" ;;
     *) echo "unknown mode $m"; exit 2 ;;
   esac
 done
