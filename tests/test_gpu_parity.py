@@ -969,6 +969,29 @@ def test_chain_predelays_long_run_and_param_change(cuda):
     assert bits_equal(y, yr), first_mismatch(y, yr)
 
 
+def test_chain_predelays_at_the_row_window_edges(cuda):
+    """The chain's reverb role with 64-instance groups whose pre-delays all sit near the edges of its
+    row window (dattorro_stage.h rows_network: a chunk reads positions of its own chunk below 16,
+    its row prefetch two chunks ahead reaches the chunk below 48): all in 48..63, one at 47 among
+    48..63, 48..8191, a partial fourth group at 48; blocks that start chunks off a row (4, 132
+    frames) and end on partial chunks: bit-exact against the composed oracle."""
+    n = 200
+    rng = np.random.default_rng(77)
+    pc, pp, pd = chorus_params(rng, n), chorus_params(rng, n)[[0, 7]], dt_params(rng, n, 0.0)
+    smp = np.concatenate([rng.integers(48, 64, 64), rng.integers(48, 64, 64), rng.integers(48, 8192, 64),
+                          np.full(8, 48)]).astype(np.float64)
+    smp[0] = 48
+    smp[64 + 17] = 47
+    pd[0] = (smp + 0.5) / 4800                   # uint16(value * 4800) = smp
+    x = fast_noise(n, 6000, seed=77)
+    e = engine("chain", n)
+    e.set_params(0, np.concatenate([pc, pp, pd], 0))
+    y = run_gpu(e, x, [256, 4, 132, 1024, 36, 2048, 500, 2000], cuda)
+    c1, c2, d = _chain_oracle(n, pc, pp, pd)
+    yr = d.process(c2.process(c1.process(x)))
+    assert bits_equal(y, yr), first_mismatch(y, yr)
+
+
 # ------------------------------------------------------------------------------- fx rack
 def _fxrack_pair(n, p):
     e = engine("fxrack", n)
