@@ -72,7 +72,19 @@ __device__ __forceinline__ float unit24(uint32_t acc) {
     return (float)(acc >> 8) * 5.9604644775390625e-8f;   // exact: 24-bit fraction in [0,1)
 }
 
-__device__ __forceinline__ float lerp_pair(float x0, float x1, float fr) { return x0 + fr * (x1 - x0); }
+// The fp32 signal path in fused multiply-adds (spec v3, round 6; the oracle's
+// chorus_ref.c the same operations): interpolation, the crossfade sum, lores~ and the dry / wet mix
+__device__ __forceinline__ float lerp_pair(float x0, float x1, float fr) { return __builtin_fmaf(fr, x1 - x0, x0); }
+__device__ __forceinline__ float xfade(float tB, float gB, float tA, float gA) { return __builtin_fmaf(tB, gB, tA * gA); }
+// lores~ (TDF-II biquad): lp = b0 w + z1; z1 = (b1 w - a1 lp) + z2; z2 = b2 w - a2 lp
+__device__ __forceinline__ float lores_step(float wet, float b0, float b1, float b2, float a1, float a2, float &z1,
+                                            float &z2) {
+    const float lp = __builtin_fmaf(b0, wet, z1);
+    z1 = __builtin_fmaf(-a1, lp, b1 * wet) + z2;
+    z2 = __builtin_fmaf(-a2, lp, b2 * wet);
+    return lp;
+}
+__device__ __forceinline__ float dry_wet(float x, float dry, float lp, float mix) { return __builtin_fmaf(lp, mix, x * dry); }
 
 // a value of lane 2j (EVEN) or 2j+1 (odd) to both lanes of the pair: DPP quad_perm [0,0,2,2] / [1,1,3,3]
 __device__ __forceinline__ float pair_even(float v) {

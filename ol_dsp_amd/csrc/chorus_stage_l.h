@@ -490,7 +490,7 @@ struct ChStageL {
                 const float *qB = wP1 + (k & ~1) * kRow + (odd ? rB1 : rB0) * kRow;
                 const float tA = lerp_pair(qA[0], qA[-kRow], odd ? fA1 : fA0);
                 const float tB = lerp_pair(qB[0], qB[-kRow], odd ? fB1 : fB0);
-                psv[k] = tB * (odd ? gB1 : gB0) + tA * (odd ? gA1 : gA0);
+                psv[k] = xfade(tB, odd ? gB1 : gB0, tA, odd ? gA1 : gA0);
             }
             if (FULL) {
 #pragma unroll
@@ -536,7 +536,7 @@ struct ChStageL {
                     const int jw = k - (int)di - cur.sB;
                     tB = lerp_pair(wP1[jw * kRow], wP1[(jw - 1) * kRow], fr);
                 }
-                const float p = tB * gB + tA * gA;
+                const float p = xfade(tB, gB, tA, gA);
                 psv[k] = p;
                 float out = p;
                 if (FULL) {
@@ -544,10 +544,8 @@ struct ChStageL {
                     chorus_split(lfo_k, D, cmaxd, di, fr);
                     const int jw = k - (int)di - cur.sC;
                     const float wet = lerp_pair(wC[jw * kRow], wC[(jw - 1) * kRow], fr);
-                    const float lp = b0 * wet + z1;
-                    z1 = (b1 * wet - a1 * lp) + z2;
-                    z2 = b2 * wet - a2 * lp;
-                    out = x[k] * dry + lp * mix;
+                    const float lp = lores_step(wet, b0, b1, b2, a1, a2, z1, z2);
+                    out = dry_wet(x[k], dry, lp, mix);
                 }
                 if (OUT_LDS && FULL) yo[k] = out;
                 else sink(k, out);
@@ -585,10 +583,8 @@ struct ChStageL {
                     const bool odd = k & 1;
                     const float *qC = wC + (k & ~1) * kRow + (odd ? r1 : r0) * kRow;
                     const float wet = lerp_pair(qC[0], qC[-kRow], odd ? f1 : f0);
-                    const float lp = b0 * wet + z1;
-                    z1 = (b1 * wet - a1 * lp) + z2;
-                    z2 = b2 * wet - a2 * lp;
-                    sink(k, x[k] * dry + lp * mix);
+                    const float lp = lores_step(wet, b0, b1, b2, a1, a2, z1, z2);
+                    sink(k, dry_wet(x[k], dry, lp, mix));
                 }
             } else {
                 lfo_acc += (uint64_t)kChunk * lfo_inc;

@@ -98,13 +98,18 @@ hipError_t launch_dattorro_pre_layout(const DattorroArgs &a, float *tmp, bool to
 // compares in a fixed order, so the host (oracle) and gfx950 produce identical bits under
 // -ffp-contract=off.  |err| < 3e-7 (measured 1.8e-7; tests/test_oracle.py).
 // ----------------------------------------------------------------------------------------------
+// Horner in fused multiply-adds (spec v3, round 6: IEEE fusedMultiplyAdd, C fmaf on the host)
 OLFX_HD float cos_poly(float t2) {                 // cos(theta), t2 = theta^2, theta in [0, pi/2]
-    return 1.0f + t2 * (-0.4999993145465851f + t2 * (0.041663989424705505f +
-           t2 * (-0.001385592739097774f + t2 * 2.31943868129747e-05f)));
+    float r = __builtin_fmaf(2.31943868129747e-05f, t2, -0.001385592739097774f);
+    r = __builtin_fmaf(r, t2, 0.041663989424705505f);
+    r = __builtin_fmaf(r, t2, -0.4999993145465851f);
+    return __builtin_fmaf(r, t2, 1.0f);
 }
 OLFX_HD float sin_poly(float th, float t2) {       // sin(theta), theta in [0, pi/2]
-    return th * (1.0f + t2 * (-0.16666656732559204f + t2 * (0.008333017118275166f +
-           t2 * (-0.00019806614727713168f + t2 * 2.6000548132287804e-06f))));
+    float r = __builtin_fmaf(2.6000548132287804e-06f, t2, -0.00019806614727713168f);
+    r = __builtin_fmaf(r, t2, 0.008333017118275166f);
+    r = __builtin_fmaf(r, t2, -0.16666656732559204f);
+    return th * __builtin_fmaf(r, t2, 1.0f);
 }
 OLFX_HD float cos2pi(float x) {
     const float u = x - rintf(x);                  // exact, u in [-0.5, 0.5]

@@ -226,7 +226,7 @@ struct PStageS {
                 pitch_split(ph + 0x80000000u, wi, wf, pmaxu, di, fr);     // p1 = (p0 + 1/2) % 1
                 const float *qB = wP1 + (k + rB - (int)di) * kRow2;
                 const float2 tB = lerp2(*(const float2 *)qB, *(const float2 *)(qB - kRow2), fr);
-                psv[k] = make_float2(tB.x * gB + tA.x * gA, tB.y * gB + tA.y * gA);
+                psv[k] = make_float2(xfade(tB.x, gB, tA.x, gA), xfade(tB.y, gB, tA.y, gA));
                 ps_acc += ps_inc;
             }
             lfo_acc += (uint64_t)kChunk * lfo_inc;
@@ -264,7 +264,7 @@ struct PStageS {
                     const int jw = k - (int)di - cur.sB;
                     tB = lerp2(*(const float2 *)(wP1 + jw * kRow2), *(const float2 *)(wP1 + (jw - 1) * kRow2), fr);
                 }
-                psv[k] = make_float2(tB.x * gB + tA.x * gA, tB.y * gB + tA.y * gA);
+                psv[k] = make_float2(xfade(tB.x, gB, tA.x, gA), xfade(tB.y, gB, tA.y, gA));
             }
         }
         // x_c into the ring: 8 lanes per instance write its 128-B stereo run from the staging

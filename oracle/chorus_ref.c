@@ -23,7 +23,10 @@
  *     argument (oracle_win_gains), standing in for gen~'s cos;
  *   - gen Delay.read: linear interpolation, delay clamped to [1, size-2] (read before write);
  *     RNBO delay~: linear interpolation, delay clamped to [0, size-2] (write before read);
- *   - lores~: RBJ biquad low-pass (transposed direct form II), Q = 1/sqrt(2) + 20 q^3.
+ *   - lores~: RBJ biquad low-pass (transposed direct form II), Q = 1/sqrt(2) + 20 q^3;
+ *   - spec v3 (round 6): the fp32 signal path in fused multiply-adds -- the gain polynomials'
+ *     Horner steps, interpolation x0 + fr (x1 - x0), the crossfade t1 g1 + t0 g0, lores~ and the
+ *     dry / wet mix, each as written here (C99 fmaf, as the GPU's v_fma_f32).
  *
  * Dataflow (mono-chorus.rnbopat patchlines):
  *   in~1 -> gen~ pitchshift (:1119) -> delay~ (:1793) -> lores~ (:1808) -> *~ mix (:1302) -> +~ -> out~1
@@ -60,17 +63,22 @@ static float unit24(uint64_t acc) { return (float)((uint32_t)(acc >> 32) >> 8) *
 
 /* minimax polynomials on [0, pi/2] in theta^2 (degree 8 cos, degree 9 sin; Remez, coefficients
    rounded to float): the same operations in the same order as the GPU (spec choice, DESIGN.md
-   section 3) */
+   section 3); Horner in fused multiply-adds (spec v3, round 6: C99 fmaf, correctly rounded, as
+   v_fma_f32) */
 static float cos_poly(float t2)
 {
-    return 1.0f + t2 * (-0.4999993145465851f + t2 * (0.041663989424705505f +
-           t2 * (-0.001385592739097774f + t2 * 2.31943868129747e-05f)));
+    float r = fmaf(2.31943868129747e-05f, t2, -0.001385592739097774f);
+    r = fmaf(r, t2, 0.041663989424705505f);
+    r = fmaf(r, t2, -0.4999993145465851f);
+    return fmaf(r, t2, 1.0f);
 }
 
 static float sin_poly(float th, float t2)
 {
-    return th * (1.0f + t2 * (-0.16666656732559204f + t2 * (0.008333017118275166f +
-           t2 * (-0.00019806614727713168f + t2 * 2.6000548132287804e-06f))));
+    float r = fmaf(2.6000548132287804e-06f, t2, -0.00019806614727713168f);
+    r = fmaf(r, t2, 0.008333017118275166f);
+    r = fmaf(r, t2, -0.16666656732559204f);
+    return th * fmaf(r, t2, 1.0f);
 }
 
 /* cos(2 pi x): reduce to b in [0, 1/4] (exact), then cos_poly */
@@ -199,12 +207,13 @@ int oracle_chorus_set(oracle_chorus *o, int inst, int field, float value)
     return 0;
 }
 
-/* linear interpolation at delay di + fr (gen Delay.read / delay~): x0 + fr (x1 - x0) */
+/* linear interpolation at delay di + fr (gen Delay.read / delay~): x0 + fr (x1 - x0), one fused
+   multiply-add (spec v3) */
 static float read_split(const float *ring, uint32_t mask, uint32_t w, uint32_t di, float fr)
 {
     const float x0 = ring[(w - di) & mask];
     const float x1 = ring[(w - di - 1u) & mask];
-    return x0 + fr * (x1 - x0);
+    return fmaf(fr, x1 - x0, x0);
 }
 
 /* the pitch-shifter's tap delay p W, p = ph / 2^32 (the phasor's high word), W = Wfix / 2^32:
@@ -273,15 +282,15 @@ static void chorus_frame(const oracle_chorus *o, const chcoef_t *k, chstate_t *s
     for (int c = 0; c < 2; c++) {
         const float t0 = read_split(s->pring[c], pmask, w, di0, fr0);
         const float t1 = read_split(s->pring[c], pmask, w, di1, fr1);
-        const float ps = t1 * g1 + t0 * g0;
+        const float ps = fmaf(t1, g1, t0 * g0);                        /* spec v3 */
         s->pring[c][w & pmask] = x[c];
         if (o->mode == 0) {
             s->cring[c][w & cmask] = ps;
             const float wet = read_split(s->cring[c], cmask, w, cdi, cfr);
-            const float lp = k->b0 * wet + s->z1[c];
-            s->z1[c] = (k->b1 * wet - k->a1 * lp) + s->z2[c];
-            s->z2[c] = k->b2 * wet - k->a2 * lp;
-            y[c] = x[c] * k->dry + lp * k->mix;
+            const float lp = fmaf(k->b0, wet, s->z1[c]);                /* lores~, spec v3 */
+            s->z1[c] = fmaf(-k->a1, lp, k->b1 * wet) + s->z2[c];
+            s->z2[c] = fmaf(-k->a2, lp, k->b2 * wet);
+            y[c] = fmaf(lp, k->mix, x[c] * k->dry);
         } else {
             y[c] = ps;
         }

@@ -196,7 +196,8 @@ def test_chorus_deviation_by_stage(golden):
     the spec computes it, everything else in double; oracle/chorus_ref_f64.c).  Round 3's delays
     (24-bit phase, fp32 p W and D cos + D) were the whole of it: the chorus delay 1.6e-4, the pitch
     delay 6e-5 (chorus) / 1.3e-4 (pitch-shift); spec v2's delays (fixed-point p W, double D cos + D)
-    bring each below 1e-6, and lores~'s fp32 state (6e-6) is what remains."""
+    bring each below 1e-6, and lores~'s fp32 state (6e-6) is what remains; spec v3's fused
+    multiply-adds (round 6) take the whole to 5.8e-6."""
     g = golden["chorus"]
     p = np.asarray(g["params"], np.float32)
     x = noise_block(g["n"], g["frames"], g["input_base"])
@@ -209,13 +210,16 @@ def test_chorus_deviation_by_stage(golden):
     # all stages as round 3 computed them == round 3's spec (the emulation is faithful: 1.62e-4)
     r3 = _dev(_c64(g, 2 | (127 << 2), p).process(x), ref)[0]
     assert 1.5e-4 < r3 < 1.8e-4
-    # spec v2: the fp32 stages with the precise delays == the spec oracle's deviation
+    # spec v2: the fp32 stages (unfused, as emulated here) with the precise delays; the spec oracle
+    # is v3 (round 6: the same stages in fused multiply-adds), whose deviation is no larger
     v2 = _dev(_c64(g, 2 | (((127 & ~(1 | 8)) | _FIX_PDELAY | _DBL_CDELAY) << 2), p).process(x), ref)[0]
     a = O.Chorus(g["n"], 48000.0, 0)
     for i in range(g["n"]):
         for f in range(8):
             a.set(i, f, float(p[f, i]))
-    assert abs(v2 - _dev(a.process(x), ref)[0]) <= 0.05 * v2
+    v3 = _dev(a.process(x), ref)[0]
+    print(f"spec v2 (unfused) {v2:.3g}, spec v3 (the oracle, fused) {v3:.3g}")
+    assert 0.5 * v2 <= v3 <= v2
     assert v2 < 1e-5
 
 
