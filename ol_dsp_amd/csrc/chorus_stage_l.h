@@ -570,11 +570,19 @@ struct ChStageL {
                 const int chC = (int)ch - cur.sC;
                 int r0 = 0, r1 = 0;
                 float f0 = 0.f, f1 = 0.f;
+                uint32_t dn = 0;                      // the next pair's split, computed with this one's
+                float fn = 0.f;
 #pragma unroll
                 for (int k = 0; k < kChunk; ++k) {
                     if ((k & 1) == 0) {
                         uint32_t di; float fr;
-                        chorus_split(lfo_acc + (ch ? lfo_inc : 0ull) + lfo_off, D, cmaxd, di, fr);
+                        if ((k & 3) == 0) {
+                            const uint64_t p = lfo_acc + (ch ? lfo_inc : 0ull) + lfo_off;
+                            chorus_split2(p, p + 2ull * lfo_inc, D, cmaxd, di, fr, dn, fn);
+                        } else {
+                            di = dn;
+                            fr = fn;
+                        }
                         const int rc = chC - (int)di;
                         r0 = pair_even_i(rc); r1 = pair_odd_i(rc);
                         f0 = pair_even(fr); f1 = pair_odd(fr);

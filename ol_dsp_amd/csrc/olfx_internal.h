@@ -251,6 +251,37 @@ OLFX_HD void chorus_split(uint64_t phase, double D, double cmax, uint32_t &di, f
     di = (uint32_t)d;
     fr = (float)(d - (double)di);                  // the subtraction is exact
 }
+// two chorus_splits with their Horner chains interleaved (each step's operand is two instructions
+// back: no dependent double-precision pair back to back), the same operations per phase
+OLFX_HD void chorus_split2(uint64_t ph0, uint64_t ph1, double D, double cmax, uint32_t &di0, float &fr0,
+                           uint32_t &di1, float &fr1) {
+    const int32_t s0 = (int32_t)(uint32_t)(ph0 >> 32), s1 = (int32_t)(uint32_t)(ph1 >> 32);
+    const uint32_t l0 = (uint32_t)ph0 >> 11, l1 = (uint32_t)ph1 >> 11;
+    const double u0 = __builtin_fma((double)s0, 2.3283064365386963e-10, (double)l0 * 1.1102230246251565e-16);
+    const double u1 = __builtin_fma((double)s1, 2.3283064365386963e-10, (double)l1 * 1.1102230246251565e-16);
+    const double a0 = __builtin_fabs(u0), a1 = __builtin_fabs(u1);
+    const bool h0 = a0 > 0.25, h1 = a1 > 0.25;
+    const double b0 = h0 ? 0.5 - a0 : a0, b1 = h1 ? 0.5 - a1 : a1;
+    const double th0 = b0 * 6.283185307179586, th1 = b1 * 6.283185307179586;
+    const double t0 = th0 * th0, t1 = th1 * th1;
+    double r0 = -1.5619206968586225e-16, r1 = -1.5619206968586225e-16;
+    r0 = fma_dc(r0, t0, 4.779477332387385e-14);    r1 = fma_dc(r1, t1, 4.779477332387385e-14);
+    r0 = fma_dc(r0, t0, -1.1470745597729725e-11);  r1 = fma_dc(r1, t1, -1.1470745597729725e-11);
+    r0 = fma_dc(r0, t0, 2.08767569878681e-09);     r1 = fma_dc(r1, t1, 2.08767569878681e-09);
+    r0 = fma_dc(r0, t0, -2.755731922398589e-07);   r1 = fma_dc(r1, t1, -2.755731922398589e-07);
+    r0 = fma_dc(r0, t0, 2.48015873015873e-05);     r1 = fma_dc(r1, t1, 2.48015873015873e-05);
+    r0 = fma_dc(r0, t0, -0.001388888888888889);    r1 = fma_dc(r1, t1, -0.001388888888888889);
+    r0 = fma_dc(r0, t0, 0.041666666666666664);     r1 = fma_dc(r1, t1, 0.041666666666666664);
+    r0 = __builtin_fma(r0, t0, -0.5);              r1 = __builtin_fma(r1, t1, -0.5);
+    r0 = __builtin_fma(r0, t0, 1.0);               r1 = __builtin_fma(r1, t1, 1.0);
+    const double c0 = h0 ? -r0 : r0, c1 = h1 ? -r1 : r1;
+    const double d0 = __builtin_fmin(__builtin_fmax(__builtin_fma(c0, D, D), 0.0), cmax);
+    const double d1 = __builtin_fmin(__builtin_fmax(__builtin_fma(c1, D, D), 0.0), cmax);
+    di0 = (uint32_t)d0;
+    di1 = (uint32_t)d1;
+    fr0 = (float)(d0 - (double)di0);
+    fr1 = (float)(d1 - (double)di1);
+}
 
 struct ChorusArgs {
     float *pitch_ring;          // [n][psize][2]  (stereo-interleaved: L and R share every tap)
