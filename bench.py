@@ -812,6 +812,27 @@ def compact_leg(r: dict) -> dict:
     return c
 
 
+def _box_copy_rate(torch, dev):
+    """The box's device-to-device copy rate (2 GiB, read + write bytes), untimed and after the legs: a
+    reference for comparing lines from different boxes, whose HBM rates differ."""
+    try:
+        a = torch.empty(1 << 29, dtype=torch.float32, device=dev)
+        b = torch.empty_like(a)
+        for _ in range(3):
+            b.copy_(a)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            b.copy_(a)
+        e1.record()
+        torch.cuda.synchronize()
+        gbs = 2 * a.numel() * 4 * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+        del a, b
+        return {"copy_gbs": _r(gbs, 1), "what": "torch device copy of 2 GiB, read + write bytes, after the legs"}
+    except Exception as ex:       # informational only
+        return {"copy_gbs": None, "error": str(ex)[:80]}
+
+
 def main():
     args = parse()
     from ol_dsp_amd.dist import env_ranks, launch_ranks, self_command
@@ -865,6 +886,7 @@ def main():
             leg.timed(K)
     results = [leg.finish() for leg in legs]
     main_res = results[0]
+    box = _box_copy_rate(torch, dev) if rank == 0 and not args.stub else None
     also_res = {key: res for (_, _, _, key), res in zip(specs[1:], results[1:])}
     cpu_jobs, cpu_reuse, parity_jobs = [], [], []
     if rank == 0 and not args.stub:
@@ -930,6 +952,8 @@ def main():
         res["output_checksum"] = main_res["output_checksum"]
         if "mix" in main_res:
             res["mix"] = main_res["mix"]
+        if box:
+            res["box"] = box
         full = dict(res, roofline=rf, cpu_baseline=cb, parity=main_res.get("parity"))
         if world == 1 and args.cpu_seconds > 0 and args.workload == "chorus" and not args.stub:
             c1 = cpu_c1(args.sample_rate, args.block)
